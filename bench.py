@@ -1,0 +1,224 @@
+"""Benchmark: GBLUP fitness evals/s on BASELINE config 2 (2000 animals x 50k SNPs,
+panel k = 1000, DE population 256 per GPU), one process per GPU.
+
+A "step" is one generation's fitness evaluation of the population: every
+individual's selected-SNP gather, exact-integer GRM block on int8 MFMA, fp64
+tile Cholesky of (K_TT + lambda I), back substitution, prediction and Pearson
+fitness, plus (N > 1) the RCCL all-gather of the fp64 fitness vector.  Inputs
+(genotypes, split, the population's decoded index sets) are resident in HBM
+before timing starts.  Weak scaling: every rank evaluates its own 256
+individuals.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (n animals, P SNPs, panel k, pop per GPU, n_train, n_valid)
+    "config2": (2000, 50_000, 1000, 256, 1280, 320),
+    "config1": (200, 1000, 100, 32, 128, 32),
+    "config4": (5000, 600_000, 5000, 256, 3200, 800),
+}
+
+# gfx950 peaks (MI355X_MICROARCH.md chip table; fp64 and int8 dense from the AMD MI355X spec sheet)
+PEAKS = {
+    "fp64_mfma_tflops": 78.6,
+    "int8_mfma_tops": 5033.0,
+    "hbm_gbs": 8000.0,
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--pop", type=int, default=None, help="individuals per GPU (default: the config's)")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--h2", type=float, default=0.4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target wall time of the CPU baseline sample")
+    ap.add_argument("--profile-json", default=None, help="write the per-kernel-class event timing here")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def make_workload(cfg, seed, rank, pop):
+    n, P, k, _, nT, nV = cfg
+    rng = np.random.default_rng(seed)
+    maf = rng.uniform(0.05, 0.5, size=P)                  # SURVEY.md section 8d synthetic panel
+    geno = rng.binomial(2, maf, size=(n, P)).astype(np.int8)
+    pheno = rng.standard_normal(n)
+    perm = np.random.default_rng(seed + 1).permutation(n)
+    T, V = perm[:nT], perm[nT:nT + nV]
+    keys = np.random.default_rng(seed + 100 + rank).uniform(size=(pop, P))
+    genomes = np.argsort(keys, axis=1)[:, -k:]            # RandomKeyIndividual decode (individual.py:154-156)
+    return geno, pheno, T, V, genomes
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+_CPU = {}
+
+
+def _cpu_init():
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)
+
+
+def _cpu_eval(i):
+    from oracle.blup_oracle import blup
+    d = _CPU
+    return blup(d["genomes"][i % len(d["genomes"])], d["T"], d["V"], d["data"], d["pheno"], d["h2"])
+
+
+def cpu_baseline(geno, pheno, T, V, genomes, h2, target_s):
+    """The oracle's numpy port of the reference evaluator (same blup dispatch, float64
+    genotypes, one single-threaded worker process per core; cf. generate_sbs.py:25
+    OMP_NUM_THREADS=1), timed on a bounded sample of the same workload."""
+    import multiprocessing as mp
+    from threadpoolctl import threadpool_limits
+    from oracle.blup_oracle import blup
+
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    _CPU.update(data=geno.astype(np.float64), pheno=pheno, T=T, V=V, genomes=genomes, h2=h2)
+    with threadpool_limits(1):
+        t0 = time.perf_counter()
+        for i in range(2):
+            blup(genomes[i], T, V, _CPU["data"], pheno, h2)
+        per_eval = (time.perf_counter() - t0) / 2
+    count = int(max(cores, min(20_000, target_s * cores / max(per_eval, 1e-6))))
+    ctx = mp.get_context("fork")
+    with ctx.Pool(cores, initializer=_cpu_init) as pool:
+        pool.map(_cpu_eval, range(cores))        # warm the workers
+        t0 = time.perf_counter()
+        pool.map(_cpu_eval, range(count), chunksize=max(1, count // (4 * cores)))
+        dt = time.perf_counter() - t0
+    _CPU.clear()
+    return {"value": count / dt, "unit": "evals/s", "cores": cores, "kind": "port",
+            "sample": f"{count} evaluations of the config workload (k={genomes.shape[1]}) by the numpy oracle "
+                      f"port of BlupParallelEvaluator.blup, {cores} single-threaded worker processes, {dt:.1f} s"}
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg = CONFIGS[args.config]
+    n, P, k, pop_default, nT, nV = cfg
+    pop = args.pop or pop_default
+
+    geno, pheno, T, V, genomes = make_workload(cfg, args.seed, rank, pop)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(geno, pheno, T, V, genomes, args.h2, args.cpu_seconds)
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from tblup_amd.engine import GpuBlupEngine, concat_genomes
+
+    eng = GpuBlupEngine(geno, pheno, device=local_rank)
+    sid = eng.split_id(T, V)
+    idx, off = concat_genomes(list(genomes))
+    d_idx = torch.from_numpy(idx).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    d_fit = torch.empty(pop, dtype=torch.float64, device="cuda")
+    full = torch.empty(pop * world, dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step():
+        eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, args.h2, d_fit.data_ptr(),
+                            stream_ptr=stream.cuda_stream)
+        if world > 1:
+            dist.all_gather_into_tensor(full, d_fit)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.reset_profile()
+    eng.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    prof = eng.profile()
+    fit = d_fit.cpu().numpy()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_evals = pop * world * args.steps
+    value = total_evals / elapsed
+
+    # roofline of the dominant kernel class, from live HIP-event timing over the timed region
+    dom = max(prof, key=lambda c: prof[c]["ms"])
+    pd = prof[dom]
+    if dom in ("chol_diag", "chol_offdiag"):
+        bound, peak, unit, achieved = "mfma", PEAKS["fp64_mfma_tflops"], "TFLOP/s", pd["flops"] / (pd["ms"] * 1e-3) / 1e12
+    elif dom == "grm":
+        bound, peak, unit, achieved = "mfma", PEAKS["int8_mfma_tops"], "TOP/s", pd["flops"] / (pd["ms"] * 1e-3) / 1e12
+    else:
+        bound, peak, unit, achieved = "hbm", PEAKS["hbm_gbs"], "GB/s", pd["bytes"] / (pd["ms"] * 1e-3) / 1e9
+    traffic = None
+    if os.path.isfile(args.pmc_json):
+        try:
+            pmc = json.load(open(args.pmc_json))
+            if pmc.get("config") == args.config and dom in pmc.get("per_launch_bytes", {}):
+                traffic = pmc["per_launch_bytes"][dom]
+        except (ValueError, OSError):
+            traffic = None
+    roofline = {"bound": bound, "kernel": dom, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "launches": pd["launches"], "avg_launch_ms": round(pd["ms"] / max(pd["launches"], 1), 4)}
+    step_ms = {c: round(prof[c]["ms"] / args.steps, 4) for c in prof}
+
+    if args.profile_json and rank == 0:
+        with open(args.profile_json, "w") as f:
+            json.dump({"config": args.config, "steps": args.steps, "profile": prof, "per_step_ms": step_ms,
+                       "elapsed_s": elapsed}, f, indent=1)
+    if rank == 0:
+        line = {
+            "metric": "GBLUP fitness evals/sec (whole node), 2k x 50k SNP, DE pop=256 per GPU",
+            "value": round(value, 2), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int8 GRM (exact int32 accumulate) + f64 Cholesky/solve",
+            "data": "synthetic (Binomial(2, U(0.05,0.5)) genotypes, N(0,1) phenotype, RandomKey individuals)",
+            "config": {"workload": f"{args.config}: {n} animals x {P} SNPs, panel k={k}, pop {pop} per GPU, "
+                                   f"n_train={nT}, n_valid={nV}, h2={args.h2}",
+                       "parallelism": f"population sharded over {world} GPU(s), RCCL fitness all-gather"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_ms_per_step": step_ms,
+            "fitness_checksum": float(np.nansum(fit)),
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,139 @@
+/*
+ * tblup_gpu.h — C ABI of the MI355X GBLUP fitness evaluator (libtblup_gpu.so).
+ *
+ * Drop-in boundary for the reference's fitness-evaluation hot path
+ * (ianwhale/tblup).  The reference has no native FFI; its boundary is the
+ * Python evaluator plugin API, whose compute leg is the multiprocessing
+ * worker pool:
+ *
+ *   ParallelEvaluator.__enter__/__exit__   tblup/evaluator.py:120-135  -> tblup_ctx_create / tblup_ctx_destroy
+ *   BlupParallelEvaluator.__init__ split   tblup/evaluator.py:188-203  -> tblup_set_split
+ *   worker() + enqueue() + blup()          tblup/evaluator.py:205-263  -> tblup_eval_batch
+ *     gblup()    evaluator.py:265-286   (branch TBLUP_BRANCH_GBLUP)
+ *     snp_blup() evaluator.py:288-314   (branch TBLUP_BRANCH_SNP)
+ *     dispatch   evaluator.py:257       (branch TBLUP_BRANCH_AUTO: k > n -> gblup)
+ *   make_grm()                             tblup/utils.py:7-18          -> tblup_debug_grm (block readback)
+ *
+ * The ctypes binding a maintainer adds on the reference side is shown in
+ * INTEGRATION.md.  All functions return 0 on success and a negative status
+ * otherwise; tblup_last_error() returns a thread-local message.  Host buffers
+ * are borrowed for the duration of the call only.  A NaN fitness (constant
+ * prediction, degenerate panel) is returned as NaN, never raised.
+ */
+#ifndef TBLUP_GPU_H
+#define TBLUP_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tblup_ctx tblup_ctx;
+
+enum {
+  TBLUP_OK = 0,
+  TBLUP_ERR_ARG = -1,      /* invalid argument (shape, index range, unknown split) */
+  TBLUP_ERR_HIP = -2,      /* HIP runtime error (no device, launch or copy failure) */
+  TBLUP_ERR_OOM = -3,      /* device allocation failed */
+  TBLUP_ERR_STATE = -4     /* call out of order */
+};
+
+enum {
+  TBLUP_BRANCH_AUTO = 0,   /* evaluator.py:257: len(indices) > n_animals -> GBLUP else SNP-BLUP */
+  TBLUP_BRANCH_GBLUP = 1,  /* evaluator.py:265-286: p over all n animals, no phenotype centring */
+  TBLUP_BRANCH_SNP = 2     /* evaluator.py:288-314: p over train animals, ridge intercept = mean(y_T) */
+};
+
+enum {
+  TBLUP_LAYOUT_ANIMAL_MAJOR = 0, /* n_animals x n_snps, row-major (the .npy the reference loads) */
+  TBLUP_LAYOUT_SNP_MAJOR = 1     /* n_snps x n_animals, row-major */
+};
+
+/* Last error message of the calling thread ("" if none). */
+const char* tblup_last_error(void);
+
+/* Library version string. */
+const char* tblup_version(void);
+
+/* Number of visible HIP devices (0 when none). */
+int tblup_device_count(int* out_count);
+
+/*
+ * Create a context on HIP device `device`: uploads the {0,1,2} genotype
+ * matrix (int8) and the phenotype vector (float64, length n_animals).
+ * Replaces the per-worker np.load of evaluator.py:215-216.
+ */
+int tblup_ctx_create(const int8_t* geno, int64_t n_animals, int64_t n_snps, int layout,
+                     const double* pheno, int device, tblup_ctx** out_ctx);
+
+int tblup_ctx_destroy(tblup_ctx* ctx);
+
+/*
+ * Register a train/validation split under `split_id` (replacing any split
+ * with that id).  train/valid are animal row ids in the reference's order
+ * (evaluator.py:196-203, 316-322, 485-491, 555-561, 413).
+ */
+int tblup_set_split(tblup_ctx* ctx, int split_id, const int64_t* train, int64_t n_train,
+                    const int64_t* valid, int64_t n_valid);
+
+int tblup_drop_split(tblup_ctx* ctx, int split_id);
+
+/*
+ * Evaluate `batch` individuals (one blup() call each, evaluator.py:244-314).
+ *   idx      : concatenated selected SNP column indices (duplicates allowed,
+ *              any order), length offsets[batch]
+ *   offsets  : batch+1 prefix offsets into idx; an individual may have k >= 1
+ *   h2       : heritability, lambda = (1-h2)/h2
+ *   branch   : TBLUP_BRANCH_*
+ *   fitness  : out, batch doubles, |pearson(EBV_V, y_V)| (NaN when undefined)
+ *   ebv      : optional out (may be NULL), batch x n_valid predicted breeding values
+ * Synchronous; host pointers.
+ */
+int tblup_eval_batch(tblup_ctx* ctx, int split_id, const int64_t* idx, const int64_t* offsets,
+                     int64_t batch, double h2, int branch, double* fitness, double* ebv);
+
+/*
+ * Same computation on device-resident inputs/outputs, enqueued on `stream`
+ * (a hipStream_t; NULL = the context's own stream) without synchronising.
+ * d_idx / d_offsets / d_fitness / d_ebv are device pointers on the
+ * context's device; h_offsets is the same batch+1 offsets on the host (used
+ * for workspace sizing).  The workspace is shared with other calls on the
+ * context: calls must be serialised on one stream.  Indices are NOT range-checked here
+ * (out-of-range ids are clamped in-kernel); use tblup_eval_batch for checked
+ * input.
+ */
+int tblup_eval_batch_device(tblup_ctx* ctx, int split_id, const int64_t* d_idx,
+                            const int64_t* d_offsets, const int64_t* h_offsets, int64_t batch,
+                            double h2, int branch, double* d_fitness, double* d_ebv, void* stream);
+
+/*
+ * Per-kernel-class timing with HIP events on the launch stream.
+ * tblup_set_profiling(ctx, 1) enables recording; tblup_get_profile returns
+ * accumulated milliseconds, launch counts and algorithmic flops per class
+ * since the last reset (classes: 0 stats, 1 gather, 2 grm, 3 chol_diag,
+ * 4 chol_offdiag, 5 solve).  Arrays must hold TBLUP_N_KCLASS entries.
+ */
+#define TBLUP_N_KCLASS 6
+int tblup_set_profiling(tblup_ctx* ctx, int enable);
+int tblup_get_profile(tblup_ctx* ctx, double* ms, int64_t* launches, double* flops, double* bytes);
+int tblup_reset_profile(tblup_ctx* ctx);
+
+/*
+ * Debug / parity readback for ONE individual: runs the pipeline up to
+ * `stage` (1 = GRM block K_{RT} incl. lambda on the TT diagonal,
+ * 2 = after the tile Cholesky: L in the TT lower triangle) and copies the
+ * (n_train + n_valid) x n_train block to `out` (row-major, R = train then
+ * valid order), plus z = L^{-1}(y_T - mu) to `z_out` (may be NULL).
+ */
+int tblup_debug_grm(tblup_ctx* ctx, int split_id, const int64_t* idx, int64_t k, double h2,
+                    int branch, int stage, double* out, double* z_out);
+
+/* Device memory currently held by the context (bytes). */
+int tblup_mem_info(tblup_ctx* ctx, int64_t* bytes_in_use);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TBLUP_GPU_H */

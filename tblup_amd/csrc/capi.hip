@@ -1,0 +1,587 @@
+// C ABI of libtblup_gpu.so (see include/tblup_gpu.h): context, splits, workspace,
+// batched evaluation pipeline and per-kernel-class event timing.
+//
+// Pipeline per chunk of B individuals (one HIP stream, no host syncs inside):
+//   k_indiv_stats -> k_gather -> k_grm -> for J: (k_chol_diag, k_chol_offdiag) -> k_solve
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/tblup_gpu.h"
+#include "tblup_internal.h"
+
+using namespace tblup;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                                      \
+  do {                                                                                                    \
+    hipError_t e_ = (expr);                                                                               \
+    if (e_ != hipSuccess) return fail(TBLUP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+struct Split {
+  int64_t nT = 0, nV = 0, nTp = 0, nVp = 0, nRp = 0;
+  double meanyT = 0.0;
+  DevBuf geno, colsumT, yT, yV;
+};
+
+enum { KC_STATS = 0, KC_GATHER, KC_GRM, KC_DIAG, KC_OFFDIAG, KC_SOLVE };
+
+struct EventPair {
+  int cls;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct tblup_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t n = 0, P = 0;
+  DevBuf geno_sm, colsum_all, scratch;
+  std::vector<double> pheno;
+  std::map<int, std::unique_ptr<Split>> splits;
+  DevBuf ws;
+  size_t budget = 0;
+  // profiling
+  bool profiling = false;
+  std::vector<EventPair> pending;
+  std::vector<hipEvent_t> event_pool;
+  double ms[TBLUP_N_KCLASS] = {0};
+  int64_t launches[TBLUP_N_KCLASS] = {0};
+  double flops[TBLUP_N_KCLASS] = {0};
+  double bytes[TBLUP_N_KCLASS] = {0};
+  int64_t mem_in_use = 0;
+};
+
+namespace {
+
+int dev_alloc(tblup_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return 0;
+  if (b.p) c->mem_in_use -= (int64_t)b.bytes;
+  b.release();
+  if (bytes == 0) return 0;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    return fail(TBLUP_ERR_OOM, std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  }
+  b.bytes = bytes;
+  c->mem_in_use += (int64_t)bytes;
+  return 0;
+}
+
+void dev_free(tblup_ctx* c, DevBuf& b) {
+  if (b.p) c->mem_in_use -= (int64_t)b.bytes;
+  b.release();
+}
+
+hipEvent_t get_event(tblup_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int drain_events(tblup_ctx* c) {
+  for (auto& p : c->pending) {
+    HIPCHK(hipEventSynchronize(p.b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+    c->ms[p.cls] += ms;
+    c->event_pool.push_back(p.a);
+    c->event_pool.push_back(p.b);
+  }
+  c->pending.clear();
+  return 0;
+}
+
+// Launch wrapper: records an event pair around the launch when profiling.
+template <typename F>
+int timed(tblup_ctx* c, hipStream_t s, int cls, double flops, double bytes, F&& launch) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->profiling) {
+    a = get_event(c);
+    b = get_event(c);
+    if (a) (void)hipEventRecord(a, s);
+  }
+  hipError_t e = launch();
+  if (e != hipSuccess) return fail(TBLUP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+  if (c->profiling && a && b) {
+    (void)hipEventRecord(b, s);
+    c->pending.push_back({cls, a, b});
+    c->launches[cls] += 1;
+    c->flops[cls] += flops;
+    c->bytes[cls] += bytes;
+  }
+  return 0;
+}
+
+struct Carve {
+  char* base;
+  size_t used = 0;
+  template <typename T>
+  T* take(size_t count) {
+    used = round_up((int64_t)used, 256);
+    T* p = reinterpret_cast<T*>(base + used);
+    used += count * sizeof(T);
+    return p;
+  }
+};
+
+size_t chunk_bytes(const EvalDims& d, int64_t B, int64_t max_kblk, int64_t sum_k, bool with_ebv) {
+  size_t s = 0;
+  auto add = [&](size_t x) { s = (size_t)round_up((int64_t)(s + x), 256); };
+  add((size_t)B * max_kblk * d.nRp * KBLK);                     // panel
+  add((size_t)B * d.nRp * 8);                                   // u
+  add((size_t)B * 64);                                          // scal
+  add((size_t)B * d.nRp * d.nTp * 8);                           // K
+  add((size_t)B * d.NT * TILE * TILE * 8);                      // Dinv
+  add((size_t)B * d.nTp * 8);                                   // z
+  add((size_t)B * 8);                                           // fitness
+  add(with_ebv ? (size_t)B * d.nV * 8 : 0);                     // ebv
+  add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
+  return s + 4096;
+}
+
+EvalDims dims_of(const tblup_ctx* c, const Split& sp) {
+  EvalDims d;
+  d.n = c->n;
+  d.P = c->P;
+  d.nT = sp.nT;
+  d.nV = sp.nV;
+  d.nTp = sp.nTp;
+  d.nVp = sp.nVp;
+  d.nRp = sp.nRp;
+  d.NT = (int)(sp.nTp / TILE);
+  d.NR = (int)(sp.nRp / TILE);
+  return d;
+}
+
+// Enqueue the full pipeline for one chunk whose idx/off already sit in device memory.
+int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, const int64_t* d_idx,
+              const int64_t* d_off, const int64_t* h_off, int64_t B, double h2,
+              int branch, Carve& cv, double* d_fit, double* d_ebv, int stop_stage, double** K_out,
+              double** z_out) {
+  int64_t max_kblk = 0;
+  double grm_flops = 0.0, gather_bytes = 0.0, stats_bytes = 0.0;
+  const double tri = (double)d.nT * (d.nT + 1) / 2.0 + (double)d.nV * d.nT;
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t k = h_off[b + 1] - h_off[b];
+    max_kblk = std::max(max_kblk, (k + KBLK - 1) / KBLK);
+    grm_flops += 2.0 * (double)k * tri;
+    gather_bytes += 2.0 * (double)k * (double)(d.nT + d.nV);
+    stats_bytes += 16.0 * (double)k;
+  }
+  const int64_t pstride = max_kblk * d.nRp * KBLK;
+  int8_t* panel = cv.take<int8_t>((size_t)B * pstride);
+  double* u = cv.take<double>((size_t)B * d.nRp);
+  double* scal = cv.take<double>((size_t)B * 8);
+  double* K = cv.take<double>((size_t)B * d.nRp * d.nTp);
+  double* Dinv = cv.take<double>((size_t)B * d.NT * TILE * TILE);
+  double* z = cv.take<double>((size_t)B * d.nTp);
+  const int32_t* csT = (const int32_t*)sp.colsumT.p;
+  const int32_t* csA = (const int32_t*)c->colsum_all.p;
+  int rc;
+  rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
+    return launch_indiv_stats(d_idx, d_off, B, csT, csA, d, branch, sp.meanyT, h2, scal, s);
+  });
+  if (rc) return rc;
+  rc = timed(c, s, KC_GATHER, 0.0, gather_bytes, [&] {
+    return launch_gather((const int8_t*)sp.geno.p, d_idx, d_off, pstride, B, csT, csA, scal, d, panel, u, s);
+  });
+  if (rc) return rc;
+  const double kbytes = (double)B * ((double)d.nT * d.nT / 2.0 + (double)d.nV * d.nT) * 8.0;
+  rc = timed(c, s, KC_GRM, grm_flops, kbytes + gather_bytes / 2.0,
+             [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
+  if (rc) return rc;
+  if (K_out) *K_out = K;
+  if (z_out) *z_out = z;
+  if (stop_stage == 1) return 0;
+  const double T3 = (double)TILE * TILE * TILE;
+  for (int J = 0; J < d.NT; ++J) {
+    const double jt = (double)J;
+    // algorithmic flops: SYRK update of the diagonal tile + potrf + trtri (+ forward-subst GEMV)
+    const double fd = (double)B * (T3 * jt + T3 / 3.0 + T3 / 3.0 + 2.0 * TILE * TILE * jt);
+    const double bd = (double)B * (TILE * TILE * jt * 8.0 + 2.0 * TILE * TILE * 8.0);
+    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(K, d, B, J, Dinv, z, (const double*)sp.yT.p, scal, s); });
+    if (rc) return rc;
+    const int nI = d.NT - J - 1;
+    if (nI > 0) {
+      // algorithmic flops per tile: GEMM update 2*128^3*J + triangular solve 128^3
+      const double fo = (double)B * nI * (2.0 * T3 * jt + T3);
+      const double bo = (double)B * nI * (TILE * TILE * jt * 8.0 + 2.0 * TILE * TILE * 8.0) +
+                        (double)B * TILE * TILE * jt * 8.0;
+      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(K, d, B, J, Dinv, s); });
+      if (rc) return rc;
+    }
+  }
+  if (stop_stage == 2) return 0;
+  const double fs = (double)B * (2.0 * (double)d.nTp * d.nTp / 2.0 + 2.0 * (double)d.nV * d.nT + 10.0 * d.nV);
+  const double bs = (double)B * (((double)d.nTp * d.nTp / 2.0 + (double)d.NT * TILE * TILE + (double)d.nV * d.nT) * 8.0);
+  rc = timed(c, s, KC_SOLVE, fs, bs, [&] {
+    return launch_solve(K, d, B, Dinv, z, (const double*)sp.yV.p, scal, d_fit, d_ebv, s);
+  });
+  return rc;
+}
+
+int check_ctx(tblup_ctx* c) {
+  if (!c) return fail(TBLUP_ERR_ARG, "null context");
+  return 0;
+}
+
+Split* find_split(tblup_ctx* c, int id) {
+  auto it = c->splits.find(id);
+  return it == c->splits.end() ? nullptr : it->second.get();
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tblup_last_error(void) { return g_err.c_str(); }
+
+const char* tblup_version(void) { return "tblup_gpu 0.1.0 (gfx950)"; }
+
+int tblup_device_count(int* out) {
+  if (!out) return fail(TBLUP_ERR_ARG, "null out");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *out = n;
+  return 0;
+}
+
+int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const double* pheno, int device,
+                     tblup_ctx** out) {
+  g_err.clear();
+  if (!out) return fail(TBLUP_ERR_ARG, "null out_ctx");
+  *out = nullptr;
+  if (!geno || !pheno || n < 2 || P < 1) return fail(TBLUP_ERR_ARG, "bad genotype/phenotype arguments");
+  if (layout != TBLUP_LAYOUT_ANIMAL_MAJOR && layout != TBLUP_LAYOUT_SNP_MAJOR) return fail(TBLUP_ERR_ARG, "bad layout");
+  if (n > (int64_t)1 << 30) return fail(TBLUP_ERR_ARG, "too many animals");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TBLUP_ERR_HIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(TBLUP_ERR_ARG, "device id out of range");
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<tblup_ctx> c(new tblup_ctx());
+  c->device = device;
+  c->n = n;
+  c->P = P;
+  c->pheno.assign(pheno, pheno + n);
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  const char* env = getenv("TBLUP_WORKSPACE_MB");
+  c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
+  const size_t gbytes = (size_t)n * (size_t)P;
+  if (int rc = dev_alloc(c.get(), c->geno_sm, gbytes)) return rc;
+  if (int rc = dev_alloc(c.get(), c->colsum_all, (size_t)P * 4)) return rc;
+  if (layout == TBLUP_LAYOUT_SNP_MAJOR) {
+    HIPCHK(hipMemcpyAsync(c->geno_sm.p, geno, gbytes, hipMemcpyHostToDevice, c->stream));
+  } else {
+    if (int rc = dev_alloc(c.get(), c->scratch, gbytes)) return rc;
+    HIPCHK(hipMemcpyAsync(c->scratch.p, geno, gbytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_transpose_geno((const int8_t*)c->scratch.p, (int8_t*)c->geno_sm.p, n, P, c->stream));
+  }
+  HIPCHK(launch_colsum_all((const int8_t*)c->geno_sm.p, (int32_t*)c->colsum_all.p, n, P, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dev_free(c.get(), c->scratch);
+  *out = c.release();
+  return 0;
+}
+
+int tblup_ctx_destroy(tblup_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& p : c->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  for (auto& kv : c->splits) {
+    kv.second->geno.release();
+    kv.second->colsumT.release();
+    kv.second->yT.release();
+    kv.second->yV.release();
+  }
+  c->geno_sm.release();
+  c->colsum_all.release();
+  c->scratch.release();
+  c->ws.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT, const int64_t* valid,
+                    int64_t nV) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (!train || !valid || nT < 1 || nV < 2) return fail(TBLUP_ERR_ARG, "split needs >= 1 train and >= 2 valid rows");
+  std::vector<char> seen_t(c->n, 0);
+  for (int64_t i = 0; i < nT; ++i)
+    if (train[i] < 0 || train[i] >= c->n) return fail(TBLUP_ERR_ARG, "train index out of range");
+  for (int64_t i = 0; i < nV; ++i)
+    if (valid[i] < 0 || valid[i] >= c->n) return fail(TBLUP_ERR_ARG, "valid index out of range");
+  HIPCHK(hipSetDevice(c->device));
+  auto sp = std::make_unique<Split>();
+  sp->nT = nT;
+  sp->nV = nV;
+  sp->nTp = round_up(nT, TILE);
+  sp->nVp = round_up(nV, TILE);
+  sp->nRp = sp->nTp + sp->nVp;
+  std::vector<int32_t> rowmap(sp->nRp, -1);
+  for (int64_t i = 0; i < nT; ++i) rowmap[i] = (int32_t)train[i];
+  for (int64_t i = 0; i < nV; ++i) rowmap[sp->nTp + i] = (int32_t)valid[i];
+  std::vector<double> yT(sp->nTp, 0.0), yV(nV);
+  // mean(y_T) as numpy computes it for Ridge's y_offset (pairwise summation differs only in rounding)
+  long double acc = 0.0L;
+  for (int64_t i = 0; i < nT; ++i) {
+    yT[i] = c->pheno[train[i]];
+    acc += yT[i];
+  }
+  sp->meanyT = (double)(acc / (long double)nT);
+  for (int64_t i = 0; i < nV; ++i) yV[i] = c->pheno[valid[i]];
+  if (int rc = dev_alloc(c, sp->geno, (size_t)c->P * sp->nRp)) return rc;
+  if (int rc = dev_alloc(c, sp->colsumT, (size_t)c->P * 4)) return rc;
+  if (int rc = dev_alloc(c, sp->yT, (size_t)sp->nTp * 8)) return rc;
+  if (int rc = dev_alloc(c, sp->yV, (size_t)nV * 8)) return rc;
+  DevBuf rm;
+  if (int rc = dev_alloc(c, rm, rowmap.size() * 4)) return rc;
+  HIPCHK(hipMemcpyAsync(rm.p, rowmap.data(), rowmap.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(sp->yT.p, yT.data(), yT.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(sp->yV.p, yV.data(), yV.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(launch_build_split((const int8_t*)c->geno_sm.p, c->n, c->P, (const int32_t*)rm.p, sp->nRp, nT,
+                            (int8_t*)sp->geno.p, (int32_t*)sp->colsumT.p, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dev_free(c, rm);
+  auto it = c->splits.find(split_id);
+  if (it != c->splits.end()) {
+    dev_free(c, it->second->geno);
+    dev_free(c, it->second->colsumT);
+    dev_free(c, it->second->yT);
+    dev_free(c, it->second->yV);
+  }
+  c->splits[split_id] = std::move(sp);
+  return 0;
+}
+
+int tblup_drop_split(tblup_ctx* c, int split_id) {
+  if (int rc = check_ctx(c)) return rc;
+  auto it = c->splits.find(split_id);
+  if (it == c->splits.end()) return fail(TBLUP_ERR_ARG, "unknown split id");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dev_free(c, it->second->geno);
+  dev_free(c, it->second->colsumT);
+  dev_free(c, it->second->yT);
+  dev_free(c, it->second->yV);
+  c->splits.erase(it);
+  return 0;
+}
+
+static int validate_batch(tblup_ctx* c, int branch, double h2, const int64_t* offsets, int64_t batch) {
+  if (branch < 0 || branch > 2) return fail(TBLUP_ERR_ARG, "bad branch");
+  if (!(h2 > 0.0) || !(h2 <= 1.0)) return fail(TBLUP_ERR_ARG, "h2 must be in (0, 1]");
+  if (batch < 0) return fail(TBLUP_ERR_ARG, "negative batch");
+  if (batch > 0 && !offsets) return fail(TBLUP_ERR_ARG, "null offsets");
+  for (int64_t b = 0; b < batch; ++b)
+    if (offsets[b + 1] - offsets[b] < 1) return fail(TBLUP_ERR_ARG, "every individual needs k >= 1 indices");
+  if (batch > 0 && offsets[0] != 0) return fail(TBLUP_ERR_ARG, "offsets[0] must be 0");
+  (void)c;
+  return 0;
+}
+
+int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64_t* offsets, int64_t batch,
+                     double h2, int branch, double* fitness, double* ebv) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_batch(c, branch, h2, offsets, batch)) return rc;
+  if (batch == 0) return 0;
+  if (!idx || !fitness) return fail(TBLUP_ERR_ARG, "null idx/fitness");
+  Split* sp = find_split(c, split_id);
+  if (!sp) return fail(TBLUP_ERR_ARG, "unknown split id");
+  for (int64_t i = 0; i < offsets[batch]; ++i)
+    if (idx[i] < 0 || idx[i] >= c->P) return fail(TBLUP_ERR_ARG, "SNP index out of range");
+  HIPCHK(hipSetDevice(c->device));
+  const EvalDims d = dims_of(c, *sp);
+  const bool want_ebv = ebv != nullptr;
+  int64_t b0 = 0;
+  while (b0 < batch) {
+    // grow the chunk while it fits the workspace budget
+    int64_t b1 = b0, max_kblk = 0, sum_k = 0;
+    while (b1 < batch) {
+      const int64_t k = offsets[b1 + 1] - offsets[b1];
+      const int64_t mkb = std::max(max_kblk, (k + KBLK - 1) / KBLK);
+      if (b1 > b0 && chunk_bytes(d, b1 + 1 - b0, mkb, sum_k + k, want_ebv) > c->budget) break;
+      if (b1 - b0 >= 65535) break;
+      max_kblk = mkb;
+      sum_k += k;
+      ++b1;
+    }
+    const int64_t B = b1 - b0;
+    const size_t need = chunk_bytes(d, B, max_kblk, sum_k, want_ebv);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (int rc = dev_alloc(c, c->ws, need)) return rc;
+    Carve cv{(char*)c->ws.p};
+    int64_t* d_idx = cv.take<int64_t>((size_t)sum_k);
+    int64_t* d_off = cv.take<int64_t>((size_t)B + 1);
+    double* d_fit = cv.take<double>((size_t)B);
+    double* d_ebv = want_ebv ? cv.take<double>((size_t)B * d.nV) : nullptr;
+    std::vector<int64_t> hoff(B + 1);
+    for (int64_t b = 0; b <= B; ++b) hoff[b] = offsets[b0 + b] - offsets[b0];
+    HIPCHK(hipMemcpyAsync(d_idx, idx + offsets[b0], (size_t)sum_k * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_off, hoff.data(), (size_t)(B + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if (int rc = run_chunk(c, *sp, d, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv, d_fit, d_ebv, 0,
+                           nullptr, nullptr))
+      return rc;
+    HIPCHK(hipMemcpyAsync(fitness + b0, d_fit, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
+    if (want_ebv)
+      HIPCHK(hipMemcpyAsync(ebv + b0 * d.nV, d_ebv, (size_t)B * d.nV * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    b0 = b1;
+  }
+  if (c->profiling) return drain_events(c);
+  return 0;
+}
+
+int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, const int64_t* d_offsets,
+                            const int64_t* h_offsets, int64_t batch, double h2, int branch, double* d_fitness,
+                            double* d_ebv, void* stream) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_batch(c, branch, h2, h_offsets, batch)) return rc;
+  if (batch == 0) return 0;
+  if (!d_idx || !d_offsets || !d_fitness) return fail(TBLUP_ERR_ARG, "null device pointers");
+  if (batch > 65535) return fail(TBLUP_ERR_ARG, "device batch limited to 65535 individuals per call");
+  Split* sp = find_split(c, split_id);
+  if (!sp) return fail(TBLUP_ERR_ARG, "unknown split id");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  const EvalDims d = dims_of(c, *sp);
+  int64_t max_kblk = 0;
+  for (int64_t b = 0; b < batch; ++b) max_kblk = std::max(max_kblk, (h_offsets[b + 1] - h_offsets[b] + KBLK - 1) / KBLK);
+  const size_t need = chunk_bytes(d, batch, max_kblk, 0, false);
+  if (need > c->ws.bytes) {
+    // the workspace may still be in use by earlier work on either stream
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (int rc = dev_alloc(c, c->ws, need)) return rc;
+  }
+  Carve cv{(char*)c->ws.p};
+  return run_chunk(c, *sp, d, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness, d_ebv, 0, nullptr,
+                   nullptr);
+}
+
+int tblup_set_profiling(tblup_ctx* c, int enable) {
+  if (int rc = check_ctx(c)) return rc;
+  c->profiling = enable != 0;
+  return 0;
+}
+
+int tblup_get_profile(tblup_ctx* c, double* ms, int64_t* launches, double* flops, double* bytes) {
+  if (int rc = check_ctx(c)) return rc;
+  HIPCHK(hipSetDevice(c->device));
+  if (int rc = drain_events(c)) return rc;
+  for (int i = 0; i < TBLUP_N_KCLASS; ++i) {
+    if (ms) ms[i] = c->ms[i];
+    if (launches) launches[i] = c->launches[i];
+    if (flops) flops[i] = c->flops[i];
+    if (bytes) bytes[i] = c->bytes[i];
+  }
+  return 0;
+}
+
+int tblup_reset_profile(tblup_ctx* c) {
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = drain_events(c)) return rc;
+  for (int i = 0; i < TBLUP_N_KCLASS; ++i) {
+    c->ms[i] = 0;
+    c->launches[i] = 0;
+    c->flops[i] = 0;
+    c->bytes[i] = 0;
+  }
+  return 0;
+}
+
+int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, double h2, int branch, int stage,
+                    double* out, double* z_out) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (!idx || k < 1 || !out) return fail(TBLUP_ERR_ARG, "bad debug arguments");
+  if (stage != 1 && stage != 2) return fail(TBLUP_ERR_ARG, "stage must be 1 or 2");
+  int64_t offs[2] = {0, k};
+  if (int rc = validate_batch(c, branch, h2, offs, 1)) return rc;
+  for (int64_t i = 0; i < k; ++i)
+    if (idx[i] < 0 || idx[i] >= c->P) return fail(TBLUP_ERR_ARG, "SNP index out of range");
+  Split* sp = find_split(c, split_id);
+  if (!sp) return fail(TBLUP_ERR_ARG, "unknown split id");
+  HIPCHK(hipSetDevice(c->device));
+  const EvalDims d = dims_of(c, *sp);
+  const int64_t nkb = (k + KBLK - 1) / KBLK;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (int rc = dev_alloc(c, c->ws, chunk_bytes(d, 1, nkb, k, false))) return rc;
+  Carve cv{(char*)c->ws.p};
+  int64_t* d_idx = cv.take<int64_t>((size_t)k);
+  int64_t* d_off = cv.take<int64_t>(2);
+  double* d_fit = cv.take<double>(1);
+  HIPCHK(hipMemcpyAsync(d_idx, idx, (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d_off, offs, 16, hipMemcpyHostToDevice, c->stream));
+  double *K = nullptr, *z = nullptr;
+  if (int rc = run_chunk(c, *sp, d, c->stream, d_idx, d_off, offs, 1, h2, branch, cv, d_fit, nullptr, stage,
+                         &K, &z))
+    return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  std::vector<double> full((size_t)d.nRp * d.nTp);
+  HIPCHK(hipMemcpy(full.data(), K, full.size() * 8, hipMemcpyDeviceToHost));
+  const int64_t nR = d.nT + d.nV;
+  for (int64_t r = 0; r < nR; ++r) {
+    const int64_t src = r < d.nT ? r : d.nTp + (r - d.nT);
+    std::memcpy(out + r * d.nT, full.data() + src * d.nTp, (size_t)d.nT * 8);
+  }
+  if (z_out) {
+    std::vector<double> zz(d.nTp);
+    HIPCHK(hipMemcpy(zz.data(), z, (size_t)d.nTp * 8, hipMemcpyDeviceToHost));
+    std::memcpy(z_out, zz.data(), (size_t)d.nT * 8);
+  }
+  if (c->profiling) return drain_events(c);
+  return 0;
+}
+
+int tblup_mem_info(tblup_ctx* c, int64_t* bytes) {
+  if (int rc = check_ctx(c)) return rc;
+  if (bytes) *bytes = c->mem_in_use;
+  return 0;
+}
+
+}  // extern "C"

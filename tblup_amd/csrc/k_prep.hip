@@ -1,0 +1,245 @@
+// Preparation kernels: genotype transpose, split build, per-individual scalars
+// and the gathered, animal-major genotype panel with exact centring sums.
+//
+// Reference behaviour restated here (ianwhale/tblup):
+//   * data[:, indices] fancy-index gather, duplicates gathered twice
+//     (tblup/evaluator.py:275, :298)
+//   * allele frequency p = column mean / 2 over ALL rows for gblup
+//     (utils.py:14 via evaluator.py:275) and over TRAIN rows for snp_blup
+//     (evaluator.py:304); d = 2 sum p(1-p) (utils.py:18, evaluator.py:305)
+//   * lambda = (1-h2)/h2 (evaluator.py:277; evaluator.py:306 is lambda*d in
+//     ridge units)
+// All centring terms are carried as exact integers: with m_s the allele count
+// of SNP s over the reference rows (N of them), 2p_s = m_s/N, so
+//   sum_s (a_is - 2p_s)(a_js - 2p_s) = (A A^T)_ij - (u_i + u_j)/N + q/N^2
+// with u_i = sum_s m_s a_is and q = sum_s m_s^2.
+#include "tblup_internal.h"
+
+namespace tblup {
+
+// ---------------------------------------------------------------------------
+// animal-major [n][P] -> SNP-major [P][n]; 64x64 byte tiles through LDS.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_transpose_geno(const int8_t* __restrict__ src, int8_t* __restrict__ dst,
+                                                        int64_t n, int64_t P) {
+  __shared__ int8_t tile[64][65];
+  const int64_t p0 = (int64_t)blockIdx.x * 64, a0 = (int64_t)blockIdx.y * 64;
+  const int t = threadIdx.x;
+  // load: thread t covers 16 bytes of animal row (t >> 2), SNP cols (t & 3) * 16 ..
+  {
+    const int ar = t >> 2, pc = (t & 3) * 16;
+    const int64_t a = a0 + ar;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t p = p0 + pc + e;
+      tile[ar][pc + e] = (a < n && p < P) ? src[a * P + p] : (int8_t)0;
+    }
+  }
+  __syncthreads();
+  {
+    const int pr = t >> 2, ac = (t & 3) * 16;
+    const int64_t p = p0 + pr;
+    if (p < P) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t a = a0 + ac + e;
+        if (a < n) dst[p * n + a] = tile[ac + e][pr];
+      }
+    }
+  }
+}
+
+hipError_t launch_transpose_geno(const int8_t* src, int8_t* dst, int64_t n, int64_t P, hipStream_t s) {
+  dim3 grid((unsigned)((P + 63) / 64), (unsigned)((n + 63) / 64));
+  hipLaunchKernelGGL(k_transpose_geno, grid, dim3(256), 0, s, src, dst, n, P);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// per-SNP allele count over all n animals (one wave per SNP row)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_colsum_all(const int8_t* __restrict__ g, int32_t* __restrict__ cs, int64_t n,
+                                                    int64_t P) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 4 + w;
+  if (p >= P) return;
+  const int8_t* row = g + p * n;
+  int s = 0;
+  for (int64_t a = l; a < n; a += 64) s += row[a];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (l == 0) cs[p] = s;
+}
+
+hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, int64_t P, hipStream_t s) {
+  hipLaunchKernelGGL(k_colsum_all, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, s, geno_sm, colsum, n, P);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// split build: permuted SNP-major rows [T | pad | V | pad] and train counts
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ g, int64_t n, int64_t P,
+                                                     const int32_t* __restrict__ rowmap, int64_t nRp, int64_t nT,
+                                                     int8_t* __restrict__ out, int32_t* __restrict__ csT) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 4 + w;
+  if (p >= P) return;
+  const int8_t* row = g + p * n;
+  int8_t* orow = out + p * nRp;
+  int s = 0;
+  for (int64_t r = l; r < nRp; r += 64) {
+    const int32_t src = rowmap[r];
+    const int8_t v = src >= 0 ? row[src] : (int8_t)0;
+    orow[r] = v;
+    if (r < nT) s += v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (l == 0) csT[p] = s;
+}
+
+hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap, int64_t nRp,
+                              int64_t nT, int8_t* geno_split, int32_t* colsum_T, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_split, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, s, geno_sm, n, P, rowmap, nRp,
+                     nT, geno_split, colsum_T);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// per-individual scalars: branch, 1/N, q/N^2, 1/d, mu, lambda
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t clamp_idx(int64_t p, int64_t P) { return p < 0 ? 0 : (p >= P ? P - 1 : p); }
+
+__global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
+                                                     const int32_t* __restrict__ csT,
+                                                     const int32_t* __restrict__ csA, int64_t n, int64_t nT,
+                                                     int64_t P, int branch, double meanyT, double h2,
+                                                     double* __restrict__ scal) {
+  const int64_t b = blockIdx.x;
+  const int64_t o0 = off[b], k = off[b + 1] - o0;
+  int mode = branch;
+  if (mode == 0) mode = (k > n) ? 1 : 2;  // evaluator.py:257
+  const int32_t* cs = (mode == 1) ? csA : csT;
+  int64_t m1 = 0, q = 0;
+  for (int64_t s = threadIdx.x; s < k; s += 256) {
+    const int64_t m = cs[clamp_idx(idx[o0 + s], P)];
+    m1 += m;
+    q += m * m;
+  }
+  __shared__ int64_t r1[256], r2[256];
+  r1[threadIdx.x] = m1;
+  r2[threadIdx.x] = q;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) {
+      r1[threadIdx.x] += r1[threadIdx.x + st];
+      r2[threadIdx.x] += r2[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double N = (mode == 1) ? (double)n : (double)nT;
+    const double M1 = (double)r1[0], Q = (double)r2[0];
+    const double d = M1 / N - Q / (2.0 * N * N);  // 2 sum p(1-p)
+    double* sc = scal + b * 8;
+    sc[0] = 1.0 / N;
+    sc[1] = Q / (N * N);
+    sc[2] = 1.0 / d;
+    sc[3] = (mode == 2) ? meanyT : 0.0;
+    sc[4] = (1.0 - h2) / h2;
+    sc[5] = d;
+    sc[6] = (double)mode;
+    sc[7] = (double)k;
+  }
+}
+
+hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
+                              const int32_t* colsum_all, const EvalDims& d, int branch, double meanyT, double h2,
+                              double* scal, hipStream_t s) {
+  hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, colsum_T, colsum_all, d.n, d.nT,
+                     d.P, branch, meanyT, h2, scal);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// gather: panel[b][kb][r][64] (animal-major 64-SNP blocks) + u_r = sum m_s a_rs
+//   grid (nRp/128, B), 128 threads; thread t owns animal row r0 + t.
+//   Each 64-SNP block: 64 gathered SNP rows x 128 animals staged in LDS
+//   (coalesced 16-B row-segment loads), then transposed by byte reads.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_gather(const int8_t* __restrict__ gs, const int64_t* __restrict__ idx,
+                                                const int64_t* __restrict__ off,
+                                                int64_t panel_stride,
+                                                const int32_t* __restrict__ csT, const int32_t* __restrict__ csA,
+                                                const double* __restrict__ scal, int64_t P, int64_t nRp,
+                                                int8_t* __restrict__ panel, double* __restrict__ u) {
+  __shared__ __attribute__((aligned(16))) int8_t tile[KBLK][GATHER_ROWS];
+  __shared__ int64_t srow[KBLK];
+  __shared__ int32_t sm[KBLK];
+  const int t = threadIdx.x;
+  const int64_t b = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.x * GATHER_ROWS;
+  const int64_t o0 = off[b], k = off[b + 1] - o0;
+  const int mode = (int)scal[b * 8 + 6];
+  const int32_t* cs = (mode == 1) ? csA : csT;
+  const int64_t nblk = (k + KBLK - 1) / KBLK;
+  int8_t* pb = panel + b * panel_stride;
+  int64_t uacc = 0;
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    if (t < KBLK) {
+      const int64_t s = kb * KBLK + t;
+      if (s < k) {
+        const int64_t p = clamp_idx(idx[o0 + s], P);
+        srow[t] = p;
+        sm[t] = cs[p];
+      } else {
+        srow[t] = -1;
+        sm[t] = 0;
+      }
+    }
+    __syncthreads();
+    // 64 rows x 128 B = 512 x 16 B chunks, 4 per thread
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = t + 128 * e, j = q >> 3, c = q & 7;
+      const int64_t p = srow[j];
+      v4i v = {0, 0, 0, 0};
+      if (p >= 0) v = *reinterpret_cast<const v4i*>(gs + p * nRp + r0 + 16 * c);
+      *reinterpret_cast<v4i*>(&tile[j][16 * c]) = v;
+    }
+    __syncthreads();
+    v4i out[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+#pragma unroll
+      for (int d4 = 0; d4 < 4; ++d4) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = q4 * 16 + d4 * 4 + e;
+          const uint32_t byte = (uint8_t)tile[j][t];
+          uacc += (int64_t)sm[j] * (int64_t)byte;
+          word |= byte << (8 * e);
+        }
+        out[q4][d4] = (int)word;
+      }
+    }
+    v4i* dstp = reinterpret_cast<v4i*>(pb + (kb * nRp + r0 + t) * KBLK);
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) dstp[q4] = out[q4];
+    __syncthreads();
+  }
+  u[b * nRp + r0 + t] = (double)uacc;
+}
+
+hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int64_t* off, int64_t panel_stride,
+                         int64_t B, const int32_t* colsum_T, const int32_t* colsum_all, const double* scal,
+                         const EvalDims& d, int8_t* panel, double* u, hipStream_t s) {
+  dim3 grid((unsigned)(d.nRp / GATHER_ROWS), (unsigned)B);
+  hipLaunchKernelGGL(k_gather, grid, dim3(GATHER_ROWS), 0, s, geno_split, idx, off, panel_stride, colsum_T, colsum_all,
+                     scal, d.P, d.nRp, panel, u);
+  return hipGetLastError();
+}
+
+}  // namespace tblup

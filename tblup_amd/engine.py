@@ -1,0 +1,183 @@
+"""GpuBlupEngine: one MI355X context holding the genotype panel in HBM.
+
+This is the compute leg that replaces the reference's worker pool
+(tblup/evaluator.py:205-241): instead of pickling one `blup` job per
+individual onto an mp.Queue, a whole batch of selected-index sets goes to
+`tblup_eval_batch` in one call.  Splits (train/validation animal lists) are
+registered once and cached by content, so InterGCV folds, the testing split
+and Monte-Carlo splits each pay the split build only when they change.
+"""
+import ctypes
+import hashlib
+from collections import OrderedDict
+
+import numpy as np
+
+from . import _native
+
+
+def _as_int64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int64))
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def validate_genotypes(data):
+    """The GPU path stores genotypes as int8 {0,1,2} (SURVEY.md section 8a data contract).
+
+    Raises ValueError for anything else (e.g. imputed dosages), instead of
+    silently changing the arithmetic.
+    """
+    g = np.asarray(data)
+    if g.ndim != 2:
+        raise ValueError("genotype matrix must be 2-D (animals x SNPs)")
+    if g.dtype == np.int8:
+        ok = bool(np.all((g >= 0) & (g <= 2)))
+        out = g
+    else:
+        ok = bool(np.all((g == 0) | (g == 1) | (g == 2)))
+        out = g.astype(np.int8) if ok else None
+    if not ok:
+        raise ValueError("genotypes must take values in {0, 1, 2} for the MI355X evaluator")
+    return np.ascontiguousarray(out)
+
+
+def concat_genomes(genomes):
+    """Concatenate ragged index arrays -> (idx int64, offsets int64[B+1])."""
+    lens = np.fromiter((len(g) for g in genomes), dtype=np.int64, count=len(genomes))
+    offsets = np.zeros(len(genomes) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    if len(genomes):
+        idx = np.concatenate([np.asarray(g, dtype=np.int64).ravel() for g in genomes])
+    else:
+        idx = np.zeros(0, dtype=np.int64)
+    return np.ascontiguousarray(idx), offsets
+
+
+class GpuBlupEngine:
+    """Genotypes + phenotypes resident on one GPU; batched BLUP fitness."""
+
+    MAX_SPLITS = 16
+
+    def __init__(self, data, labels, device=0, snp_major=False):
+        self._lib = _native.load()
+        geno = validate_genotypes(data)
+        pheno = np.ascontiguousarray(np.asarray(labels, dtype=np.float64).ravel())
+        if snp_major:
+            n_snps, n = geno.shape
+            layout = _native.LAYOUT_SNP_MAJOR
+        else:
+            n, n_snps = geno.shape
+            layout = _native.LAYOUT_ANIMAL_MAJOR
+        if pheno.shape[0] != n:
+            raise ValueError(f"phenotype length {pheno.shape[0]} != number of animals {n}")
+        self.n_animals, self.n_snps, self.device = n, n_snps, int(device)
+        ctx = ctypes.c_void_p()
+        _native.check("tblup_ctx_create", self._lib.tblup_ctx_create(
+            geno.ctypes.data_as(ctypes.c_void_p), n, n_snps, layout, _ptr(pheno, ctypes.c_double), self.device,
+            ctypes.byref(ctx)))
+        self._ctx = ctx
+        self._splits = OrderedDict()   # key -> (split_id, n_valid)
+        self._next_split = 0
+
+    # ------------------------------------------------------------------ splits
+    def split_id(self, train, valid):
+        t = _as_int64(train)
+        v = _as_int64(valid)
+        key = hashlib.sha1(t.tobytes() + b"|" + v.tobytes()).hexdigest()
+        hit = self._splits.get(key)
+        if hit is not None:
+            self._splits.move_to_end(key)
+            return hit[0]
+        if len(self._splits) >= self.MAX_SPLITS:
+            _, (old_id, _) = self._splits.popitem(last=False)
+            _native.check("tblup_drop_split", self._lib.tblup_drop_split(self._ctx, old_id))
+        sid = self._next_split
+        self._next_split += 1
+        _native.check("tblup_set_split", self._lib.tblup_set_split(
+            self._ctx, sid, _ptr(t, ctypes.c_int64), len(t), _ptr(v, ctypes.c_int64), len(v)))
+        self._splits[key] = (sid, len(v))
+        return sid
+
+    # -------------------------------------------------------------- evaluation
+    def evaluate(self, genomes, train, valid, h2, branch="auto", return_ebv=False):
+        """Fitness |pearson(EBV_V, y_V)| for each selected-index set (evaluator.py:244-314)."""
+        sid = self.split_id(train, valid)
+        idx, offsets = concat_genomes(genomes)
+        B = len(genomes)
+        fit = np.empty(B, dtype=np.float64)
+        n_valid = len(valid)
+        ebv = np.empty((B, n_valid), dtype=np.float64) if return_ebv else None
+        if B:
+            _native.check("tblup_eval_batch", self._lib.tblup_eval_batch(
+                self._ctx, sid, _ptr(idx, ctypes.c_int64), _ptr(offsets, ctypes.c_int64), B, float(h2),
+                _native.BRANCH[branch], _ptr(fit, ctypes.c_double),
+                _ptr(ebv, ctypes.c_double) if return_ebv else None))
+        return (fit, ebv) if return_ebv else fit
+
+    def evaluate_device(self, split_id, d_idx_ptr, d_off_ptr, h_offsets, h2, d_fit_ptr, d_ebv_ptr=None,
+                        stream_ptr=None, branch="auto"):
+        """Asynchronous evaluation on device-resident buffers (raw device pointers)."""
+        h_off = _as_int64(h_offsets)
+        B = len(h_off) - 1
+        _native.check("tblup_eval_batch_device", self._lib.tblup_eval_batch_device(
+            self._ctx, split_id, ctypes.c_void_p(d_idx_ptr), ctypes.c_void_p(d_off_ptr),
+            _ptr(h_off, ctypes.c_int64), B, float(h2), _native.BRANCH[branch], ctypes.c_void_p(d_fit_ptr),
+            ctypes.c_void_p(d_ebv_ptr) if d_ebv_ptr else None,
+            ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def debug_grm(self, indices, train, valid, h2, branch="auto", stage=1):
+        """K_{R,T} (stage 1) or the factored block (stage 2) and z for one individual."""
+        sid = self.split_id(train, valid)
+        idx = _as_int64(indices)
+        nT, nV = len(train), len(valid)
+        out = np.empty((nT + nV, nT), dtype=np.float64)
+        z = np.empty(nT, dtype=np.float64)
+        _native.check("tblup_debug_grm", self._lib.tblup_debug_grm(
+            self._ctx, sid, _ptr(idx, ctypes.c_int64), len(idx), float(h2), _native.BRANCH[branch], int(stage),
+            _ptr(out, ctypes.c_double), _ptr(z, ctypes.c_double)))
+        return out, z
+
+    # --------------------------------------------------------------- profiling
+    def set_profiling(self, enable=True):
+        _native.check("tblup_set_profiling", self._lib.tblup_set_profiling(self._ctx, 1 if enable else 0))
+
+    def reset_profile(self):
+        _native.check("tblup_reset_profile", self._lib.tblup_reset_profile(self._ctx))
+
+    def profile(self):
+        n = _native.N_KCLASS
+        ms = np.zeros(n)
+        la = np.zeros(n, dtype=np.int64)
+        fl = np.zeros(n)
+        by = np.zeros(n)
+        _native.check("tblup_get_profile", self._lib.tblup_get_profile(
+            self._ctx, _ptr(ms, ctypes.c_double), _ptr(la, ctypes.c_int64), _ptr(fl, ctypes.c_double),
+            _ptr(by, ctypes.c_double)))
+        return {name: {"ms": float(ms[i]), "launches": int(la[i]), "flops": float(fl[i]), "bytes": float(by[i])}
+                for i, name in enumerate(_native.KCLASS_NAMES)}
+
+    def mem_in_use(self):
+        v = ctypes.c_int64(0)
+        _native.check("tblup_mem_info", self._lib.tblup_mem_info(self._ctx, ctypes.byref(v)))
+        return v.value
+
+    # ----------------------------------------------------------------- cleanup
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.tblup_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

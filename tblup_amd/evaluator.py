@@ -1,0 +1,367 @@
+"""Drop-in evaluators for TBLUP's fitness plugin API, computed on MI355X.
+
+Mirrors the reference module `tblup/evaluator.py` (ianwhale/tblup): the same
+class names, constructor signatures, attributes the rest of TBLUP reads
+(`training_indices`, `validation_indices`, `testing_indices`, `snp_remover`,
+`data_path`, `labels_path`, `h2`, `archive`), the same RNG consumption for the
+splits, the same archive/SNP-removal semantics and error behaviour.  What
+changes is the compute leg: instead of `n_procs` worker processes each
+running `blup()` on a private copy of the data (evaluator.py:120-131,
+205-241), `__enter__` opens a GPU context (tblup_amd.engine.GpuBlupEngine) and
+every `_evaluate` sends the whole batch of selected-index sets to the HIP
+pipeline in one call.  Under torch.distributed (one process per GPU) the batch
+is sharded across ranks and the fitnesses are all-gathered.
+
+There is no CPU fallback: without the HIP library, entering the evaluator
+raises ImportError.
+"""
+import abc
+import os
+import random
+import weakref
+from math import sqrt
+
+import numpy as np
+
+from .distributed import allgather_fitness, shard_range, world
+
+
+def get_evaluator(args):
+    """Factory with the reference's flag semantics (evaluator.py:14-55)."""
+    splitter = None
+    if args.splitter == "pca":
+        raise NotImplementedError(
+            "--splitter pca is not available in the MI355X evaluator yet (SURVEY.md section 8f)")
+    r = args.features if args.removal_r is None else args.removal_r
+    remover = SNPRemovalHandler(r, args.h2_alpha, args.heritability, args.remove_snps)
+    common = dict(n_procs=args.processes, splitter=splitter, snp_remover=remover)
+    pos = (args.geno, args.pheno, args.heritability)
+    kind = args.regressor
+    if kind == args.REGRESSOR_TYPE_BLUP:
+        return BlupParallelEvaluator(*pos, **common)
+    if kind == args.REGRESSOR_TYPE_INTRACV_BLUP:
+        return IntraGCVBlupParallelEvaluator(*pos, n_folds=args.cv_folds, **common)
+    if kind == args.REGRESSOR_TYPE_INTERCV_BLUP:
+        return InterGCVBlupParallelEvaluator(*pos, n_folds=args.cv_folds, **common)
+    if kind == args.REGRESSOR_TYPE_MONTECV_BLUP:
+        return MonteCarloCVBlupParallelEvaluator(*pos, **common)
+    raise NotImplementedError("Regressor with config option {} not implemented.".format(kind))
+
+
+# ---------------------------------------------------------------------------
+# Base classes
+# ---------------------------------------------------------------------------
+class Evaluator(abc.ABC):
+    """Evaluator plugin interface (evaluator.py:63-99)."""
+
+    def __init__(self, data_path, labels_path):
+        assert os.path.isfile(data_path), "Argument for data_path {} not found.".format(data_path)
+        assert os.path.isfile(labels_path), "Argument for labels_path {} not found.".format(labels_path)
+        self.data_path = data_path
+        self.labels_path = labels_path
+
+    @abc.abstractmethod
+    def __enter__(self):
+        pass
+
+    @abc.abstractmethod
+    def __exit__(self, exc_type, exc_val, exc_tb):
+        pass
+
+    @abc.abstractmethod
+    def evaluate(self, previous_population, next_population, generation):
+        raise NotImplementedError()
+
+    @abc.abstractmethod
+    def genomes_to_evaluate(self, population):
+        raise NotImplementedError()
+
+
+class ParallelEvaluator(Evaluator):
+    """Context-managed compute resource (evaluator.py:102-155).
+
+    The reference spawns `n_procs` workers in __enter__; here __enter__ opens
+    the GPU context for this process (device = `device`, else LOCAL_RANK, else 0).
+    `n_procs` is kept for signature compatibility.
+    """
+
+    def __init__(self, data_path, labels_path, n_procs=-1, device=None):
+        super().__init__(data_path, labels_path)
+        self.n_procs = n_procs
+        self.device = device
+        self.engine = None
+
+    def _device(self):
+        if self.device is not None:
+            return int(self.device)
+        return int(os.environ.get("LOCAL_RANK", "0"))
+
+    def _open_engine(self):
+        from .engine import GpuBlupEngine  # loads libtblup_gpu.so or raises ImportError
+        data = np.load(self.data_path)
+        labels = np.load(self.labels_path)
+        return GpuBlupEngine(data, labels, device=self._device())
+
+    def __enter__(self):
+        if self.engine is None:
+            self.engine = self._open_engine()
+        return self
+
+    def __exit__(self, exc_type, exc_val, exc_tb):
+        if self.engine is not None:
+            self.engine.close()
+            self.engine = None
+
+    def genomes_to_evaluate(self, population):
+        raise NotImplementedError()
+
+    def evaluate(self, previous_population, next_population, generation):
+        if self.engine is None:
+            raise AttributeError("Workers are not set up.")
+
+
+# ---------------------------------------------------------------------------
+# BLUP evaluators
+# ---------------------------------------------------------------------------
+def _default_split(n_samples, train_test, train_valid):
+    """Shuffled split with the reference's RNG consumption (evaluator.py:196-203):
+    python `random.sample` for the shuffle, then two sklearn train_test_split
+    calls drawing from numpy's global RNG."""
+    from sklearn.model_selection import train_test_split
+
+    order = random.sample(range(n_samples), n_samples)
+    train, test = train_test_split(order, train_size=train_test, test_size=1 - train_test)
+    train, valid = train_test_split(train, train_size=train_valid, test_size=1 - train_valid)
+    return train, valid, test
+
+
+class BlupParallelEvaluator(ParallelEvaluator):
+    """GBLUP / SNP-BLUP fitness on MI355X (reference: evaluator.py:158-431)."""
+
+    TRAIN_TEST_SPLIT = 0.8
+    TRAIN_VALID_SPLIT = 0.8
+
+    def __init__(self, data_path, labels_path, h2, n_procs=-1, splitter=None, snp_remover=None, device=None):
+        super().__init__(data_path, labels_path, n_procs=n_procs, device=device)
+        self.archive = {}
+        self.snp_remover = snp_remover
+        self.h2 = h2
+        data = np.load(data_path, mmap_mode="r")
+        self.n_samples, self.n_columns = data.shape[0], data.shape[1]
+        if splitter:
+            self.training_indices, self.testing_indices = splitter(np.asarray(data))
+            from sklearn.model_selection import train_test_split
+            self.training_indices, self.validation_indices = train_test_split(
+                self.training_indices, train_size=self.TRAIN_VALID_SPLIT, test_size=1 - self.TRAIN_VALID_SPLIT)
+        else:
+            self.training_indices, self.validation_indices, self.testing_indices = _default_split(
+                self.n_samples, self.TRAIN_TEST_SPLIT, self.TRAIN_VALID_SPLIT)
+
+    # -- the hot path -------------------------------------------------------
+    def _fitness(self, genomes, train_indices, validation_indices):
+        """Batched blup() over `genomes`; sharded across ranks under torch.distributed."""
+        rank, ws = world()
+        total = len(genomes)
+        if ws == 1:
+            return self.engine.evaluate(genomes, train_indices, validation_indices, self.h2)
+        lo, hi = shard_range(total, rank, ws)
+        local = self.engine.evaluate(genomes[lo:hi], train_indices, validation_indices, self.h2)
+        return allgather_fitness(local, total)
+
+    @staticmethod
+    def blup(indices, train_indices, validation_indices, data, labels, h2):
+        """Single-individual blup (evaluator.py:244-263), used in-process by local search.
+
+        Runs on the GPU through an engine cached per (data, labels) array pair.
+        """
+        eng = _static_engine(data, labels)
+        return float(eng.evaluate([np.asarray(indices)], train_indices, validation_indices, h2)[0])
+
+    @staticmethod
+    def gblup(indices, train_indices, validation_indices, data, labels, h2):
+        eng = _static_engine(data, labels)
+        return float(eng.evaluate([np.asarray(indices)], train_indices, validation_indices, h2, branch="gblup")[0])
+
+    @staticmethod
+    def snp_blup(indices, train_indices, validation_indices, data, labels, h2):
+        eng = _static_engine(data, labels)
+        return float(eng.evaluate([np.asarray(indices)], train_indices, validation_indices, h2, branch="snp")[0])
+
+    # -- reference control flow ---------------------------------------------
+    def train_validation_indices(self, generation):
+        return self.training_indices, self.validation_indices
+
+    def __getstate__(self):
+        return {k: v for k, v in self.__dict__.items() if k not in ("archive", "pool", "engine")}
+
+    def genomes_to_evaluate(self, population):
+        """Individuals whose uid is not archived (evaluator.py:339-357)."""
+        if self.snp_remover is not None and self.snp_remover.should_remove():
+            return self.snp_remover.genomes_to_evaluate(population, self.archive)
+        todo, where = [], []
+        for i, indv in enumerate(population):
+            if indv.uid not in self.archive:
+                where.append(i)
+                todo.append(indv.genome)
+        return todo, where, False
+
+    def evaluate(self, previous_population, next_population, generation):
+        """evaluator.py:359-378."""
+        super().evaluate(previous_population, next_population, generation)
+        todo, where, reevaluate = self.genomes_to_evaluate(next_population)
+        next_population = self._evaluate(next_population, todo, where, generation)
+        if reevaluate:
+            todo, where, _ = self.genomes_to_evaluate(previous_population)
+            self._evaluate(previous_population, todo, where, generation)
+            previous_population.monitor.log_snp_removal_event(generation)
+        return next_population
+
+    def _evaluate(self, population, to_evaluate, indices, generation):
+        """evaluator.py:380-405, one batched GPU call instead of the queue fan-out."""
+        train, valid = self.train_validation_indices(generation)
+        fits = self._fitness(list(to_evaluate), train, valid) if to_evaluate else []
+        for i, f in zip(indices, fits):
+            population[i].set_fitness(f)
+            self.archive[population[i].uid] = population[i].fitness
+        return population
+
+    def evaluate_testing(self, population):
+        """Testing accuracy with train = T u V and the genome merged with removed SNPs
+        (evaluator.py:407-431); returned in population order."""
+        if self.engine is None:
+            raise AttributeError("Workers are not set up.")
+        train = np.concatenate((self.training_indices, self.validation_indices))
+        genomes = []
+        for indv in population:
+            if self.snp_remover is not None:
+                genomes.append(self.snp_remover.combine_with_removed(indv.genome))
+            else:   # same sorted-unique genome the reference's empty remover yields
+                genomes.append(np.union1d(indv.genome, np.array([])).astype(int))
+        return list(self._fitness(genomes, train, self.testing_indices))
+
+
+class InterGCVBlupParallelEvaluator(BlupParallelEvaluator):
+    """Validation fold rotates with the generation (evaluator.py:434-491)."""
+
+    def __init__(self, data_path, labels_path, h2, n_procs=-1, n_folds=5, splitter=None, snp_remover=None,
+                 device=None):
+        super().__init__(data_path, labels_path, h2, n_procs=n_procs, splitter=splitter, snp_remover=snp_remover,
+                         device=device)
+        self.n_folds = n_folds
+        self.fold_indices = self.make_fold_indices(self.training_indices, self.n_folds)
+
+    @staticmethod
+    def make_fold_indices(indices, n_folds):
+        """Contiguous folds, the first len % n_folds one element longer; fold i is the
+        validation set and the others, in order, the training set (evaluator.py:454-483)."""
+        n = len(indices)
+        sizes = [n // n_folds + (1 if i < n % n_folds else 0) for i in range(n_folds)]
+        bounds = np.concatenate(([0], np.cumsum(sizes))).astype(int)
+        folds = [list(indices[bounds[i]:bounds[i + 1]]) for i in range(n_folds)]
+        out = []
+        for i in range(n_folds):
+            train = []
+            for j in range(n_folds):
+                if j != i:
+                    train += folds[j]
+            out.append([train, folds[i]])
+        return out
+
+    def train_validation_indices(self, generation):
+        return self.fold_indices[generation % self.n_folds]
+
+
+class IntraGCVBlupParallelEvaluator(InterGCVBlupParallelEvaluator):
+    """k-fold CV inside every fitness evaluation; fitness = mean over folds (evaluator.py:494-537)."""
+
+    def _evaluate(self, population, to_evaluate, indices, generation):
+        sums = {i: 0 for i in indices}
+        for k in range(self.n_folds):
+            train, valid = self.train_validation_indices(k)
+            fits = self._fitness(list(to_evaluate), train, valid) if to_evaluate else []
+            for i, f in zip(indices, fits):
+                sums[i] += f
+        for i, s in sums.items():
+            population[i].set_fitness(s / self.n_folds)
+            self.archive[population[i].uid] = population[i].fitness
+        return population
+
+
+class MonteCarloCVBlupParallelEvaluator(BlupParallelEvaluator):
+    """Fresh random 80/20 split of T u V on every _evaluate (evaluator.py:540-561)."""
+
+    def __init__(self, data_path, labels_path, h2, n_procs=-1, splitter=None, snp_remover=None, device=None):
+        super().__init__(data_path, labels_path, h2, n_procs=n_procs, splitter=splitter, snp_remover=snp_remover,
+                         device=device)
+        self.indices = np.concatenate((self.training_indices, self.validation_indices))
+
+    def train_validation_indices(self, generation):
+        from sklearn.model_selection import train_test_split
+        return train_test_split(self.indices, test_size=0.2)
+
+
+# ---------------------------------------------------------------------------
+# SNP removal (evaluator.py:569-633)
+# ---------------------------------------------------------------------------
+class SNPRemovalHandler:
+    """Removes the best individual's SNPs from evaluation once its fitness passes
+    sqrt(h2) * (1 + alpha)."""
+
+    def __init__(self, r, alpha, h2, remove_snps):
+        self.r = r
+        self.threshold = sqrt(h2) * (1 + alpha)
+        self.removed = np.array([])
+        self.remove_snps = remove_snps
+
+    def should_remove(self):
+        return self.remove_snps
+
+    def genomes_to_evaluate(self, population, archive):
+        todo, where = [], []
+        best = max(population, key=lambda x: x.fitness)
+        triggered = best.fitness > self.threshold
+        if triggered:
+            count = len(best) if self.r < len(best) else self.r
+            self.removed = np.union1d(self.removed, best.genome[-count:])
+            for key in list(archive.keys()):   # flush in place: the evaluator keeps its reference
+                del archive[key]
+        for i, indv in enumerate(population):
+            if indv.uid in archive:
+                continue
+            kept = np.setdiff1d(indv.genome, self.removed)
+            if len(kept) == 0:   # every selected SNP removed: fitness 0 without evaluation
+                archive[indv.uid] = 0.0
+                indv.set_fitness(0.0)
+            else:
+                where.append(i)
+                todo.append(kept)
+        return todo, where, triggered
+
+    def combine_with_removed(self, genome):
+        return np.union1d(genome, self.removed).astype(int)
+
+
+# ---------------------------------------------------------------------------
+# engine cache for the static blup() entry points
+# ---------------------------------------------------------------------------
+_STATIC = {}
+
+
+def _static_engine(data, labels):
+    key = (id(data), id(labels))
+    hit = _STATIC.get(key)
+    if hit is not None:
+        dref, lref, eng = hit
+        if dref() is data and lref() is labels:
+            return eng
+    from .engine import GpuBlupEngine
+    eng = GpuBlupEngine(data, labels, device=int(os.environ.get("LOCAL_RANK", "0")))
+    try:
+        dref, lref = weakref.ref(data), weakref.ref(labels)
+    except TypeError:
+        dref = lref = (lambda: None)
+    # drop engines whose arrays are gone
+    for k in [k for k, (d, l, _) in _STATIC.items() if d() is None or l() is None]:
+        _STATIC.pop(k)[2].close()
+    _STATIC[key] = (dref, lref, eng)
+    return eng

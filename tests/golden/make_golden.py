@@ -1,0 +1,335 @@
+"""Generate golden input/output vectors from the upstream reference (ianwhale/tblup).
+
+Run ONLY in the build container, where the read-only reference is mounted at
+/root/reference (it never travels to the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference is imported as a library and exercised through its own public
+functions (`tblup.utils.make_grm`, `BlupParallelEvaluator.blup/gblup/snp_blup`,
+the evaluator classes, the individual decoders, `SNPRemovalHandler`).  Predicted
+breeding values (EBVs) are not returned by the reference, so they are captured by
+wrapping `tblup.evaluator.pearsonr` (argument order differs per branch:
+gblup passes (y_V, pred_V) at evaluator.py:286, snp_blup passes (pred_V, y_V) at
+evaluator.py:314).
+
+Outputs are small .npz files next to this script: data only (inputs and expected
+outputs), no reference source.
+"""
+import os
+import sys
+import random
+import tempfile
+import hashlib
+
+import numpy as np
+
+REF = os.environ.get("TBLUP_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REF)
+sys.dont_write_bytecode = True
+
+# numpy>=1.23 removed np.asscalar, which the reference's monitor/evolver call.
+if not hasattr(np, "asscalar"):
+    np.asscalar = lambda a: a.item()
+
+import tblup  # noqa: E402  (reference package)
+import tblup.evaluator as ref_ev  # noqa: E402
+from tblup.utils import make_grm  # noqa: E402
+
+
+def synth_geno(rng, n, p, maf_lo=0.05, maf_hi=0.5):
+    maf = rng.uniform(maf_lo, maf_hi, size=p)
+    return rng.binomial(2, maf, size=(n, p)).astype(np.int8)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+class Capture:
+    """Wraps scipy.stats.pearsonr inside the reference evaluator to record EBVs."""
+
+    def __init__(self):
+        self.orig = ref_ev.pearsonr
+        self.calls = []
+
+    def __enter__(self):
+        def wrapped(a, b):
+            self.calls.append((np.array(a, dtype=np.float64), np.array(b, dtype=np.float64)))
+            return self.orig(a, b)
+        ref_ev.pearsonr = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        ref_ev.pearsonr = self.orig
+
+
+def ref_blup(indices, T, V, data, labels, h2):
+    """Calls the reference blup and returns (fitness, ebv_V, branch)."""
+    k = len(indices)
+    branch = "gblup" if k > data.shape[0] else "snp"
+    with Capture() as cap:
+        fit = ref_ev.BlupParallelEvaluator.blup(np.asarray(indices), list(T), list(V),
+                                               data.copy(), labels, h2)
+    a, b = cap.calls[-1]
+    ebv = b if branch == "gblup" else a
+    return float(fit), ebv, branch
+
+
+def gen_grm():
+    rng = np.random.default_rng(11)
+    geno = synth_geno(rng, 64, 200)
+    G = make_grm(geno.astype(np.float64))
+    # int input too (reference accepts ints for make_grm)
+    G_int = make_grm(geno.astype(np.int64))
+    np.savez_compressed(os.path.join(HERE, "grm_64x200.npz"), geno=geno, G=G, G_int=G_int)
+
+
+def make_cases(rng, n, p):
+    """Index sets covering both branches, duplicates, boundaries and ragged k."""
+    cases = []
+    cases.append(("snp_k100", rng.choice(p, 100, replace=False)))
+    cases.append(("snp_k100_b", rng.choice(p, 100, replace=False)))
+    cases.append(("snp_dup", rng.integers(0, 60, 100)))          # duplicates (IndexIndividual)
+    cases.append(("snp_k1", rng.choice(p, 1, replace=False)))
+    cases.append(("snp_k2", rng.choice(p, 2, replace=False)))
+    cases.append(("snp_k150_kernel", rng.choice(p, 150, replace=False)))  # k > n_T: sklearn kernel solver
+    cases.append(("snp_k_eq_n", rng.choice(p, n, replace=False)))  # k == n -> snp branch (strict >)
+    cases.append(("gblup_k_n_plus_1", rng.choice(p, n + 1, replace=False)))
+    cases.append(("gblup_k300", rng.choice(p, 300, replace=False)))
+    cases.append(("gblup_dup", rng.integers(0, p, 350)))
+    cases.append(("snp_sorted_desc", np.sort(rng.choice(p, 77, replace=False))[::-1].copy()))
+    return cases
+
+
+def gen_blup_small():
+    """200 animals x 1000 SNPs (BASELINE config 1 shape)."""
+    rng = np.random.default_rng(2024)
+    n, p = 200, 1000
+    geno = synth_geno(rng, n, p)
+    # a few monomorphic columns (p=0 and p=1) to exercise the p(1-p) terms
+    geno[:, 5] = 0
+    geno[:, 6] = 2
+    pheno = rng.standard_normal(n)
+    h2 = 0.4
+    data = geno.astype(np.float64)
+
+    # Split exactly as BlupParallelEvaluator.__init__ does (evaluator.py:196-203).
+    with tempfile.TemporaryDirectory() as td:
+        gp, pp = os.path.join(td, "g.npy"), os.path.join(td, "p.npy")
+        np.save(gp, data)
+        np.save(pp, pheno)
+        random.seed(0)
+        np.random.seed(0)
+        ev = ref_ev.BlupParallelEvaluator(gp, pp, h2, n_procs=1)
+        T, V, X = list(ev.training_indices), list(ev.validation_indices), list(ev.testing_indices)
+
+    out = dict(geno=geno, pheno=pheno, h2=h2, T=np.array(T), V=np.array(V), X=np.array(X))
+    names, idx_concat, offs, fits, ebvs, branches = [], [], [0], [], [], []
+    TV = T + V
+    test_fits, test_ebvs = [], []
+    for name, idx in make_cases(rng, n, p):
+        idx = np.asarray(idx, dtype=np.int64)
+        f, e, br = ref_blup(idx, T, V, data, pheno, h2)
+        ft, et, _ = ref_blup(idx, TV, X, data, pheno, h2)
+        names.append(name)
+        idx_concat.append(idx)
+        offs.append(offs[-1] + len(idx))
+        fits.append(f)
+        ebvs.append(e)
+        branches.append(br)
+        test_fits.append(ft)
+        test_ebvs.append(et)
+    out.update(names=np.array(names), idx=np.concatenate(idx_concat), offsets=np.array(offs),
+               fitness=np.array(fits), ebv=np.stack(ebvs), branch=np.array(branches),
+               test_fitness=np.array(test_fits), test_ebv=np.stack(test_ebvs))
+
+    # Other heritabilities (lambda = (1-h2)/h2) on the first snp and first gblup case.
+    h2s = np.array([0.1, 0.25, 0.7, 0.95])
+    hf = []
+    for h in h2s:
+        hf.append([ref_blup(np.asarray(idx_concat[0]), T, V, data, pheno, h)[0],
+                   ref_blup(np.asarray(idx_concat[8]), T, V, data, pheno, h)[0]])
+    out.update(h2_sweep=h2s, h2_sweep_fitness=np.array(hf))
+    np.savez_compressed(os.path.join(HERE, "blup_200x1000.npz"), **out)
+
+
+def gen_blup_edge():
+    """Degenerate inputs: all-monomorphic selections (d == 0), constant phenotype."""
+    rng = np.random.default_rng(5)
+    n, p = 200, 300
+    geno = synth_geno(rng, n, p)
+    geno[:, :10] = 1          # monomorphic heterozygous columns -> p = 0.5 (d != 0 but W == 0)
+    geno[:, 10:20] = 0        # monomorphic, p = 0 -> d == 0 when selected alone
+    pheno = rng.standard_normal(n)
+    perm = rng.permutation(n)
+    T, V = list(perm[:128]), list(perm[128:160])
+    data = geno.astype(np.float64)
+    res = {}
+    import warnings
+    for name, idx in [("mono0_snp", np.arange(10, 20)), ("mono0_gblup", np.tile(np.arange(10, 20), 21)),
+                      ("het_snp", np.arange(0, 10))]:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            try:
+                f, e, br = ref_blup(idx, T, V, data, pheno, 0.4)
+                res[name] = ("value", f)
+            except Exception as exc:  # record the reference's failure mode
+                res[name] = ("raise", type(exc).__name__)
+    np.savez_compressed(os.path.join(HERE, "blup_edge.npz"), geno=geno, pheno=pheno, T=np.array(T),
+                        V=np.array(V),
+                        names=np.array(list(res.keys())),
+                        kind=np.array([v[0] for v in res.values()]),
+                        value=np.array([str(v[1]) for v in res.values()]))
+
+
+def gen_decode():
+    """Genome decode per individual type (individual.py:93-95, 154-156, 187-237)."""
+    from tblup.individual import (IndexIndividual, RandomKeyIndividual, CoevolutionIndividual,
+                                  NullableIndexIndividual)
+    rng = np.random.default_rng(9)
+    d = 500
+    out = {}
+    keys = rng.uniform(size=(6, d))
+    keys[5, 100:140] = 0.5   # explicit ties in the keys
+    rk = [RandomKeyIndividual(37, d, genome=keys[i].copy()).genome for i in range(6)]
+    out["rk_keys"] = keys
+    out["rk_length"] = 37
+    out["rk_genome"] = np.stack(rk)
+    # float-length (coevolution lengths are floats after DE)
+    ck = CoevolutionIndividual(40, d, genome=keys[0].copy())
+    ck.set_internal_genome(np.append(keys[1].copy(), 53.7))
+    out["coev_keys"] = keys[1]
+    out["coev_length"] = ck.length
+    out["coev_genome"] = ck.genome
+    ck.set_fitness(0.5)
+    out["coev_fitness"] = ck.fitness
+    ig = rng.uniform(-20, d + 20, size=80)
+    out["index_internal"] = ig
+    out["index_genome"] = IndexIndividual(80, d, genome=ig.copy()).genome
+    out["nullable_genome"] = NullableIndexIndividual(80, d, genome=ig.copy()).genome
+    np.savez_compressed(os.path.join(HERE, "decode.npz"), **out)
+
+
+def gen_evaluator_flow():
+    """Evaluator-level flows on the 200x1000 panel: splits, CV folds, population eval,
+    SNP removal and evaluate_testing, all through the reference's own classes."""
+    from tblup.individual import RandomKeyIndividual, IndexIndividual
+    z = np.load(os.path.join(HERE, "blup_200x1000.npz"))
+    geno, pheno = z["geno"], z["pheno"]
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        gp, pp = os.path.join(td, "g.npy"), os.path.join(td, "p.npy")
+        np.save(gp, geno.astype(np.float64))
+        np.save(pp, pheno)
+
+        # --- plain BLUP evaluator, generation-0 population of RandomKey individuals ---
+        random.seed(3)
+        np.random.seed(3)
+        remover = ref_ev.SNPRemovalHandler(100, 0.0, 0.4, False)
+        ev = ref_ev.BlupParallelEvaluator(gp, pp, 0.4, n_procs=2, snp_remover=remover)
+        pop = [RandomKeyIndividual(100, 1000) for _ in range(32)]
+        out["flow_T"], out["flow_V"], out["flow_X"] = (np.array(ev.training_indices),
+                                                      np.array(ev.validation_indices),
+                                                      np.array(ev.testing_indices))
+        out["flow_keys"] = np.stack([i.get_internal_genome() for i in pop])
+        with ev:
+            ev.evaluate(pop, pop, 0)
+            out["flow_fitness"] = np.array([i.fitness for i in pop])
+            out["flow_testing"] = np.array(ev.evaluate_testing(pop))
+
+        # --- InterGCV folds + IntraGCV mean fitness ---
+        random.seed(4)
+        np.random.seed(4)
+        remover = ref_ev.SNPRemovalHandler(100, 0.0, 0.4, False)
+        iev = ref_ev.IntraGCVBlupParallelEvaluator(gp, pp, 0.4, n_procs=2, n_folds=5, snp_remover=remover)
+        out["cv_T"] = np.array(iev.training_indices)
+        folds = iev.fold_indices
+        out["cv_fold_train"] = np.concatenate([np.array(f[0]) for f in folds])
+        out["cv_fold_train_len"] = np.array([len(f[0]) for f in folds])
+        out["cv_fold_valid"] = np.concatenate([np.array(f[1]) for f in folds])
+        out["cv_fold_valid_len"] = np.array([len(f[1]) for f in folds])
+        ipop = [IndexIndividual(80, 1000) for _ in range(8)]
+        out["cv_genomes"] = np.stack([i.get_internal_genome() for i in ipop])
+        with iev:
+            iev.evaluate(ipop, ipop, 0)
+            out["cv_intra_fitness"] = np.array([i.fitness for i in ipop])
+
+        # --- MonteCarlo split sequence (numpy global RNG, evaluator.py:555-561) ---
+        random.seed(5)
+        np.random.seed(5)
+        mev = ref_ev.MonteCarloCVBlupParallelEvaluator(gp, pp, 0.4, n_procs=1, snp_remover=remover)
+        seq = [mev.train_validation_indices(g) for g in range(3)]
+        out["mc_T"] = np.array(mev.training_indices)
+        out["mc_V"] = np.array(mev.validation_indices)
+        out["mc_split_train"] = np.array([np.array(s[0]) for s in seq])
+        out["mc_split_valid"] = np.array([np.array(s[1]) for s in seq])
+
+        # --- SNP removal: threshold 0 forces removal of the best individual's SNPs ---
+        random.seed(6)
+        np.random.seed(6)
+        remover = ref_ev.SNPRemovalHandler(30, -1.0, 0.4, True)   # threshold = sqrt(h2)*0 = 0
+        rev = ref_ev.BlupParallelEvaluator(gp, pp, 0.4, n_procs=2, snp_remover=remover)
+        prev = [RandomKeyIndividual(60, 1000) for _ in range(10)]
+        for i, ind in enumerate(prev):
+            ind.set_fitness(0.01 * i)           # individual 9 is "best"
+        nxt = [RandomKeyIndividual(60, 1000) for _ in range(10)]
+        for i, ind in enumerate(nxt):
+            ind.set_fitness(0.02 * ((i * 7) % 10))   # offspring carry a (deep-copied) parent fitness
+
+        class _Mon:
+            def log_snp_removal_event(self, g):
+                pass
+
+        class _Pop(list):
+            monitor = _Mon()
+
+        prev_pop = _Pop(prev)
+        out["rm_T"], out["rm_V"], out["rm_X"] = (np.array(rev.training_indices),
+                                                np.array(rev.validation_indices),
+                                                np.array(rev.testing_indices))
+        out["rm_prev_keys"] = np.stack([i.get_internal_genome() for i in prev])
+        out["rm_next_keys"] = np.stack([i.get_internal_genome() for i in nxt])
+        with rev:
+            rev.evaluate(prev_pop, nxt, 1)
+            out["rm_removed"] = np.array(remover.removed)
+            out["rm_next_fitness"] = np.array([i.fitness for i in nxt])
+            out["rm_prev_fitness"] = np.array([i.fitness for i in prev_pop])
+            out["rm_testing"] = np.array(rev.evaluate_testing(nxt))
+    np.savez_compressed(os.path.join(HERE, "evaluator_flow.npz"), **out)
+
+
+def gen_blup_config2():
+    """Config-2 shape (2000 animals, panel k=1000) on a 4000-SNP synthetic panel.
+    The genotype matrix is regenerated in tests from the seed; its sha256 is pinned."""
+    seed = 77
+    rng = np.random.default_rng(seed)
+    n, p = 2000, 4000
+    geno = synth_geno(rng, n, p)
+    pheno = rng.standard_normal(n)
+    perm = np.random.default_rng(seed + 1).permutation(n)
+    T, V = perm[:1280], perm[1280:1600]
+    data = geno.astype(np.float64)
+    sel = np.random.default_rng(seed + 2)
+    cases = [sel.choice(p, 1000, replace=False) for _ in range(3)] + [sel.choice(p, 2100, replace=False)]
+    fits, ebvs, offs = [], [], [0]
+    for idx in cases:
+        f, e, _ = ref_blup(idx, T, V, data, pheno, 0.4)
+        fits.append(f)
+        ebvs.append(e)
+        offs.append(offs[-1] + len(idx))
+    np.savez_compressed(os.path.join(HERE, "blup_2000x4000.npz"), seed=seed, n=n, p=p,
+                        geno_sha256=sha(geno), pheno=pheno, T=T, V=V,
+                        idx=np.concatenate(cases), offsets=np.array(offs),
+                        fitness=np.array(fits), ebv=np.stack(ebvs[:3]), ebv_gblup=ebvs[3])
+
+
+if __name__ == "__main__":
+    gen_grm()
+    gen_blup_small()
+    gen_blup_edge()
+    gen_decode()
+    gen_evaluator_flow()
+    gen_blup_config2()
+    print("golden fixtures written to", HERE)

@@ -1,0 +1,52 @@
+"""C-ABI library checks that need no GPU: it loads and exports every declared symbol."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from tblup_amd import _native
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "tblup_gpu.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tblup_[a-z_]+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = _native.load()
+    names = declared_functions()
+    assert len(names) >= 14
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(names) == set(_native.SIGNATURES), "ctypes signature table out of sync with the header"
+
+
+def test_version_and_error_strings():
+    lib = _native.load()
+    assert lib.tblup_version().startswith(b"tblup_gpu")
+    assert isinstance(lib.tblup_last_error(), bytes)
+
+
+def test_device_count_without_gpu_does_not_crash():
+    assert _native.device_count() >= 0
+
+
+def test_bad_arguments_return_status_not_crash():
+    lib = _native.load()
+    out = ctypes.c_void_p()
+    rc = lib.tblup_ctx_create(None, 10, 10, 0, None, 0, ctypes.byref(out))
+    assert rc == -1
+    assert b"bad" in lib.tblup_last_error()
+    assert lib.tblup_ctx_destroy(None) == 0
+    assert lib.tblup_set_split(None, 0, None, 0, None, 0) == -1
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(ImportError):
+        _native.load()

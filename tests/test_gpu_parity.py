@@ -1,0 +1,216 @@
+"""GPU parity: the HIP pipeline (through the C ABI) against the reference goldens and the oracle.
+
+Tolerances (north star: EBVs within 1e-5 relative of the numpy reference):
+  * GRM block K_{R,T}: max |dK| <= 1e-12 * max |K| (exact-integer A A^T + fp64 centring)
+  * Cholesky factor / forward solve: <= 1e-10 relative
+  * EBV_V: max |dEBV| <= 1e-9 * max |EBV| (well inside the 1e-5 bar); fitness |df| <= 1e-9
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle import blup_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EBV_RTOL = 1e-9
+FIT_ATOL = 1e-9
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def _cases(z):
+    return [(str(z["names"][i]), z["idx"][z["offsets"][i]:z["offsets"][i + 1]]) for i in range(len(z["names"]))]
+
+
+@pytest.fixture(scope="module")
+def small(golden_dir, gpu):
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_200x1000.npz")
+    eng = GpuBlupEngine(z["geno"], z["pheno"], device=0)
+    yield z, eng
+    eng.close()
+
+
+def _relmax(a, b):
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def test_grm_block_matches_oracle(small):
+    z, eng = small
+    T, V, g = z["T"], z["V"], z["geno"]
+    lam = (1 - 0.4) / 0.4
+    for name, idx in _cases(z):
+        K, _ = eng.debug_grm(idx, T, V, 0.4, stage=1)
+        ref = O.grm_block(idx, T, V, g)
+        ref[np.arange(len(T)), np.arange(len(T))] += lam
+        assert _relmax(K, ref) <= 1e-12, name
+
+
+def test_cholesky_factor_and_forward_solve(small):
+    z, eng = small
+    T, V, g, y = z["T"], z["V"], z["geno"], z["pheno"]
+    lam = (1 - 0.4) / 0.4
+    nT = len(T)
+    for name, idx in _cases(z):
+        F, zz = eng.debug_grm(idx, T, V, 0.4, stage=2)
+        K = O.grm_block(idx, T, V, g)[:nT]
+        K[np.arange(nT), np.arange(nT)] += lam
+        L = np.linalg.cholesky(K)
+        assert _relmax(np.tril(F[:nT]), L) <= 1e-10, name
+        branch = "gblup" if len(idx) > g.shape[0] else "snp"
+        mu = 0.0 if branch == "gblup" else float(np.mean(y[T]))
+        zref = np.linalg.solve(L, y[T] - mu)
+        assert _relmax(zz, zref) <= 1e-10, name
+
+
+def test_fitness_and_ebv_vs_reference_goldens(small):
+    """All cases in ONE ragged batch: mixed k, duplicates, both branches."""
+    z, eng = small
+    genomes = [idx for _, idx in _cases(z)]
+    fit, ebv = eng.evaluate(genomes, z["T"], z["V"], float(z["h2"]), return_ebv=True)
+    for i, (name, _) in enumerate(_cases(z)):
+        assert abs(fit[i] - z["fitness"][i]) <= FIT_ATOL, name
+        assert _relmax(ebv[i], z["ebv"][i]) <= EBV_RTOL, name
+
+
+def test_testing_split_goldens(small):
+    z, eng = small
+    genomes = [idx for _, idx in _cases(z)]
+    TV = np.concatenate([z["T"], z["V"]])
+    fit, ebv = eng.evaluate(genomes, TV, z["X"], float(z["h2"]), return_ebv=True)
+    for i, (name, _) in enumerate(_cases(z)):
+        assert abs(fit[i] - z["test_fitness"][i]) <= FIT_ATOL, name
+        assert _relmax(ebv[i], z["test_ebv"][i]) <= EBV_RTOL, name
+
+
+def test_h2_sweep(small):
+    z, eng = small
+    c = _cases(z)
+    for h, (fs, fg) in zip(z["h2_sweep"], z["h2_sweep_fitness"]):
+        f = eng.evaluate([c[0][1], c[8][1]], z["T"], z["V"], float(h))
+        assert abs(f[0] - fs) <= FIT_ATOL and abs(f[1] - fg) <= FIT_ATOL
+
+
+def test_forced_branches_match_oracle(small):
+    z, eng = small
+    g, y, T, V = z["geno"].astype(np.float64), z["pheno"], z["T"], z["V"]
+    idx = _cases(z)[0][1]
+    f_g = eng.evaluate([idx], T, V, 0.4, branch="gblup")[0]
+    f_s = eng.evaluate([idx], T, V, 0.4, branch="snp")[0]
+    assert abs(f_g - O.gblup(idx, T, V, g, y, 0.4)) <= FIT_ATOL
+    assert abs(f_s - O.snp_blup(idx, T, V, g, y, 0.4)) <= FIT_ATOL
+
+
+def test_degenerate_panels_give_nan(golden_dir, gpu):
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_edge.npz")
+    with GpuBlupEngine(z["geno"], z["pheno"]) as eng:
+        sel = [np.arange(10, 20), np.tile(np.arange(10, 20), 21), np.arange(0, 10)]
+        f = eng.evaluate(sel, z["T"], z["V"], 0.4)
+        assert np.all(np.isnan(f)), f
+
+
+def test_config2_shape_golden(golden_dir, gpu):
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_2000x4000.npz")
+    geno = O.synth_geno(np.random.default_rng(int(z["seed"])), int(z["n"]), int(z["p"]))
+    assert hashlib.sha256(geno.tobytes()).hexdigest() == str(z["geno_sha256"])
+    genomes = [z["idx"][z["offsets"][i]:z["offsets"][i + 1]] for i in range(len(z["offsets"]) - 1)]
+    with GpuBlupEngine(geno, z["pheno"]) as eng:
+        fit, ebv = eng.evaluate(genomes, z["T"], z["V"], 0.4, return_ebv=True)
+    for i in range(4):
+        assert abs(fit[i] - z["fitness"][i]) <= FIT_ATOL
+        ref = z["ebv"][i] if i < 3 else z["ebv_gblup"]
+        assert _relmax(ebv[i], ref) <= EBV_RTOL
+
+
+def test_chunked_workspace_is_identical(golden_dir, gpu, monkeypatch):
+    """A tiny workspace budget forces many chunks; results must be bit-identical."""
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_200x1000.npz")
+    genomes = [idx for _, idx in _cases(z)] * 3
+    with GpuBlupEngine(z["geno"], z["pheno"]) as eng:
+        ref = eng.evaluate(genomes, z["T"], z["V"], 0.4)
+    monkeypatch.setenv("TBLUP_WORKSPACE_MB", "1")
+    with GpuBlupEngine(z["geno"], z["pheno"]) as eng:
+        got = eng.evaluate(genomes, z["T"], z["V"], 0.4)
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_device_pointer_path_matches_host_path(small):
+    import torch
+    z, eng = small
+    genomes = [idx for _, idx in _cases(z)]
+    ref = eng.evaluate(genomes, z["T"], z["V"], 0.4)
+    from tblup_amd.engine import concat_genomes
+    idx, off = concat_genomes(genomes)
+    sid = eng.split_id(z["T"], z["V"])
+    d_idx = torch.from_numpy(idx).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    d_fit = torch.empty(len(genomes), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream()
+    eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(),
+                        stream_ptr=stream.cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_fit.cpu().numpy(), ref)
+
+
+# ---------------------------------------------------------------------------
+# Full BASELINE config-2 size: 2000 animals x 50k SNPs, k = 1000, 256 individuals
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def config2(gpu):
+    from tblup_amd.engine import GpuBlupEngine
+    rng = np.random.default_rng(2)
+    n, P = 2000, 50_000
+    geno = O.synth_geno(rng, n, P)
+    pheno = rng.standard_normal(n)
+    perm = np.random.default_rng(3).permutation(n)
+    T, V = perm[:1280], perm[1280:1600]
+    keys = np.random.default_rng(4).uniform(size=(256, P))
+    genomes = [O.decode_randkeys(k, 1000) for k in keys]
+    eng = GpuBlupEngine(geno, pheno)
+    fit, ebv = eng.evaluate(genomes, T, V, 0.4, return_ebv=True)
+    yield dict(geno=geno, pheno=pheno, T=T, V=V, genomes=genomes, fit=fit, ebv=ebv, eng=eng)
+    eng.close()
+
+
+def test_config2_sample_vs_oracle(config2):
+    c = config2
+    for i in (0, 1, 77, 128, 200, 255):
+        f, e = O.blup_grm_form(c["genomes"][i], c["T"], c["V"], c["geno"], c["pheno"], 0.4)
+        assert abs(c["fit"][i] - f) <= FIT_ATOL
+        assert _relmax(c["ebv"][i], e) <= EBV_RTOL
+
+
+def test_config2_properties(config2):
+    """Size-independent properties at full size: determinism, batch independence,
+    invariance to index order, finite fitness in [0, 1]."""
+    c = config2
+    eng = c["eng"]
+    assert np.all(np.isfinite(c["fit"])) and np.all((c["fit"] >= 0) & (c["fit"] <= 1))
+    again = eng.evaluate(c["genomes"], c["T"], c["V"], 0.4)
+    np.testing.assert_array_equal(again, c["fit"])
+    alone = eng.evaluate([c["genomes"][5]], c["T"], c["V"], 0.4)
+    assert alone[0] == c["fit"][5]
+    rng = np.random.default_rng(9)
+    shuffled = [rng.permutation(c["genomes"][i]) for i in range(8)]
+    f = eng.evaluate(shuffled, c["T"], c["V"], 0.4)
+    np.testing.assert_allclose(f, c["fit"][:8], rtol=0, atol=1e-12)
+
+
+def test_config2_gblup_branch_sample(config2):
+    """k > n at config-2 size: the GBLUP branch (p over all n animals, no y centring)."""
+    c = config2
+    rng = np.random.default_rng(11)
+    genomes = [rng.choice(50_000, 2500, replace=False) for _ in range(3)]
+    fit, ebv = c["eng"].evaluate(genomes, c["T"], c["V"], 0.4, return_ebv=True)
+    for i, g in enumerate(genomes):
+        f, e = O.blup_grm_form(g, c["T"], c["V"], c["geno"], c["pheno"], 0.4)
+        assert abs(fit[i] - f) <= FIT_ATOL
+        assert _relmax(ebv[i], e) <= EBV_RTOL
