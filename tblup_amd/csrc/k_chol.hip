@@ -22,7 +22,6 @@ namespace {
 
 constexpr int BKD = 16;               // fp64 K step (128 B per row)
 constexpr int STAGE = TILE * BKD;     // doubles per operand stage
-constexpr int TS = 144;               // row stride (doubles) of the diag kernel's LDS tile
 
 __device__ __forceinline__ int st_off(int row, int k) {
   // [128 rows][16 doubles]; 16-B chunk c=k>>1 of row r stored at c ^ ((r>>1)&7):
@@ -101,104 +100,98 @@ struct NoStage {
   __device__ void operator()(const double*, int) const {}
 };
 
-struct ElimState {
-  double (&v)[8][8];
-  double (&rv)[8];
-  double (*colbuf)[TILE];
-  double (*erow)[TILE];
-  double* rbuf;
-  double* pivs;
-  double* Kb;
-  int64_t nTp, j0;
-  int t, tr, tc;
-};
+// ---- packed lower-triangular 16x16 block storage of a 128x128 tile in LDS ----
+constexpr int NB = 16;                       // base block edge
+constexpr int NBLK = TILE / NB;              // 8 block rows
+constexpr int NPACK = NBLK * (NBLK + 1) / 2; // 36 lower blocks
+constexpr int BLKD = NB * NB;                // doubles per block
 
-// Steps j = 16*JB .. 16*JB+15 of the in-register elimination of the diagonal
-// tile.  Thread (tr, tc) owns elements (tr + 16a, tc + 16bb); JB is a
-// template parameter so every register index is static.  Element (i,c), i >= c:
-//   c > j : Schur update  T_ic -= T_ij T_cj / piv_j
-//   c == j: becomes E_ij = -T_ij/piv_j (i > j) or 1 (i == j)   [E = L'^{-1}]
-//   c < j : E_ic -= (T_ij/piv_j) E_jc
-// L column j (= T_ij / sqrt(piv_j)) is written to K as it is published; the
-// right-hand side r is eliminated alongside (forward substitution).
-template <int JB>
-__device__ __forceinline__ void elim_block(ElimState& S) {
-  double(&v)[8][8] = S.v;
-  double(&rv)[8] = S.rv;
-  const int tr = S.tr, tc = S.tc;
-  for (int jj = 0; jj < 16; ++jj) {
-    const int j = 16 * JB + jj;
-    const int buf = j & 1;
-    if (tc == jj) {
+__device__ __forceinline__ int pk(int q, int s) { return (q * (q + 1) / 2 + s) * BLKD; }
+// element (r, c) of a 16x16 block; 16-B chunk swizzle makes the fragment reads conflict-free
+__device__ __forceinline__ int bo(int r, int c) { return r * NB + 2 * ((c >> 1) ^ ((r >> 1) & 7)) + (c & 1); }
+
+// acc (16x16, f64 MFMA C layout) += A(16x16) * B(16x16)^T, both blocks in LDS
+__device__ __forceinline__ v4d mma_abt(const double* A, const double* Bt, v4d acc, int l) {
 #pragma unroll
-      for (int a = JB; a < 8; ++a) {
-        const int i = tr + 16 * a;
-        if (i >= j) S.colbuf[buf][i] = v[a][JB];
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 4 * kk + (l >> 4);
+    acc = mfma64(A[bo(l & 15, k)], Bt[bo(l & 15, k)], acc);
+  }
+  return acc;
+}
+
+// Factor the 16x16 SPD block D in place with ONE wave (no barriers): D <- L (lower),
+// X <- L^{-1} (lower, zeros above).  Lane l holds row i = l&15, columns 4g..4g+3
+// (g = l>>4).  Right-looking elimination with unscaled pivots; a column, once
+// eliminated, turns into the matching column of E = L'^{-1} (row operations on I):
+//   c > j : T_ic -= T_ij T_cj / piv_j
+//   c == j: E_ij = -T_ij / piv_j (i > j), 1 (i == j)
+//   c < j : E_ic -= (T_ij / piv_j) E_jc
+// L = L' D^{1/2}  ->  L_ij = T_ij / sqrt(piv_j);  X = D^{-1/2} E.
+__device__ __forceinline__ void factor16(double* D, double* X, int l) {
+  const int i = l & 15, g = l >> 4;
+  double v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = D[bo(i, 4 * g + q)];
+  double piv_own = 1.0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int jg = j >> 2, jq = j & 3;
+    const double ci = __shfl(v[jq], i + 16 * jg);
+    const double piv = __shfl(v[jq], j + 16 * jg);
+    double cc[4], ej[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cc[q] = __shfl(v[jq], 4 * g + q + 16 * jg);
+      ej[q] = __shfl(v[q], j + 16 * g);
+    }
+    if (g == jg && i >= j) D[bo(i, j)] = ci / sqrt(piv);
+    if (i == j) piv_own = piv;
+    const double li = ci / piv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * g + q;
+      if (c > j) {
+        if (i >= c) v[q] -= li * cc[q];
+      } else if (c == j) {
+        if (i >= j) v[q] = (i == j) ? 1.0 : -li;
+      } else {
+        if (i > j) v[q] -= li * ej[q];
       }
     }
-    if (tr == jj) {
+  }
+  const double rs = 1.0 / sqrt(piv_own);
 #pragma unroll
-      for (int bb = 0; bb <= JB; ++bb) {
-        const int c = tc + 16 * bb;
-        if (c < j) S.erow[buf][c] = v[JB][bb];
-      }
-      if (tc == 15) S.rbuf[buf] = rv[JB];
-    }
-    __syncthreads();
-    const double piv = S.colbuf[buf][j];
-    const double ip = 1.0 / piv;
-    const double rj = S.rbuf[buf];
-    if (S.t == 0) S.pivs[j] = piv;
-    if (tc == jj) {
-      const double rs = 1.0 / sqrt(piv);
-#pragma unroll
-      for (int a = JB; a < 8; ++a) {
-        const int i = tr + 16 * a;
-        if (i >= j) S.Kb[(S.j0 + i) * S.nTp + S.j0 + j] = v[a][JB] * rs;
-      }
-    }
-#pragma unroll
-    for (int a = JB; a < 8; ++a) {
-      const int i = tr + 16 * a;
-      const double li = (i >= j) ? S.colbuf[buf][i] * ip : 0.0;
-#pragma unroll
-      for (int bb = 0; bb < 8; ++bb) {
-        const int c = tc + 16 * bb;
-        if (bb > JB) {
-          if (i >= c) v[a][bb] -= li * S.colbuf[buf][c];
-        } else if (bb == JB) {
-          if (c > j) {
-            if (i >= c) v[a][bb] -= li * S.colbuf[buf][c];
-          } else if (c == j) {
-            if (i >= j) v[a][bb] = (i == j) ? 1.0 : -li;
-          } else {
-            if (i > j) v[a][bb] -= li * S.erow[buf][c];
-          }
-        } else {
-          if (i > j) v[a][bb] -= li * S.erow[buf][c];
-        }
-      }
-      if (tc == 15 && i > j) rv[a] -= li * rj;
-    }
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * g + q;
+    X[bo(i, c)] = (i >= c) ? v[q] * rs : 0.0;
   }
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// diagonal tile: SYRK update, factorisation, inverse and forward substitution
+// diagonal tile: SYRK update, blocked factorisation, blocked inverse, forward solve
 // ---------------------------------------------------------------------------
+//   A. acc = sum_{L<J} L_JL L_JL^T (fp64 MFMA), w = sum_{L<J} L_JL z_L (fused)
+//   B. T = A_JJ - acc -> LDS, packed lower 16x16 blocks; r = y_J - mu - w
+//   C. for panel p: one wave factors T_pp (-> L_pp, X_pp = L_pp^{-1});
+//      all waves: L_qp = T_qp X_pp^T (q > p); T_qs -= L_qp L_sp^T (q >= s > p)   [MFMA]
+//   D. blocked inverse X = L^{-1}: X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
+//   E. write L (lower blocks) to K, X to Dinv (zeros above the diagonal), z_J = X r
 __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, int64_t nTp, int64_t nT, int64_t mstride,
                                                    int J, double* __restrict__ Dinv, double* __restrict__ z,
                                                    const double* __restrict__ yT, const double* __restrict__ scal) {
-  __shared__ __attribute__((aligned(16))) double lds[TILE * TS];  // 144 KiB: staging, then the T tile
-  __shared__ double colbuf[2][TILE], erow[2][TILE], rbuf[2], pivs[TILE], rsh[TILE], wsh[TILE];
+  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];  // 144 KiB: staging, then T and X blocks
+  __shared__ double rsh[TILE];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
   const int64_t b = blockIdx.x;
   double* Kb = K + b * mstride;
   const int64_t j0 = (int64_t)J * TILE;
   const double* zb = z + b * nTp;
   const double mu = scal[b * 8 + 3];
+  double* Tp = lds;
+  double* Xp = lds + NPACK * BLKD;
 
   v4d acc[4][4];
 #pragma unroll
@@ -206,7 +199,6 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, int64
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = v4d{0.0, 0.0, 0.0, 0.0};
 
-  // forward-substitution partial sums w_i = sum_{k<j0} L[j0+i][k] z[k], fused into the staging loop
   double wpart = 0.0;
   auto on_stage = [&](const double* As, int k0) {
     if (t < TILE) {
@@ -217,58 +209,99 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, int64
   if (J > 0) gemm_nt_f64<true>(Kb + j0 * nTp, Kb + j0 * nTp, nTp, (int)j0, acc, lds, on_stage);
   __syncthreads();
 
-  // T = A_JJ - acc  -> LDS (stride TS); r = y_J - mu - w
+  // B. lower blocks of T = A_JJ - acc (wave (wr,wc) holds block rows 4wr+m, block cols 4wc+n)
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < 4; ++n) {
+      const int q = 4 * wr + m, sb = 4 * wc + n;
+      if (q >= sb) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 64 * wr + 16 * m + (l >> 4) + 4 * r, col = 64 * wc + 16 * n + (l & 15);
-        lds[row * TS + col] = Kb[(j0 + row) * nTp + j0 + col] - acc[m][n][r];
+        for (int r = 0; r < 4; ++r) {
+          const int rr = (l >> 4) + 4 * r, cc = l & 15;
+          Tp[pk(q, sb) + bo(rr, cc)] = Kb[(j0 + 16 * q + rr) * nTp + j0 + 16 * sb + cc] - acc[m][n][r];
+        }
       }
+    }
   if (t < TILE) {
     const int64_t gi = j0 + t;
-    wsh[t] = wpart;
     rsh[t] = (gi < nT) ? (yT[gi] - mu - wpart) : 0.0;
   }
   __syncthreads();
 
-  // ownership: thread (tr, tc) holds elements (tr + 16a, tc + 16bb)
-  const int tr = t >> 4, tc = t & 15;
-  double v[8][8];
-  double rv[8];
+  // C. blocked right-looking factorisation over 16-column panels
+  for (int p = 0; p < NBLK; ++p) {
+    if (w == 0) factor16(Tp + pk(p, p), Xp + pk(p, p), l);
+    __syncthreads();
+    // panel solve L_qp = T_qp X_pp^T
+    for (int q = p + 1 + w; q < NBLK; q += 4) {
+      v4d a = {0.0, 0.0, 0.0, 0.0};
+      a = mma_abt(Tp + pk(q, p), Xp + pk(p, p), a, l);
 #pragma unroll
-  for (int a = 0; a < 8; ++a) {
+      for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = a[r];
+    }
+    __syncthreads();
+    // trailing update T_qs -= L_qp L_sp^T for q >= s > p
+    const int nb = NBLK - 1 - p;
+    for (int e = w; e < nb * (nb + 1) / 2; e += 4) {
+      int qq = 0;
+      while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
+      const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
+      v4d a = {0.0, 0.0, 0.0, 0.0};
+      a = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), a, l);
+      double* dst = Tp + pk(q, sb);
 #pragma unroll
-    for (int bb = 0; bb < 8; ++bb) v[a][bb] = lds[(tr + 16 * a) * TS + tc + 16 * bb];
-    rv[a] = rsh[tr + 16 * a];
+      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= a[r];
+    }
+    __syncthreads();
   }
 
-  // Right-looking elimination with unscaled pivots (see elim_block).
-  ElimState st{v, rv, colbuf, erow, rbuf, pivs, Kb, nTp, j0, t, tr, tc};
-  elim_block<0>(st);
-  elim_block<1>(st);
-  elim_block<2>(st);
-  elim_block<3>(st);
-  elim_block<4>(st);
-  elim_block<5>(st);
-  elim_block<6>(st);
-  elim_block<7>(st);
-  __syncthreads();
-
-  // X = L^{-1} = D^{-1/2} E ; z_J = D^{-1/2} r
-  double* Db = Dinv + (b * (nTp / TILE) + J) * (int64_t)(TILE * TILE);
+  // D. blocked inverse, one block diagonal per round
+  for (int dd = 1; dd < NBLK; ++dd) {
+    for (int jb = w; jb + dd < NBLK; jb += 4) {
+      const int q = jb + dd;
+      v4d sacc = {0.0, 0.0, 0.0, 0.0};
+      for (int lb = jb; lb < q; ++lb) {
+        // S += L_{q,lb} X_{lb,jb}:  B[k][c] = X_{lb,jb}[k][c]
+        const double* A = Tp + pk(q, lb);
+        const double* Xb = Xp + pk(lb, jb);
 #pragma unroll
-  for (int a = 0; a < 8; ++a) {
-    const int i = tr + 16 * a;
-    const double rs = 1.0 / sqrt(pivs[i]);
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * kk + (l >> 4);
+          sacc = mfma64(A[bo(l & 15, k)], Xb[bo(k, l & 15)], sacc);
+        }
+      }
+      // X_{q,jb} = -X_{q,q} S ; S in C layout feeds the B operand directly (k = 4kk + (l>>4))
+      v4d xo = {0.0, 0.0, 0.0, 0.0};
+      const double* Xqq = Xp + pk(q, q);
 #pragma unroll
-    for (int bb = 0; bb < 8; ++bb) {
-      const int c = tc + 16 * bb;
-      Db[i * TILE + c] = (i >= c) ? v[a][bb] * rs : 0.0;
+      for (int kk = 0; kk < 4; ++kk) xo = mfma64(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Xp[pk(q, jb) + bo((l >> 4) + 4 * r, l & 15)] = -xo[r];
     }
-    if (tc == 15) z[b * nTp + j0 + i] = rv[a] * rs;
+    __syncthreads();
+  }
+
+  // E. outputs
+  double* Db = Dinv + (b * (nTp / TILE) + J) * (int64_t)(TILE * TILE);
+  for (int e = t; e < TILE * TILE; e += 256) {
+    const int rr = e >> 7, cc = e & 127, q = rr >> 4, sb = cc >> 4;
+    double xv = 0.0;
+    if (q >= sb) {
+      xv = Xp[pk(q, sb) + bo(rr & 15, cc & 15)];
+      if (rr >= cc) Kb[(j0 + rr) * nTp + j0 + cc] = Tp[pk(q, sb) + bo(rr & 15, cc & 15)];
+    }
+    Db[e] = xv;
+  }
+  if (t < TILE) {
+    const int q = t >> 4;
+    double acc_z = 0.0;
+    for (int sb = 0; sb <= q; ++sb) {
+      const double* Xb = Xp + pk(q, sb);
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc_z += Xb[bo(t & 15, c)] * rsh[16 * sb + c];
+    }
+    z[b * nTp + j0 + t] = acc_z;
   }
 }
 

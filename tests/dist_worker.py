@@ -1,0 +1,42 @@
+"""Worker for tests/test_distributed.py (world_size 2, gloo, CPU)."""
+import json
+import os
+import sys
+
+
+def run(rank, world, port, gp, pp, keys_path, out_dir):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import random
+
+    import numpy as np
+    import torch.distributed as dist
+
+    from tblup_amd import evaluator as E
+    from tblup_amd.distributed import shard_range
+    from tests.helpers import KeyIndividual, OracleEngine
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    random.seed(3)
+    np.random.seed(3)
+    ev = E.BlupParallelEvaluator(gp, pp, 0.4, snp_remover=E.SNPRemovalHandler(100, 0.0, 0.4, False))
+    eng = OracleEngine(np.load(gp), np.load(pp))
+    seen = []
+    orig = eng.evaluate
+
+    def spy(genomes, *a, **k):
+        seen.append(len(genomes))
+        return orig(genomes, *a, **k)
+
+    eng.evaluate = spy
+    ev.engine = eng
+    keys = np.load(keys_path)
+    pop = [KeyIndividual(k, 100) for k in keys]
+    ev.evaluate(pop, pop, 0)
+    testing = ev.evaluate_testing(pop)
+    lo, hi = shard_range(len(pop), rank, world)
+    json.dump({"fitness": [float(p.fitness) for p in pop], "testing": [float(x) for x in testing],
+               "evaluated": seen, "shard": [lo, hi]}, open(os.path.join(out_dir, f"rank{rank}.json"), "w"))
+    dist.barrier()
+    dist.destroy_process_group()

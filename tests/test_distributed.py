@@ -1,0 +1,52 @@
+"""Multi-process population sharding + fitness all-gather (world_size 2, gloo backend on CPU)."""
+import json
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from tblup_amd.distributed import shard_range
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 32, 33):
+        for ws in (1, 2, 3, 8):
+            spans = [shard_range(n, r, ws) for r in range(ws)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_two_rank_gloo_matches_single_process(golden_dir, tmp_path):
+    from tests import dist_worker
+    z = np.load(os.path.join(golden_dir, "blup_200x1000.npz"))
+    flow = np.load(os.path.join(golden_dir, "evaluator_flow.npz"))
+    gp, pp, kp = str(tmp_path / "g.npy"), str(tmp_path / "p.npy"), str(tmp_path / "k.npy")
+    np.save(gp, z["geno"].astype(np.float64))
+    np.save(pp, z["pheno"])
+    keys = flow["flow_keys"][:31]          # odd count: uneven shards
+    np.save(kp, keys)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=dist_worker.run, args=(r, 2, port, gp, pp, kp, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    expect = flow["flow_fitness"][:31]
+    for r in range(2):
+        np.testing.assert_allclose(res[r]["fitness"], expect, rtol=0, atol=1e-12)
+        lo, hi = res[r]["shard"]
+        assert res[r]["evaluated"][0] == hi - lo      # each rank computed only its own block
+    assert res[0]["testing"] == res[1]["testing"]
+    np.testing.assert_allclose(res[0]["testing"], flow["flow_testing"][:31], rtol=0, atol=1e-12)

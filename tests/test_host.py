@@ -1,0 +1,188 @@
+"""Host-side evaluator logic (no GPU): splits, CV folds, archive, SNP removal,
+testing evaluation — checked against flows recorded from the reference evaluator
+(tests/golden/evaluator_flow.npz).  Compute goes through tests.helpers.OracleEngine,
+a test-only stand-in with GpuBlupEngine's evaluate() contract."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from tests.helpers import IdxIndividual, KeyIndividual, OracleEngine
+from tblup_amd import evaluator as E
+
+
+@pytest.fixture(scope="module")
+def panel(golden_dir, tmp_path_factory):
+    z = np.load(os.path.join(golden_dir, "blup_200x1000.npz"))
+    d = tmp_path_factory.mktemp("panel")
+    gp, pp = str(d / "geno.npy"), str(d / "pheno.npy")
+    np.save(gp, z["geno"].astype(np.float64))
+    np.save(pp, z["pheno"])
+    return gp, pp, z
+
+
+@pytest.fixture(scope="module")
+def flow(golden_dir):
+    return np.load(os.path.join(golden_dir, "evaluator_flow.npz"))
+
+
+def _enter_with_oracle(ev, gp, pp):
+    ev.engine = OracleEngine(np.load(gp), np.load(pp))
+    return ev
+
+
+def test_default_split_reproduces_reference(panel):
+    gp, pp, z = panel
+    random.seed(0)
+    np.random.seed(0)
+    ev = E.BlupParallelEvaluator(gp, pp, 0.4, n_procs=1)
+    np.testing.assert_array_equal(ev.training_indices, z["T"])
+    np.testing.assert_array_equal(ev.validation_indices, z["V"])
+    np.testing.assert_array_equal(ev.testing_indices, z["X"])
+    assert (len(ev.training_indices), len(ev.validation_indices), len(ev.testing_indices)) == (128, 32, 40)
+
+
+def test_split_disjoint_like_reference_unit_test(tmp_path):
+    """tblup/test/evaluator.py:25-39: train/valid/test duplicate-free and disjoint."""
+    gp, pp = str(tmp_path / "g.npy"), str(tmp_path / "p.npy")
+    np.save(gp, np.random.randint(0, 2, (100, 100)))
+    np.save(pp, np.random.rand(100))
+    ev = E.BlupParallelEvaluator(gp, pp, 0.5)
+    tr, va, te = set(ev.training_indices), set(ev.validation_indices), set(ev.testing_indices)
+    assert len(tr) == len(ev.training_indices) and len(va) == len(ev.validation_indices)
+    assert len(te) == len(ev.testing_indices)
+    assert not (tr & va) and not (tr & te) and not (va & te)
+
+
+def test_generation0_population_and_testing(panel, flow):
+    gp, pp, _ = panel
+    random.seed(3)
+    np.random.seed(3)
+    rem = E.SNPRemovalHandler(100, 0.0, 0.4, False)
+    ev = E.BlupParallelEvaluator(gp, pp, 0.4, n_procs=2, snp_remover=rem)
+    np.testing.assert_array_equal(ev.training_indices, flow["flow_T"])
+    np.testing.assert_array_equal(ev.testing_indices, flow["flow_X"])
+    pop = [KeyIndividual(k, 100) for k in flow["flow_keys"]]
+    _enter_with_oracle(ev, gp, pp)
+    ev.evaluate(pop, pop, 0)
+    np.testing.assert_allclose([p.fitness for p in pop], flow["flow_fitness"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(ev.evaluate_testing(pop), flow["flow_testing"], rtol=0, atol=1e-12)
+    # archive hit: a second evaluate computes nothing new
+    calls = ev.engine.calls
+    ev.evaluate(pop, pop, 1)
+    assert ev.engine.calls == calls
+
+
+def test_evaluate_requires_context():
+    ev = E.BlupParallelEvaluator.__new__(E.BlupParallelEvaluator)
+    ev.engine = None
+    with pytest.raises(AttributeError):
+        ev.evaluate([], [], 0)
+
+
+def test_intergcv_folds_and_intragcv_mean(panel, flow):
+    gp, pp, _ = panel
+    random.seed(4)
+    np.random.seed(4)
+    rem = E.SNPRemovalHandler(100, 0.0, 0.4, False)
+    ev = E.IntraGCVBlupParallelEvaluator(gp, pp, 0.4, n_procs=2, n_folds=5, snp_remover=rem)
+    np.testing.assert_array_equal(ev.training_indices, flow["cv_T"])
+    tr = np.concatenate([np.asarray(f[0]) for f in ev.fold_indices])
+    va = np.concatenate([np.asarray(f[1]) for f in ev.fold_indices])
+    np.testing.assert_array_equal(tr, flow["cv_fold_train"])
+    np.testing.assert_array_equal(va, flow["cv_fold_valid"])
+    np.testing.assert_array_equal([len(f[1]) for f in ev.fold_indices], flow["cv_fold_valid_len"])
+    pop = [IdxIndividual(g, 80) for g in flow["cv_genomes"]]
+    _enter_with_oracle(ev, gp, pp)
+    ev.evaluate(pop, pop, 0)
+    np.testing.assert_allclose([p.fitness for p in pop], flow["cv_intra_fitness"], rtol=0, atol=1e-12)
+    # InterGCV rotates the fold with the generation
+    inter = E.InterGCVBlupParallelEvaluator.__new__(E.InterGCVBlupParallelEvaluator)
+    inter.fold_indices, inter.n_folds = ev.fold_indices, 5
+    assert inter.train_validation_indices(7) is ev.fold_indices[2]
+
+
+def test_montecarlo_split_sequence(panel, flow):
+    gp, pp, _ = panel
+    random.seed(5)
+    np.random.seed(5)
+    rem = E.SNPRemovalHandler(100, 0.0, 0.4, False)
+    ev = E.MonteCarloCVBlupParallelEvaluator(gp, pp, 0.4, n_procs=1, snp_remover=rem)
+    np.testing.assert_array_equal(ev.training_indices, flow["mc_T"])
+    seq = [ev.train_validation_indices(g) for g in range(3)]
+    np.testing.assert_array_equal(np.array([s[0] for s in seq]), flow["mc_split_train"])
+    np.testing.assert_array_equal(np.array([s[1] for s in seq]), flow["mc_split_valid"])
+
+
+def test_snp_removal_flow(panel, flow):
+    gp, pp, _ = panel
+    random.seed(6)
+    np.random.seed(6)
+    rem = E.SNPRemovalHandler(30, -1.0, 0.4, True)
+    ev = E.BlupParallelEvaluator(gp, pp, 0.4, n_procs=2, snp_remover=rem)
+    np.testing.assert_array_equal(ev.testing_indices, flow["rm_X"])
+    prev = [KeyIndividual(k, 60) for k in flow["rm_prev_keys"]]
+    for i, p in enumerate(prev):
+        p.set_fitness(0.01 * i)
+    nxt = [KeyIndividual(k, 60) for k in flow["rm_next_keys"]]
+    for i, p in enumerate(nxt):
+        p.set_fitness(0.02 * ((i * 7) % 10))
+
+    class _Mon:
+        def __init__(self):
+            self.events = []
+
+        def log_snp_removal_event(self, g):
+            self.events.append(g)
+
+    class _Pop(list):
+        monitor = _Mon()
+
+    prev_pop = _Pop(prev)
+    _enter_with_oracle(ev, gp, pp)
+    ev.evaluate(prev_pop, nxt, 1)
+    np.testing.assert_array_equal(rem.removed, flow["rm_removed"])
+    np.testing.assert_allclose([p.fitness for p in nxt], flow["rm_next_fitness"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose([p.fitness for p in prev_pop], flow["rm_prev_fitness"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(ev.evaluate_testing(nxt), flow["rm_testing"], rtol=0, atol=1e-12)
+    assert prev_pop.monitor.events == [1]
+
+
+def test_combine_with_removed_is_sorted_union():
+    rem = E.SNPRemovalHandler(3, 0.0, 0.4, True)
+    rem.removed = np.array([7.0, 2.0])
+    np.testing.assert_array_equal(rem.combine_with_removed(np.array([9, 2, 9, 1])), [1, 2, 7, 9])
+
+
+def test_get_evaluator_factory(panel):
+    import argparse
+    gp, pp, _ = panel
+    ns = argparse.Namespace(splitter=None, removal_r=None, features=10, h2_alpha=0.0, heritability=0.4,
+                            remove_snps=False, processes=2, geno=gp, pheno=pp, cv_folds=5,
+                            REGRESSOR_TYPE_BLUP="blup", REGRESSOR_TYPE_INTRACV_BLUP="intracv_blup",
+                            REGRESSOR_TYPE_INTERCV_BLUP="intercv_blup", REGRESSOR_TYPE_MONTECV_BLUP="montecv_blup")
+    for kind, cls in [("blup", E.BlupParallelEvaluator), ("intracv_blup", E.IntraGCVBlupParallelEvaluator),
+                      ("intercv_blup", E.InterGCVBlupParallelEvaluator),
+                      ("montecv_blup", E.MonteCarloCVBlupParallelEvaluator)]:
+        ns.regressor = kind
+        assert type(E.get_evaluator(ns)) is cls
+    ns.regressor = "nope"
+    with pytest.raises(NotImplementedError):
+        E.get_evaluator(ns)
+
+
+def test_genotype_validation_rejects_dosages():
+    from tblup_amd.engine import validate_genotypes
+    assert validate_genotypes(np.array([[0.0, 1.0], [2.0, 1.0]])).dtype == np.int8
+    with pytest.raises(ValueError):
+        validate_genotypes(np.array([[0.0, 1.5], [2.0, 1.0]]))
+    with pytest.raises(ValueError):
+        validate_genotypes(np.array([[0, 3], [2, 1]], dtype=np.int8))
+
+
+def test_concat_genomes_ragged():
+    from tblup_amd.engine import concat_genomes
+    idx, off = concat_genomes([np.array([3, 1]), np.array([5]), np.array([2, 2, 2])])
+    np.testing.assert_array_equal(idx, [3, 1, 5, 2, 2, 2])
+    np.testing.assert_array_equal(off, [0, 2, 3, 6])
