@@ -78,6 +78,7 @@ struct tblup_ctx {
   double flops[TBLUP_N_KCLASS] = {0};
   double bytes[TBLUP_N_KCLASS] = {0};
   int64_t mem_in_use = 0;
+  int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
 };
 
 namespace {
@@ -165,7 +166,7 @@ size_t chunk_bytes(const EvalDims& d, int64_t B, int64_t max_kblk, int64_t sum_k
   add((size_t)B * max_kblk * d.nRp * KBLK);                     // panel
   add((size_t)B * d.nRp * 8);                                   // u
   add((size_t)B * 64);                                          // scal
-  add((size_t)B * d.nRp * d.nTp * 8);                           // K
+  add((size_t)B * d.nTp * d.nTp * 8);                           // L
   add((size_t)B * d.NT * TILE * TILE * 8);                      // Dinv
   add((size_t)B * d.nTp * 8);                                   // z
   add((size_t)B * 8);                                           // fitness
@@ -207,7 +208,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, c
   int8_t* panel = cv.take<int8_t>((size_t)B * pstride);
   double* u = cv.take<double>((size_t)B * d.nRp);
   double* scal = cv.take<double>((size_t)B * 8);
-  double* K = cv.take<double>((size_t)B * d.nRp * d.nTp);
+  double* L = cv.take<double>((size_t)B * d.nTp * d.nTp);
   double* Dinv = cv.take<double>((size_t)B * d.NT * TILE * TILE);
   double* z = cv.take<double>((size_t)B * d.nTp);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
@@ -221,37 +222,44 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, c
     return launch_gather((const int8_t*)sp.geno.p, d_idx, d_off, pstride, B, csT, csA, scal, d, panel, u, s);
   });
   if (rc) return rc;
-  const double kbytes = (double)B * ((double)d.nT * d.nT / 2.0 + (double)d.nV * d.nT) * 8.0;
-  rc = timed(c, s, KC_GRM, grm_flops, kbytes + gather_bytes / 2.0,
-             [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
-  if (rc) return rc;
-  if (K_out) *K_out = K;
   if (z_out) *z_out = z;
-  if (stop_stage == 1) return 0;
+  if (stop_stage == 1) {
+    // parity readback only: the full K_{R,T} block of the unified form (k_grm); the
+    // production path never materialises K (the Cholesky kernels rebuild each tile)
+    double* K = cv.take<double>((size_t)B * d.nRp * d.nTp);
+    if (K_out) *K_out = K;
+    const double kbytes = (double)B * ((double)d.nT * d.nT / 2.0 + (double)d.nV * d.nT) * 8.0;
+    return timed(c, s, KC_GRM, grm_flops, kbytes + gather_bytes / 2.0,
+                 [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
+  }
+  if (K_out) *K_out = L;
+  CholLaunch cl{d, B, L, Dinv, z, (const double*)sp.yT.p, (const double*)sp.yV.p, panel, pstride, d_off, u, scal,
+                c->dbg_skip};
   const double T3 = (double)TILE * TILE * TILE;
+  const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
   for (int J = 0; J < d.NT; ++J) {
     const double jt = (double)J;
-    // algorithmic flops: SYRK update of the diagonal tile + potrf + trtri (+ forward-subst GEMV)
-    const double fd = (double)B * (T3 * jt + T3 / 3.0 + T3 / 3.0 + 2.0 * TILE * TILE * jt);
+    // algorithmic fp64 work: SYRK update of the diagonal tile, potrf + trtri, forward-substitution GEMV
+    // (the fused int8 GRM tile, 128*129*k int-ops, is not counted in these fp64 flops)
+    const double fd = (double)B * (T3 * jt + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
     const double bd = (double)B * (TILE * TILE * jt * 8.0 + 2.0 * TILE * TILE * 8.0);
-    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(K, d, B, J, Dinv, z, (const double*)sp.yT.p, scal, s); });
+    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol(cl, J, s, true); });
     if (rc) return rc;
     const int nI = d.NT - J - 1;
     if (nI > 0) {
-      // algorithmic flops per tile: GEMM update 2*128^3*J + triangular solve 128^3
+      // per tile: GEMM update 2*128^3*J, triangular solve 128^3 (fused GRM tile int-ops excluded)
       const double fo = (double)B * nI * (2.0 * T3 * jt + T3);
-      const double bo = (double)B * nI * (TILE * TILE * jt * 8.0 + 2.0 * TILE * TILE * 8.0) +
+      const double bo = (double)B * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) +
                         (double)B * TILE * TILE * jt * 8.0;
-      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(K, d, B, J, Dinv, s); });
+      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol(cl, J, s, false); });
       if (rc) return rc;
     }
   }
   if (stop_stage == 2) return 0;
-  const double fs = (double)B * (2.0 * (double)d.nTp * d.nTp / 2.0 + 2.0 * (double)d.nV * d.nT + 10.0 * d.nV);
-  const double bs = (double)B * (((double)d.nTp * d.nTp / 2.0 + (double)d.NT * TILE * TILE + (double)d.nV * d.nT) * 8.0);
-  rc = timed(c, s, KC_SOLVE, fs, bs, [&] {
-    return launch_solve(K, d, B, Dinv, z, (const double*)sp.yV.p, scal, d_fit, d_ebv, s);
-  });
+  const double fs = (double)B * (2.0 * (double)d.nTp * d.nTp / 2.0 + 2.0 * kbar * (double)(d.nT + d.nV) + 10.0 * d.nV);
+  const double bs = (double)B * (((double)d.nTp * d.nTp / 2.0 + (double)d.NT * TILE * TILE) * 8.0 +
+                                 kbar * (double)(d.nT + d.nV));
+  rc = timed(c, s, KC_SOLVE, fs, bs, [&] { return launch_solve(cl, d_fit, d_ebv, s); });
   return rc;
 }
 
@@ -302,6 +310,8 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   const char* env = getenv("TBLUP_WORKSPACE_MB");
   c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
+  const char* dbg = getenv("TBLUP_DBG_SKIP");
+  c->dbg_skip = dbg ? atoi(dbg) : 0;
   const size_t gbytes = (size_t)n * (size_t)P;
   if (int rc = dev_alloc(c.get(), c->geno_sm, gbytes)) return rc;
   if (int rc = dev_alloc(c.get(), c->colsum_all, (size_t)P * 4)) return rc;
@@ -550,7 +560,7 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
   const EvalDims d = dims_of(c, *sp);
   const int64_t nkb = (k + KBLK - 1) / KBLK;
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (int rc = dev_alloc(c, c->ws, chunk_bytes(d, 1, nkb, k, false))) return rc;
+  if (int rc = dev_alloc(c, c->ws, chunk_bytes(d, 1, nkb, k, false) + (size_t)d.nRp * d.nTp * 8 + 4096)) return rc;
   Carve cv{(char*)c->ws.p};
   int64_t* d_idx = cv.take<int64_t>((size_t)k);
   int64_t* d_off = cv.take<int64_t>(2);
@@ -562,10 +572,15 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
                          &K, &z))
     return rc;
   HIPCHK(hipStreamSynchronize(c->stream));
-  std::vector<double> full((size_t)d.nRp * d.nTp);
+  const int64_t rows = (stage == 1) ? d.nRp : d.nTp;
+  std::vector<double> full((size_t)rows * d.nTp);
   HIPCHK(hipMemcpy(full.data(), K, full.size() * 8, hipMemcpyDeviceToHost));
   const int64_t nR = d.nT + d.nV;
   for (int64_t r = 0; r < nR; ++r) {
+    if (stage == 2 && r >= d.nT) {
+      std::memset(out + r * d.nT, 0, (size_t)d.nT * 8);   // the factor has no V rows
+      continue;
+    }
     const int64_t src = r < d.nT ? r : d.nTp + (r - d.nT);
     std::memcpy(out + r * d.nT, full.data() + src * d.nTp, (size_t)d.nT * 8);
   }

@@ -1,0 +1,146 @@
+// int8 MFMA tile GEMM shared by the GRM kernels:
+//   C(128x128, int32) = sum_s A[i][s] * B[j][s]
+// where A and B are 128-row tiles of the animal-major panel ([kb][row][64 SNPs]).
+// 256 threads = 4 waves in a 2x2 grid, each wave a 64x64 block of 2x2
+// v_mfma_i32_32x32x32_i8 tiles (lane l holds 16 consecutive k of row l&31).
+// Genotypes are {0,1,2}: every partial sum is an exact integer.
+#pragma once
+#include "tblup_internal.h"
+
+namespace tblup {
+
+// [128 rows][64 B]; 16-B chunk c of row r stored at c ^ ((r >> 2) & 3):
+// conflict-free ds_read_b128 for the 32x32x32 i8 fragment pattern.
+__device__ __forceinline__ int lds_off_i8(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 2) & 3)); }
+
+// lds: >= 32 KiB (two buffers x A/B x 8 KiB).  a_base/b_base point at kb = 0 of the
+// two 128-row tiles; consecutive kb blocks are kb_stride bytes apart.
+__device__ __forceinline__ void i8_tile_gemm(const int8_t* __restrict__ a_base, const int8_t* __restrict__ b_base,
+                                             bool same, int64_t nblk, int64_t kb_stride, int8_t* lds,
+                                             v16i (&acc)[2][2]) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
+  if (nblk <= 0) return;
+  constexpr int TB = TILE * KBLK;  // 8 KiB
+  v4i ra[2], rb[2];
+  auto gload = [&](int64_t kb) {
+    const int8_t* A = a_base + kb * kb_stride;
+    const int8_t* Bp = b_base + kb * kb_stride;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int q = t + 256 * e;
+      ra[e] = *reinterpret_cast<const v4i*>(A + 16 * q);
+      if (!same) rb[e] = *reinterpret_cast<const v4i*>(Bp + 16 * q);
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int q = t + 256 * e, row = q >> 2, c = q & 3;
+      *reinterpret_cast<v4i*>(lds + (2 * buf) * TB + lds_off_i8(row, c)) = ra[e];
+      if (!same) *reinterpret_cast<v4i*>(lds + (2 * buf + 1) * TB + lds_off_i8(row, c)) = rb[e];
+    }
+  };
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    const int cur = (int)(kb & 1);
+    if (kb + 1 < nblk) gload(kb + 1);
+    const int8_t* As = lds + (2 * cur) * TB;
+    const int8_t* Bs = same ? As : lds + (2 * cur + 1) * TB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = (l >> 5) + 2 * kk;
+      v4i a[2], bb[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) a[m] = *reinterpret_cast<const v4i*>(As + lds_off_i8(64 * wr + 32 * m + (l & 31), chunk));
+#pragma unroll
+      for (int n = 0; n < 2; ++n) bb[n] = *reinterpret_cast<const v4i*>(Bs + lds_off_i8(64 * wc + 32 * n + (l & 31), chunk));
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bb[n], acc[m][n], 0, 0, 0);
+    }
+    if (kb + 1 < nblk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+}
+
+// Same product with an LDS-DMA ring (global_load_lds_dwordx4): D stage slots, D-1
+// stages in flight while one is consumed, one barrier per stage.  The LDS image is
+// lane-linear per wave instruction; the chunk swizzle of lds_off_i8 is applied to the
+// SOURCE address (an involution), so fragment reads use lds_off_i8 unchanged.
+// lds must hold D * (SAME ? 8 : 16) KiB.
+template <bool SAME, int D>
+__device__ __forceinline__ void i8_tile_gemm_ring(const int8_t* __restrict__ a_base, const int8_t* __restrict__ b_base,
+                                                  int64_t nblk, int64_t kb_stride, int8_t* lds, v16i (&acc)[2][2]) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
+  if (nblk <= 0) return;
+  constexpr int TB = TILE * KBLK;             // 8 KiB per operand tile
+  constexpr int SB = (SAME ? 1 : 2) * TB;     // bytes per stage
+  constexpr int NI = SAME ? 2 : 4;            // glds instructions per thread per stage
+  auto issue = [&](int64_t kb) {
+    int8_t* slot = lds + (int)(kb % D) * SB;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int cb = w * 2 + e;               // 1 KiB chunk block of the 8 KiB tile
+      const int q = cb * 64 + l, row = q >> 2, pos = q & 3;
+      const int src = row * 64 + 16 * (pos ^ ((row >> 2) & 3));
+      __builtin_amdgcn_global_load_lds(a_base + kb * kb_stride + src,
+                                       (__attribute__((address_space(3))) void*)(slot + cb * 1024), 16, 0, 0);
+      if (!SAME)
+        __builtin_amdgcn_global_load_lds(b_base + kb * kb_stride + src,
+                                         (__attribute__((address_space(3))) void*)(slot + TB + cb * 1024), 16, 0, 0);
+    }
+  };
+  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    if (kb + D - 2 < nblk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * NI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kb + D - 1 < nblk) issue(kb + D - 1);   // into the slot consumed at kb-1
+    const int8_t* As = lds + (int)(kb % D) * SB;
+    const int8_t* Bs = SAME ? As : As + TB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = (l >> 5) + 2 * kk;
+      v4i a[2], bb[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) a[m] = *reinterpret_cast<const v4i*>(As + lds_off_i8(64 * wr + 32 * m + (l & 31), chunk));
+#pragma unroll
+      for (int n = 0; n < 2; ++n) bb[n] = *reinterpret_cast<const v4i*>(Bs + lds_off_i8(64 * wc + 32 * n + (l & 31), chunk));
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bb[n], acc[m][n], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Row / column (within the 128x128 tile) of accumulator element r of block (m, n) for lane l.
+__device__ __forceinline__ int i8_row(int wr, int m, int r, int l) { return 64 * wr + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
+__device__ __forceinline__ int i8_col(int wc, int n, int l) { return 64 * wc + 32 * n + (l & 31); }
+
+// K value of the unified form from the exact integer count c = (A A^T)_ij.
+__device__ __forceinline__ double grm_value(int32_t c, double ui, double uj, double invN, double cN, double invd) {
+  return ((double)c - (ui + uj) * invN + cN) * invd;
+}
+
+}  // namespace tblup

@@ -14,7 +14,7 @@
 //                  T = A_IJ - sum_L L_IL L_JL^T, then L_IJ = T inv(L_JJ)^T, both on MFMA.
 // fp64 MFMA: v_mfma_f64_16x16x4_f64, A[i=l&15][k=l>>4], B[k=l>>4][j=l&15],
 // C/D row=(l>>4)+4r, col=l&15 (verified on gfx950 by tools/mfma_probe.hip).
-#include "tblup_internal.h"
+#include "i8_tile.h"
 
 namespace tblup {
 
@@ -41,7 +41,7 @@ __device__ __forceinline__ v4d mfma64(double a, double b, v4d c) {
 // acc[m][n] += sum_{k < kmax} A[64wr+16m+i][k] * Bm[64wc+16n+j][k]  (row-major, ld)
 // 256 threads, double-buffered LDS staging with register prefetch.
 // OnStage(buf_ptr, k0) is called by every thread once per staged A panel.
-template <bool SAME, typename OnStage>
+template <bool SAME, typename OnStage, bool NEG_A = false>
 __device__ __forceinline__ void gemm_nt_f64(const double* __restrict__ A, const double* __restrict__ Bm, int64_t ld,
                                             int kmax, v4d (&acc)[4][4], double* lds, OnStage on_stage) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
@@ -65,7 +65,7 @@ __device__ __forceinline__ void gemm_nt_f64(const double* __restrict__ A, const 
     for (int e = 0; e < 4; ++e) {
       const int q = t + 256 * e, r = q >> 3, c = q & 7;
       const int o = r * BKD + 2 * (c ^ ((r >> 1) & 7));
-      *reinterpret_cast<v2d*>(as + o) = ra[e];
+      *reinterpret_cast<v2d*>(as + o) = NEG_A ? -ra[e] : ra[e];
       if (!SAME) *reinterpret_cast<v2d*>(bs + o) = rb[e];
     }
   };
@@ -99,6 +99,73 @@ __device__ __forceinline__ void gemm_nt_f64(const double* __restrict__ A, const 
 struct NoStage {
   __device__ void operator()(const double*, int) const {}
 };
+
+// ---- SYRK restricted to the 36 lower 16x16 blocks of a 128x128 tile ----
+// Block e (row-major over q >= s) goes to wave e % 4: 9 blocks per wave, so the
+// lower triangle costs 36 block-MFMA streams instead of the 64 of a full GEMM.
+__host__ __device__ constexpr int tri_q(int e) {
+  int q = 0;
+  while ((q + 1) * (q + 2) / 2 <= e) ++q;
+  return q;
+}
+__host__ __device__ constexpr int tri_s(int e) { return e - tri_q(e) * (tri_q(e) + 1) / 2; }
+
+template <int W>
+__device__ __forceinline__ void syrk_stage(const double* As, v4d (&acc)[9], int l) {
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 4 * kk + (l >> 4);
+    double a8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a8[q] = As[st_off(16 * q + (l & 15), k)];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int e = W + 4 * i;
+      acc[i] = mfma64(a8[tri_q(e)], a8[tri_s(e)], acc[i]);
+    }
+  }
+}
+
+// acc[i] (block e = w + 4i) += sum_{k < kmax} A[16q + r][k] A[16s + c][k]; staging as gemm_nt_f64<true>.
+template <typename OnStage>
+__device__ __forceinline__ void syrk_lower_f64(const double* __restrict__ A, int64_t ld, int kmax, v4d (&acc)[9],
+                                               double* lds, OnStage on_stage) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  double* As0 = lds;
+  double* As1 = lds + STAGE;
+  v2d ra[4];
+  const int nst = kmax / BKD;
+  if (nst == 0) return;
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = t + 256 * e, r = q >> 3, c = q & 7;
+      ra[e] = *reinterpret_cast<const v2d*>(A + (int64_t)r * ld + k0 + 2 * c);
+    }
+  };
+  auto swrite = [&](double* as) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = t + 256 * e, r = q >> 3, c = q & 7;
+      *reinterpret_cast<v2d*>(as + r * BKD + 2 * (c ^ ((r >> 1) & 7))) = ra[e];
+    }
+  };
+  gload(0);
+  swrite(As0);
+  __syncthreads();
+  for (int s = 0; s < nst; ++s) {
+    const bool odd = (s & 1) != 0;
+    const double* As = odd ? As1 : As0;
+    if (s + 1 < nst) gload((s + 1) * BKD);
+    on_stage(As, s * BKD);
+    if (w == 0) syrk_stage<0>(As, acc, l);
+    else if (w == 1) syrk_stage<1>(As, acc, l);
+    else if (w == 2) syrk_stage<2>(As, acc, l);
+    else syrk_stage<3>(As, acc, l);
+    if (s + 1 < nst) swrite(odd ? As0 : As1);
+    __syncthreads();
+  }
+}
 
 // ---- packed lower-triangular 16x16 block storage of a 128x128 tile in LDS ----
 constexpr int NB = 16;                       // base block edge
@@ -170,35 +237,81 @@ __device__ __forceinline__ void factor16(double* D, double* X, int l) {
 
 }  // namespace
 
+// Per-launch arguments shared by the two Cholesky kernels.
+struct CholArgs {
+  double* L;                // [B][nTp][nTp] factor (TT lower tiles)
+  double* Dinv;             // [B][NT][128][128]
+  double* z;                // [B][nTp]
+  const double* yT;         // [nTp]
+  const int8_t* panel;      // [B] x pstride
+  int64_t pstride;
+  const int64_t* off;       // [B+1]
+  const double* u;          // [B][nRp]
+  const double* scal;       // [B][8]
+  int64_t nT, nTp, nRp;
+  int NT, J;
+  int skip;                 // diagnostic ablation mask (TBLUP_DBG_SKIP); 0 in production
+};
+
 // ---------------------------------------------------------------------------
-// diagonal tile: SYRK update, blocked factorisation, blocked inverse, forward solve
+// diagonal tile: fused GRM tile, SYRK update, blocked factorisation, blocked
+// inverse, forward solve
 // ---------------------------------------------------------------------------
+//   0. K_JJ from the panel on int8 MFMA (exact counts + fp64 centring) -> packed lower blocks
 //   A. acc = sum_{L<J} L_JL L_JL^T (fp64 MFMA), w = sum_{L<J} L_JL z_L (fused)
-//   B. T = A_JJ - acc -> LDS, packed lower 16x16 blocks; r = y_J - mu - w
+//   B. T = K_JJ - acc (in place, packed lower 16x16 blocks); r = y_J - mu - w
 //   C. for panel p: one wave factors T_pp (-> L_pp, X_pp = L_pp^{-1});
 //      all waves: L_qp = T_qp X_pp^T (q > p); T_qs -= L_qp L_sp^T (q >= s > p)   [MFMA]
 //   D. blocked inverse X = L^{-1}: X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
-//   E. write L (lower blocks) to K, X to Dinv (zeros above the diagonal), z_J = X r
-__global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, int64_t nTp, int64_t nT, int64_t mstride,
-                                                   int J, double* __restrict__ Dinv, double* __restrict__ z,
-                                                   const double* __restrict__ yT, const double* __restrict__ scal) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];  // 144 KiB: staging, then T and X blocks
+//   E. write L (lower blocks), X to Dinv (zeros above the diagonal), z_J = X r
+__global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];  // 144 KiB: T blocks | X blocks (+staging)
   __shared__ double rsh[TILE];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  const int64_t b = blockIdx.x;
-  double* Kb = K + b * mstride;
+  const int64_t b = blockIdx.x, nTp = a.nTp;
+  const int J = a.J;
+  double* Lb = a.L + b * nTp * nTp;
   const int64_t j0 = (int64_t)J * TILE;
-  const double* zb = z + b * nTp;
-  const double mu = scal[b * 8 + 3];
+  const double* zb = a.z + b * nTp;
+  const double* sc = a.scal + b * 8;
+  const double invN = sc[0], cN = sc[1], invd = sc[2], mu = sc[3], lam = sc[4];
+  const double* ub = a.u + b * a.nRp;
   double* Tp = lds;
-  double* Xp = lds + NPACK * BLKD;
+  double* Xp = lds + NPACK * BLKD;   // also the staging area of steps 0 and A
 
-  v4d acc[4][4];
+  // 0. fused GRM tile K_JJ (lower 16x16 blocks only)
+  if (!(a.skip & 1)) {
+    const int64_t k = a.off[b + 1] - a.off[b];
+    const int8_t* pj = a.panel + b * a.pstride + j0 * KBLK;
+    v16i ci[2][2];
+    i8_tile_gemm_ring<true, 8>(pj, pj, (k + KBLK - 1) / KBLK, a.nRp * KBLK, reinterpret_cast<int8_t*>(Xp), ci);
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = v4d{0.0, 0.0, 0.0, 0.0};
+      for (int n = 0; n < 2; ++n) {
+        const int col = i8_col(wc, n, l);
+        const int64_t gj = j0 + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = i8_row(wr, m, r, l);
+          if ((row >> 4) >= (col >> 4)) {
+            const int64_t gi = j0 + row;
+            double v;
+            if (gi < a.nT && gj < a.nT) {
+              v = grm_value(ci[m][n][r], ub[gi], ub[gj], invN, cN, invd);
+              if (gi == gj) v += lam;
+            } else {
+              v = (gi == gj) ? 1.0 : 0.0;
+            }
+            Tp[pk(row >> 4, col >> 4) + bo(row & 15, col & 15)] = v;
+          }
+        }
+      }
+  }
 
+  v4d acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
   double wpart = 0.0;
   auto on_stage = [&](const double* As, int k0) {
     if (t < TILE) {
@@ -206,63 +319,55 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, int64
       for (int kk = 0; kk < BKD; ++kk) wpart += As[st_off(t, kk)] * zb[k0 + kk];
     }
   };
-  if (J > 0) gemm_nt_f64<true>(Kb + j0 * nTp, Kb + j0 * nTp, nTp, (int)j0, acc, lds, on_stage);
   __syncthreads();
+  if (J > 0 && !(a.skip & 2)) syrk_lower_f64(Lb + j0 * nTp, nTp, (int)j0, acc, Xp, on_stage);
 
-  // B. lower blocks of T = A_JJ - acc (wave (wr,wc) holds block rows 4wr+m, block cols 4wc+n)
+  // B. T = K_JJ - acc on the lower blocks (wave w holds blocks e = w + 4i)
+  if (J > 0) {
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+    for (int i = 0; i < 9; ++i) {
+      const int e = w + 4 * i, q = tri_q(e), sb = tri_s(e);
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int q = 4 * wr + m, sb = 4 * wc + n;
-      if (q >= sb) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rr = (l >> 4) + 4 * r, cc = l & 15;
-          Tp[pk(q, sb) + bo(rr, cc)] = Kb[(j0 + 16 * q + rr) * nTp + j0 + 16 * sb + cc] - acc[m][n][r];
-        }
-      }
+      for (int r = 0; r < 4; ++r) Tp[pk(q, sb) + bo((l >> 4) + 4 * r, l & 15)] -= acc[i][r];
     }
+  }
   if (t < TILE) {
     const int64_t gi = j0 + t;
-    rsh[t] = (gi < nT) ? (yT[gi] - mu - wpart) : 0.0;
+    rsh[t] = (gi < a.nT) ? (a.yT[gi] - mu - wpart) : 0.0;
   }
   __syncthreads();
 
   // C. blocked right-looking factorisation over 16-column panels
-  for (int p = 0; p < NBLK; ++p) {
-    if (w == 0) factor16(Tp + pk(p, p), Xp + pk(p, p), l);
+  for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
+    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xp + pk(p, p), l);
     __syncthreads();
-    // panel solve L_qp = T_qp X_pp^T
-    for (int q = p + 1 + w; q < NBLK; q += 4) {
-      v4d a = {0.0, 0.0, 0.0, 0.0};
-      a = mma_abt(Tp + pk(q, p), Xp + pk(p, p), a, l);
+    for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += 4) {
+      v4d x = {0.0, 0.0, 0.0, 0.0};
+      x = mma_abt(Tp + pk(q, p), Xp + pk(p, p), x, l);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = a[r];
+      for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
     }
     __syncthreads();
-    // trailing update T_qs -= L_qp L_sp^T for q >= s > p
     const int nb = NBLK - 1 - p;
-    for (int e = w; e < nb * (nb + 1) / 2; e += 4) {
+    for (int e = w; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += 4) {
       int qq = 0;
       while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
       const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
-      v4d a = {0.0, 0.0, 0.0, 0.0};
-      a = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), a, l);
+      v4d x = {0.0, 0.0, 0.0, 0.0};
+      x = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), x, l);
       double* dst = Tp + pk(q, sb);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= a[r];
+      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
     }
     __syncthreads();
   }
 
   // D. blocked inverse, one block diagonal per round
-  for (int dd = 1; dd < NBLK; ++dd) {
+  for (int dd = 1; dd < ((a.skip & 8) ? 0 : NBLK); ++dd) {
     for (int jb = w; jb + dd < NBLK; jb += 4) {
       const int q = jb + dd;
       v4d sacc = {0.0, 0.0, 0.0, 0.0};
       for (int lb = jb; lb < q; ++lb) {
-        // S += L_{q,lb} X_{lb,jb}:  B[k][c] = X_{lb,jb}[k][c]
         const double* A = Tp + pk(q, lb);
         const double* Xb = Xp + pk(lb, jb);
 #pragma unroll
@@ -283,13 +388,14 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, int64
   }
 
   // E. outputs
-  double* Db = Dinv + (b * (nTp / TILE) + J) * (int64_t)(TILE * TILE);
+  double* Db = a.Dinv + (b * a.NT + J) * (int64_t)(TILE * TILE);
+  if (a.skip & 16) return;
   for (int e = t; e < TILE * TILE; e += 256) {
     const int rr = e >> 7, cc = e & 127, q = rr >> 4, sb = cc >> 4;
     double xv = 0.0;
     if (q >= sb) {
       xv = Xp[pk(q, sb) + bo(rr & 15, cc & 15)];
-      if (rr >= cc) Kb[(j0 + rr) * nTp + j0 + cc] = Tp[pk(q, sb) + bo(rr & 15, cc & 15)];
+      if (rr >= cc) Lb[(j0 + rr) * nTp + j0 + cc] = Tp[pk(q, sb) + bo(rr & 15, cc & 15)];
     }
     Db[e] = xv;
   }
@@ -301,41 +407,67 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, int64
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc_z += Xb[bo(t & 15, c)] * rsh[16 * sb + c];
     }
-    z[b * nTp + j0 + t] = acc_z;
+    a.z[b * nTp + j0 + t] = acc_z;
   }
 }
 
-hipError_t launch_chol_diag(double* K, const EvalDims& d, int64_t B, int J, double* Dinv, double* z,
-                            const double* yT, const double* scal, hipStream_t s) {
-  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)B), dim3(256), 0, s, K, d.nTp, d.nT, d.nRp * d.nTp, J, Dinv, z, yT,
-                     scal);
-  return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------
-// off-diagonal tiles of column J: L_IJ = (A_IJ - sum_L L_IL L_JL^T) inv(L_JJ)^T
+// off-diagonal tiles of column J: L_IJ = (K_IJ - sum_L L_IL L_JL^T) inv(L_JJ)^T
+//   0. K_IJ from the panel (int8 MFMA) -> fp64 image in LDS -> accumulators
+//   1. acc -= sum_L L_IL L_JL^T (fp64 MFMA, A operand negated at staging)
+//   2. L_IJ = T X^T with X = inv(L_JJ) lower triangular (fp64 MFMA)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_chol_offdiag(double* __restrict__ K, int64_t nTp, int64_t mstride, int J,
-                                                      int NT, const double* __restrict__ Dinv) {
-  __shared__ __attribute__((aligned(16))) double lds[TILE * TILE + STAGE];  // T tile + X stage (144 KiB)
+__global__ __launch_bounds__(256) void k_chol_offdiag(CholArgs a) {
+  __shared__ __attribute__((aligned(16))) double lds[TILE * TILE + STAGE];  // T image + X stage (144 KiB)
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+  const int J = a.J, NT = a.NT;
   const int nI = NT - J - 1;
   const int64_t logical = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t b = logical / nI;
   const int I = J + 1 + (int)(logical % nI);
-  double* Kb = K + b * mstride;
+  const int64_t nTp = a.nTp;
+  double* Lb = a.L + b * nTp * nTp;
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
+  double* Tl = lds;
+  double* Xs = lds + TILE * TILE;
 
+  // 0. fused GRM tile
+  if (!(a.skip & 32)) {
+    const int64_t k = a.off[b + 1] - a.off[b];
+    const int8_t* pb = a.panel + b * a.pstride;
+    v16i ci[2][2];
+    i8_tile_gemm_ring<false, 8>(pb + i0 * KBLK, pb + j0 * KBLK, (k + KBLK - 1) / KBLK, a.nRp * KBLK,
+                                reinterpret_cast<int8_t*>(lds), ci);
+    const double* sc = a.scal + b * 8;
+    const double invN = sc[0], cN = sc[1], invd = sc[2];
+    const double* ub = a.u + b * a.nRp;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int col = i8_col(wc, n, l);
+        const int64_t gj = j0 + col;
+        const double uj = ub[gj];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = i8_row(wr, m, r, l);
+          const int64_t gi = i0 + row;
+          Tl[t_off(row, col)] = (gi < a.nT && gj < a.nT) ? grm_value(ci[m][n][r], ub[gi], uj, invN, cN, invd) : 0.0;
+        }
+      }
+  }
+  __syncthreads();
   v4d acc[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = v4d{0.0, 0.0, 0.0, 0.0};
-  if (J > 0) gemm_nt_f64<false>(Kb + i0 * nTp, Kb + j0 * nTp, nTp, (int)j0, acc, lds, NoStage{});
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[m][n][r] = Tl[t_off(64 * wr + 16 * m + (l >> 4) + 4 * r, 64 * wc + 16 * n + (l & 15))];
+  __syncthreads();
+  if (J > 0 && !(a.skip & 64)) gemm_nt_f64<false, NoStage, true>(Lb + i0 * nTp, Lb + j0 * nTp, nTp, (int)j0, acc, lds, NoStage{});
   __syncthreads();
 
-  double* Tl = lds;
-  double* Xs = lds + TILE * TILE;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -343,12 +475,12 @@ __global__ __launch_bounds__(256) void k_chol_offdiag(double* __restrict__ K, in
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 64 * wr + 16 * m + (l >> 4) + 4 * r, col = 64 * wc + 16 * n + (l & 15);
-        Tl[t_off(row, col)] = Kb[(i0 + row) * nTp + j0 + col] - acc[m][n][r];
+        Tl[t_off(row, col)] = acc[m][n][r];
         acc[m][n][r] = 0.0;
       }
 
   // out[i][j] = sum_c T[i][c] X[j][c], X = inv(L_JJ) lower triangular (X[j][c] = 0 for c > j)
-  const double* X = Dinv + (b * NT + J) * (int64_t)(TILE * TILE);
+  const double* X = a.Dinv + (b * NT + J) * (int64_t)(TILE * TILE);
   v2d rx[4];
   auto gload = [&](int s) {
 #pragma unroll
@@ -358,7 +490,7 @@ __global__ __launch_bounds__(256) void k_chol_offdiag(double* __restrict__ K, in
     }
   };
   gload(0);
-  for (int s = 0; s < TILE / BKD; ++s) {
+  for (int s = 0; s < ((a.skip & 128) ? 0 : TILE / BKD); ++s) {
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -371,15 +503,15 @@ __global__ __launch_bounds__(256) void k_chol_offdiag(double* __restrict__ K, in
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int k = 4 * kk + (l >> 4);
-        double a[4], bv[4];
+        double av[4], bv[4];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) a[m] = Tl[t_off(64 * wr + 16 * m + (l & 15), s * BKD + k)];
+        for (int m = 0; m < 4; ++m) av[m] = Tl[t_off(64 * wr + 16 * m + (l & 15), s * BKD + k)];
 #pragma unroll
         for (int n = 0; n < 4; ++n) bv[n] = Xs[st_off(64 * wc + 16 * n + (l & 15), k)];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int n = 0; n < 4; ++n) acc[m][n] = mfma64(a[m], bv[n], acc[m][n]);
+          for (int n = 0; n < 4; ++n) acc[m][n] = mfma64(av[m], bv[n], acc[m][n]);
       }
     }
   }
@@ -391,15 +523,20 @@ __global__ __launch_bounds__(256) void k_chol_offdiag(double* __restrict__ K, in
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 64 * wr + 16 * m + (l >> 4) + 4 * r, col = 64 * wc + 16 * n + (l & 15);
-        Kb[(i0 + row) * nTp + j0 + col] = acc[m][n][r];
+        Lb[(i0 + row) * nTp + j0 + col] = acc[m][n][r];
       }
 }
 
-hipError_t launch_chol_offdiag(double* K, const EvalDims& d, int64_t B, int J, const double* Dinv, hipStream_t s) {
-  const int nI = d.NT - J - 1;
-  if (nI <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(B * nI)), dim3(256), 0, s, K, d.nTp, d.nRp * d.nTp, J, d.NT,
-                     Dinv);
+hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag) {
+  CholArgs a{c.L, c.Dinv, c.z, c.yT, c.panel, c.pstride, c.off, c.u, c.scal, c.d.nT, c.d.nTp, c.d.nRp, c.d.NT, J,
+             c.skip};
+  if (diag) {
+    hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
+  } else {
+    const int nI = c.d.NT - J - 1;
+    if (nI <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(c.B * nI)), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

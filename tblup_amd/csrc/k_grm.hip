@@ -13,25 +13,15 @@
 // Cholesky and the prediction read are computed: the TT lower triangle
 // (diagonal tiles in full) and the VT block.  Workgroups of one individual are
 // kept on one XCD (xcd_remap) so the individual's panel is re-read from L2.
-#include "tblup_internal.h"
+#include "i8_tile.h"
 
 namespace tblup {
-
-namespace {
-
-__device__ __forceinline__ int lds_off_i8(int row, int chunk) {
-  // [128 rows][64 B]; 16-B chunk c of row r stored at chunk c ^ ((r >> 2) & 3):
-  // conflict-free ds_read_b128 for the 32x32x32 i8 fragment pattern.
-  return row * 64 + 16 * (chunk ^ ((row >> 2) & 3));
-}
-
-}  // namespace
 
 __global__ __launch_bounds__(256) void k_grm(const int8_t* __restrict__ panel, int64_t panel_stride,
                                              const int64_t* __restrict__ off, const double* __restrict__ u,
                                              const double* __restrict__ scal, int64_t nT, int64_t nTp, int64_t nV,
                                              int64_t nRp, int NT, int64_t tiles_per, double* __restrict__ K) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[2][2][TILE * KBLK];  // [buf][A/B]
+  __shared__ __attribute__((aligned(16))) int8_t lds[4 * TILE * KBLK];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
   const int64_t logical = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t b = logical / tiles_per;
@@ -49,71 +39,11 @@ __global__ __launch_bounds__(256) void k_grm(const int8_t* __restrict__ panel, i
     ti = NT + (int)(tt / NT);
     tj = (int)(tt % NT);
   }
-  const bool same = (ti == tj);
   const int64_t k = off[b + 1] - off[b];
-  const int64_t nblk = (k + KBLK - 1) / KBLK;
   const int8_t* pb = panel + b * panel_stride;
-
   v16i acc[2][2];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
-
-  v4i ra[2], rb[2];
-  auto gload = [&](int64_t kb) {
-    const int8_t* A = pb + (kb * nRp + (int64_t)ti * TILE) * KBLK;
-    const int8_t* Bp = pb + (kb * nRp + (int64_t)tj * TILE) * KBLK;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int q = t + 256 * e;
-      ra[e] = *reinterpret_cast<const v4i*>(A + 16 * q);
-      if (!same) rb[e] = *reinterpret_cast<const v4i*>(Bp + 16 * q);
-    }
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int q = t + 256 * e, row = q >> 2, c = q & 3;
-      *reinterpret_cast<v4i*>(&lds[buf][0][lds_off_i8(row, c)]) = ra[e];
-      if (!same) *reinterpret_cast<v4i*>(&lds[buf][1][lds_off_i8(row, c)]) = rb[e];
-    }
-  };
-
-  if (nblk > 0) {
-    gload(0);
-    swrite(0);
-    __syncthreads();
-    for (int64_t kb = 0; kb < nblk; ++kb) {
-      const int cur = (int)(kb & 1);
-      if (kb + 1 < nblk) gload(kb + 1);
-      const int8_t* As = lds[cur][0];
-      const int8_t* Bs = same ? lds[cur][0] : lds[cur][1];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = (l >> 5) + 2 * kk;
-        v4i a[2], bb[2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const int row = 64 * wr + 32 * m + (l & 31);
-          a[m] = *reinterpret_cast<const v4i*>(As + lds_off_i8(row, chunk));
-        }
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const int row = 64 * wc + 32 * n + (l & 31);
-          bb[n] = *reinterpret_cast<const v4i*>(Bs + lds_off_i8(row, chunk));
-        }
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bb[n], acc[m][n], 0, 0, 0);
-      }
-      if (kb + 1 < nblk) swrite(cur ^ 1);
-      __syncthreads();
-    }
-  }
+  i8_tile_gemm(pb + (int64_t)ti * TILE * KBLK, pb + (int64_t)tj * TILE * KBLK, ti == tj, (k + KBLK - 1) / KBLK,
+               nRp * KBLK, lds, acc);
 
   // epilogue: exact-integer centring in fp64, padding rows/cols -> identity
   const double* sc = scal + b * 8;

@@ -1,7 +1,7 @@
 // Back substitution, prediction and fitness, one 1024-thread workgroup per individual.
 //
 //   alpha = L^{-T} z                       (z = L^{-1}(y_T - mu) from k_chol_diag)
-//   EBV_V = K_VT alpha + mu                gblup: evaluator.py:284 (G[:,T] Ginv y_T, mu = 0)
+//   EBV_V = K_VT alpha + mu, K_VT applied in factored form from the int8 panel                gblup: evaluator.py:284 (G[:,T] Ginv y_T, mu = 0)
 //                                          snp:   evaluator.py:314 (clf.predict, intercept mean(y_T))
 //   fitness = |pearsonr(EBV_V, y_V)|       evaluator.py:286 / :314, scipy 1.15.3 pearsonr:
 //            exact-equality constant input -> NaN; mean-centre; max-abs scaled
@@ -42,32 +42,33 @@ __device__ double block_max(double v, double* red) {
 
 }  // namespace
 
-__global__ __launch_bounds__(NTH) void k_solve(const double* __restrict__ K, int64_t nTp, int64_t nT, int64_t nV,
-                                               int NT, int64_t mstride, const double* __restrict__ Dinv,
-                                               const double* __restrict__ z, const double* __restrict__ yV,
-                                               const double* __restrict__ scal, double* __restrict__ fit,
-                                               double* __restrict__ ebv) {
+__global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict__ fit, double* __restrict__ ebv) {
   extern __shared__ double dyn[];  // alpha[nTp] then e[nV]
-  __shared__ double part[NTH / 64][TILE];
+  __shared__ double part[NTH / 64][2 * TILE];   // back-substitution partials; reused as [64][64]
   __shared__ double vsh[TILE];
+  __shared__ double wblk[KBLK];
   __shared__ double red[NTH / 64];
+  const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, nRp = c.d.nRp;
+  const double* yV = c.yV;
+  const int NT = c.d.NT;
   double* alpha = dyn;
   double* e = dyn + nTp;
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
-  const double* Kb = K + b * mstride;
-  const double* Db = Dinv + b * (int64_t)NT * TILE * TILE;
-  const double mu = scal[b * 8 + 3];
+  const double* Lb = c.L + b * nTp * nTp;
+  const double* Db = c.Dinv + b * (int64_t)NT * TILE * TILE;
+  const double* sc = c.scal + b * 8;
+  const double invN = sc[0], cN = sc[1], invd = sc[2], mu = sc[3];
   const int cp = t & 63;   // column pair: columns 2cp, 2cp+1 of the tile
   const int g = t >> 6;    // row group: rows g, g+16, ...
 
+  // alpha = L^{-T} z, block rows from the bottom, using the stored diagonal inverses
   for (int I = NT - 1; I >= 0; --I) {
-    // s = sum_{J>I} L_JI^T alpha_J
     v2d s = {0.0, 0.0};
     for (int J = I + 1; J < NT; ++J) {
-      const double* base = Kb + (int64_t)J * TILE * nTp + (int64_t)I * TILE + 2 * cp;
+      const double* base = Lb + (int64_t)J * TILE * nTp + (int64_t)I * TILE + 2 * cp;
       const double* al = alpha + J * TILE;
-#pragma unroll 8
+#pragma unroll 4
       for (int r = g; r < TILE; r += 16) {
         const v2d x = *reinterpret_cast<const v2d*>(base + (int64_t)r * nTp);
         s += x * al[r];
@@ -80,10 +81,9 @@ __global__ __launch_bounds__(NTH) void k_solve(const double* __restrict__ K, int
       double acc = 0.0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc += part[q][t];
-      vsh[t] = z[b * nTp + (int64_t)I * TILE + t] - acc;
+      vsh[t] = c.z[b * nTp + (int64_t)I * TILE + t] - acc;
     }
     __syncthreads();
-    // alpha_I = X_I^T v  (X lower triangular, zeros stored above the diagonal)
     const double* X = Db + (int64_t)I * TILE * TILE + 2 * cp;
     v2d s2 = {0.0, 0.0};
 #pragma unroll 8
@@ -103,22 +103,60 @@ __global__ __launch_bounds__(NTH) void k_solve(const double* __restrict__ K, int
     __syncthreads();
   }
 
-  // EBV_V = K_VT alpha + mu : one wave per validation row
-  for (int64_t v = w; v < nV; v += NTH / 64) {
-    const double* row = Kb + (nTp + v) * nTp;
-    double s = 0.0;
-    for (int64_t c = 2 * l; c < nT; c += 128) {
-      if (c + 1 < nT) {
-        const v2d x = *reinterpret_cast<const v2d*>(row + c);
-        s += x[0] * alpha[c] + x[1] * alpha[c + 1];
-      } else {
-        s += row[c] * alpha[c];
-      }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (l == 0) e[v] = s + mu;
+  // EBV_V = K_VT alpha + mu without materialising K_VT (exact-integer factored form):
+  //   sum_t K_vt alpha_t = [sum_s a_vs w_s - u_v S/N - (u_T . alpha)/N + cN S] / d,
+  //   w_s = sum_t a_ts alpha_t,  S = sum_t alpha_t
+  const double* ub = c.u + b * nRp;
+  double s_a = 0.0, s_ua = 0.0;
+  for (int64_t r = t; r < nT; r += NTH) {
+    s_a += alpha[r];
+    s_ua += ub[r] * alpha[r];
   }
+  const double S = block_sum(s_a, red);
+  const double UA = block_sum(s_ua, red);
+  for (int64_t v = t; v < nV; v += NTH) e[v] = 0.0;
+  const int64_t k = c.off[b + 1] - c.off[b];
+  const int64_t nblk = (k + KBLK - 1) / KBLK;
+  const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
+  const int dq = t & 15, rg = t >> 4;   // dword (4 SNPs) within a 64-SNP row block, row group (64)
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    const uint32_t* blk = pb + kb * nRp * (KBLK / 4);
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+    for (int64_t r = rg; r < nT; r += NTH / 16) {
+      const uint32_t x = blk[r * (KBLK / 4) + dq];
+      const double ar = alpha[r];
+      p0 += (double)(x & 0xff) * ar;
+      p1 += (double)((x >> 8) & 0xff) * ar;
+      p2 += (double)((x >> 16) & 0xff) * ar;
+      p3 += (double)(x >> 24) * ar;
+    }
+    __syncthreads();
+    double* pw = &part[0][0];   // [64 row groups][64 SNPs]
+    pw[rg * KBLK + 4 * dq + 0] = p0;
+    pw[rg * KBLK + 4 * dq + 1] = p1;
+    pw[rg * KBLK + 4 * dq + 2] = p2;
+    pw[rg * KBLK + 4 * dq + 3] = p3;
+    __syncthreads();
+    if (t < KBLK) {
+      double acc = 0.0;
+      for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
+      wblk[t] = acc;
+    }
+    __syncthreads();
+    for (int64_t v = t; v < nV; v += NTH) {
+      const uint32_t* row = blk + (nTp + v) * (KBLK / 4);
+      double acc = 0.0;
+#pragma unroll 4
+      for (int d4 = 0; d4 < KBLK / 4; ++d4) {
+        const uint32_t x = row[d4];
+        acc += (double)(x & 0xff) * wblk[4 * d4] + (double)((x >> 8) & 0xff) * wblk[4 * d4 + 1] +
+               (double)((x >> 16) & 0xff) * wblk[4 * d4 + 2] + (double)(x >> 24) * wblk[4 * d4 + 3];
+      }
+      e[v] += acc;
+    }
+  }
+  __syncthreads();
+  for (int64_t v = t; v < nV; v += NTH) e[v] = (e[v] - ub[nTp + v] * S * invN - UA * invN + cN * S) * invd + mu;
   __syncthreads();
 
   // Pearson correlation (scipy.stats.pearsonr restated), fitness = |r|
@@ -163,11 +201,13 @@ __global__ __launch_bounds__(NTH) void k_solve(const double* __restrict__ K, int
   }
 }
 
-hipError_t launch_solve(const double* K, const EvalDims& d, int64_t B, const double* Dinv, const double* z,
-                        const double* yV, const double* scal, double* fitness, double* ebv, hipStream_t s) {
-  const size_t shm = (size_t)(d.nTp + d.nV) * sizeof(double);
-  hipLaunchKernelGGL(k_solve, dim3((unsigned)B), dim3(NTH), shm, s, K, d.nTp, d.nT, d.nV, d.NT, d.nRp * d.nTp, Dinv,
-                     z, yV, scal, fitness, ebv);
+hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s) {
+  const size_t shm = (size_t)(c.d.nTp + c.d.nV) * sizeof(double);
+  if (shm > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_solve, dim3((unsigned)c.B), dim3(NTH), shm, s, c, fitness, ebv);
   return hipGetLastError();
 }
 

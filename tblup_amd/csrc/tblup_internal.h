@@ -58,15 +58,25 @@ hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int
 hipError_t launch_grm(const int8_t* panel, int64_t panel_stride, const int64_t* off, const double* u,
                       const double* scal, const EvalDims& d, int64_t B, double* K, hipStream_t s);
 
-// ---- launchers (k_chol.hip) ----
-hipError_t launch_chol_diag(double* K, const EvalDims& d, int64_t B, int J, double* Dinv, double* z,
-                            const double* yT, const double* scal, hipStream_t s);
-hipError_t launch_chol_offdiag(double* K, const EvalDims& d, int64_t B, int J, const double* Dinv,
-                               hipStream_t s);
-
-// ---- launchers (k_solve.hip) ----
-hipError_t launch_solve(const double* K, const EvalDims& d, int64_t B, const double* Dinv, const double* z,
-                        const double* yV, const double* scal, double* fitness, double* ebv, hipStream_t s);
+// ---- launchers (k_chol.hip, k_solve.hip) ----
+struct CholLaunch {
+  EvalDims d;
+  int64_t B;
+  double* L;             // [B][nTp][nTp] Cholesky factor (TT lower tiles)
+  double* Dinv;          // [B][NT][128][128]
+  double* z;             // [B][nTp]
+  const double* yT;      // split phenotypes [nTp]
+  const double* yV;      // [nV]
+  const int8_t* panel;   // gathered genotypes
+  int64_t pstride;       // panel bytes per individual
+  const int64_t* off;    // [B+1] device offsets
+  const double* u;       // [B][nRp]
+  const double* scal;    // [B][8]
+  int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
+};
+// one tile column J of the fused GRM + Cholesky: diag=true -> k_chol_diag, else k_chol_offdiag
+hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag);
+hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s);
 
 // XCD-aware bijective remap of a 1-D block id (blocks b and b+8 share an XCD
 // under the observed round-robin placement; speed only, never correctness).
