@@ -52,6 +52,7 @@ struct Split {
 };
 
 enum { KC_STATS = 0, KC_GATHER, KC_GRM, KC_DIAG, KC_OFFDIAG, KC_SOLVE };
+#define TBLUP_MAX_GROUPS 4
 
 struct EventPair {
   int cls;
@@ -78,6 +79,9 @@ struct tblup_ctx {
   double flops[TBLUP_N_KCLASS] = {0};
   double bytes[TBLUP_N_KCLASS] = {0};
   int64_t mem_in_use = 0;
+  int n_groups = 2;   // TBLUP_STREAMS: concurrent stream groups for the Cholesky
+  hipStream_t aux[TBLUP_MAX_GROUPS - 1] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[TBLUP_MAX_GROUPS - 1] = {};
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
 };
 
@@ -169,6 +173,9 @@ size_t chunk_bytes(const EvalDims& d, int64_t B, int64_t max_kblk, int64_t sum_k
   add((size_t)B * d.nTp * d.nTp * 8);                           // L
   add((size_t)B * d.NT * TILE * TILE * 8);                      // Dinv
   add((size_t)B * d.nTp * 8);                                   // z
+  add((size_t)B * d.nTp * 8);                                   // w
+  add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                            // SYRK partials
+  add((size_t)B * d.NT * 36 * 256 * 8);                         // diagonal GRM tiles
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nV * 8 : 0);                     // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
@@ -211,6 +218,9 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, c
   double* L = cv.take<double>((size_t)B * d.nTp * d.nTp);
   double* Dinv = cv.take<double>((size_t)B * d.NT * TILE * TILE);
   double* z = cv.take<double>((size_t)B * d.nTp);
+  double* wv = cv.take<double>((size_t)B * d.nTp);
+  double* Sp = cv.take<double>((size_t)B * TBLUP_NSLOT * 36 * 256);
+  double* Kdg = cv.take<double>((size_t)B * d.NT * 36 * 256);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
@@ -233,26 +243,66 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, c
                  [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
   }
   if (K_out) *K_out = L;
-  CholLaunch cl{d, B, L, Dinv, z, (const double*)sp.yT.p, (const double*)sp.yV.p, panel, pstride, d_off, u, scal,
+  CholLaunch cl{d, B, L, Dinv, z, wv, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p, panel, pstride, d_off, u, scal,
                 c->dbg_skip};
   const double T3 = (double)TILE * TILE * TILE;
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
+  // The batch is split into groups on separate streams so that one group's latency-bound
+  // diagonal-tile work overlaps another group's MFMA-bound off-diagonal tiles.
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_groups, B / 32));
+  hipStream_t gs[TBLUP_MAX_GROUPS];
+  CholLaunch gl[TBLUP_MAX_GROUPS];
+  for (int g = 0; g < G; ++g) {
+    const int64_t b0 = B * g / G, b1 = B * (g + 1) / G;
+    CholLaunch x = cl;
+    x.B = b1 - b0;
+    x.L = cl.L + b0 * (int64_t)d.NT * d.NT * TILE * TILE;
+    x.Dinv = cl.Dinv + b0 * (int64_t)d.NT * TILE * TILE;
+    x.z = cl.z + b0 * d.nTp;
+    x.w = cl.w + b0 * d.nTp;
+    x.S = cl.S + b0 * TBLUP_NSLOT * 36 * 256;
+    x.Kd = cl.Kd + b0 * (int64_t)d.NT * 36 * 256;
+    x.panel = cl.panel + b0 * pstride;
+    x.off = cl.off + b0;
+    x.u = cl.u + b0 * d.nRp;
+    x.scal = cl.scal + b0 * 8;
+    gl[g] = x;
+    gs[g] = (g == 0) ? s : c->aux[g - 1];
+  }
+  {
+    const double fg = (double)B * d.NT * 128.0 * 129.0 * kbar;   // int ops of the diagonal GRM tiles
+    rc = timed(c, s, KC_GRM, fg, (double)B * d.NT * 36 * 256 * 8.0, [&] { return launch_diag_grm(cl, s); });
+    if (rc) return rc;
+  }
+  if (G > 1) {
+    HIPCHK(hipEventRecord(c->ev_fork, s));
+    for (int g = 1; g < G; ++g) HIPCHK(hipStreamWaitEvent(gs[g], c->ev_fork, 0));
+  }
   for (int J = 0; J < d.NT; ++J) {
     const double jt = (double)J;
-    // algorithmic fp64 work: SYRK update of the diagonal tile, potrf + trtri, forward-substitution GEMV
-    // (the fused int8 GRM tile, 128*129*k int-ops, is not counted in these fp64 flops)
-    const double fd = (double)B * (T3 * jt + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
-    const double bd = (double)B * (TILE * TILE * jt * 8.0 + 2.0 * TILE * TILE * 8.0);
-    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol(cl, J, s, true); });
-    if (rc) return rc;
     const int nI = d.NT - J - 1;
-    if (nI > 0) {
-      // per tile: GEMM update 2*128^3*J, triangular solve 128^3 (fused GRM tile int-ops excluded)
-      const double fo = (double)B * nI * (2.0 * T3 * jt + T3);
-      const double bo = (double)B * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) +
-                        (double)B * TILE * TILE * jt * 8.0;
-      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol(cl, J, s, false); });
+    for (int g = 0; g < G; ++g) {
+      const double Bg = (double)gl[g].B;
+      // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
+      // forward-substitution GEMV (the int8 GRM tiles are counted under KC_GRM)
+      const double fd = Bg * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
+      const double bd = Bg * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
+      rc = timed(c, gs[g], KC_DIAG, fd, bd, [&] { return launch_chol(gl[g], J, gs[g], true); });
       if (rc) return rc;
+      if (nI > 0) {
+        // per tile: GEMM update 2*128^3*J, triangular solve 128^3 (fused GRM tile int-ops excluded);
+        // plus the L < J SYRK terms of diagonal tile J+1 (128^3 per L, lower half stored)
+        const double fo = Bg * nI * (2.0 * T3 * jt + T3) + Bg * T3 * jt;
+        const double bo = Bg * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * Bg * TILE * TILE * jt * 8.0;
+        rc = timed(c, gs[g], KC_OFFDIAG, fo, bo, [&] { return launch_chol(gl[g], J, gs[g], false); });
+        if (rc) return rc;
+      }
+    }
+  }
+  if (G > 1) {
+    for (int g = 1; g < G; ++g) {
+      HIPCHK(hipEventRecord(c->ev_join[g - 1], gs[g]));
+      HIPCHK(hipStreamWaitEvent(s, c->ev_join[g - 1], 0));
     }
   }
   if (stop_stage == 2) return 0;
@@ -312,6 +362,13 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
   const char* dbg = getenv("TBLUP_DBG_SKIP");
   c->dbg_skip = dbg ? atoi(dbg) : 0;
+  const char* ns = getenv("TBLUP_STREAMS");
+  c->n_groups = std::max(1, std::min(TBLUP_MAX_GROUPS, ns ? atoi(ns) : 1));
+  for (int g = 0; g < TBLUP_MAX_GROUPS - 1; ++g) {
+    HIPCHK(hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_join[g], hipEventDisableTiming));
+  }
+  HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   const size_t gbytes = (size_t)n * (size_t)P;
   if (int rc = dev_alloc(c.get(), c->geno_sm, gbytes)) return rc;
   if (int rc = dev_alloc(c.get(), c->colsum_all, (size_t)P * 4)) return rc;
@@ -348,6 +405,11 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->colsum_all.release();
   c->scratch.release();
   c->ws.release();
+  for (int g = 0; g < TBLUP_MAX_GROUPS - 1; ++g) {
+    if (c->aux[g]) (void)hipStreamDestroy(c->aux[g]);
+    if (c->ev_join[g]) (void)hipEventDestroy(c->ev_join[g]);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -576,13 +638,20 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
   std::vector<double> full((size_t)rows * d.nTp);
   HIPCHK(hipMemcpy(full.data(), K, full.size() * 8, hipMemcpyDeviceToHost));
   const int64_t nR = d.nT + d.nV;
-  for (int64_t r = 0; r < nR; ++r) {
-    if (stage == 2 && r >= d.nT) {
-      std::memset(out + r * d.nT, 0, (size_t)d.nT * 8);   // the factor has no V rows
-      continue;
+  if (stage == 2) {
+    // Lt tiles: tile (I, J) at ((I*NT + J) * 128*128), element [j][i] = L[128I+i][128J+j]
+    std::memset(out, 0, (size_t)nR * d.nT * 8);   // upper triangle and V rows are zero
+    const int64_t TT = (int64_t)TILE * TILE;
+    for (int64_t r = 0; r < d.nT; ++r)
+      for (int64_t cc = 0; cc <= r; ++cc) {
+        const int64_t I = r / TILE, Jt = cc / TILE;
+        out[r * d.nT + cc] = full[(I * d.NT + Jt) * TT + (cc % TILE) * TILE + (r % TILE)];
+      }
+  } else {
+    for (int64_t r = 0; r < nR; ++r) {
+      const int64_t src = r < d.nT ? r : d.nTp + (r - d.nT);
+      std::memcpy(out + r * d.nT, full.data() + src * d.nTp, (size_t)d.nT * 8);
     }
-    const int64_t src = r < d.nT ? r : d.nTp + (r - d.nT);
-    std::memcpy(out + r * d.nT, full.data() + src * d.nTp, (size_t)d.nT * 8);
   }
   if (z_out) {
     std::vector<double> zz(d.nTp);

@@ -1,108 +1,164 @@
-// Batched left-looking tile Cholesky of (K_TT + lambda I), fp64, 128x128 tiles.
+// Batched left-looking tile Cholesky of (K_TT + lambda I), fp64, 128x128 tiles,
+// with the GRM tiles rebuilt on the fly from the int8 panel (K is never stored).
 //
 // Replaces the reference's per-individual dense solves
 //   gblup:    G_inv = np.linalg.inv(G_TT + lambda I)          (tblup/evaluator.py:280-284)
 //   snp_blup: Ridge(alpha).fit -> scipy.linalg.solve(assume_a="pos") (evaluator.py:311-312,
 //             scikit-learn 1.7.2 _ridge.py _solve_cholesky[_kernel])
-// by one Cholesky factorisation per individual, batched over the population:
-// for each tile column J
-//   k_chol_diag    (one WG per individual): T = A_JJ - sum_L L_JL L_JL^T on fp64 MFMA,
-//                  in-register right-looking factorisation of T that also produces
-//                  inv(L_JJ) (row operations applied to I) and the forward-substitution
-//                  block z_J = L_JJ^{-1}(y_J - mu - sum_L L_JL z_L)
-//   k_chol_offdiag (one WG per individual x tile row I > J):
-//                  T = A_IJ - sum_L L_IL L_JL^T, then L_IJ = T inv(L_JJ)^T, both on MFMA.
-// fp64 MFMA: v_mfma_f64_16x16x4_f64, A[i=l&15][k=l>>4], B[k=l>>4][j=l&15],
-// C/D row=(l>>4)+4r, col=l&15 (verified on gfx950 by tools/mfma_probe.hip).
+// by one Cholesky factorisation per individual, batched over the population.
+// For each tile column J:
+//   k_chol_diag    (one WG per individual): K_JJ (int8 MFMA) - sum_L L_JL L_JL^T (fp64 MFMA
+//                  SYRK on the lower blocks), blocked 16x16 factorisation, blocked inverse
+//                  X_J = L_JJ^{-1}, forward-substitution block z_J = X_J (y_J - mu - w_J)
+//   k_chol_offdiag (one WG per individual x tile row I > J), all transposes in registers:
+//                  T^T = K_JI - sum_L L_JL L_IL^T  (int8 MFMA for K, fp64 MFMA, acc = T^T)
+//                  L_IJ^T = X_J T^T               (acc of T^T is the B operand directly)
+//                  w_I += L_IJ z_J                (forward-substitution partial sums)
+//
+// Storage of L ("Lt"): tile-contiguous and transposed.  Tile (I, J), I >= J, of matrix b
+// is 128x128 doubles at L + ((b*NT + I)*NT + J)*128*128 with Lt[j][i] = L[128I+i][128J+j],
+// so a 16-k-row stage of any operand is 16 KiB contiguous and every tile write coalesces.
+//
+// MFMA layouts (verified on gfx950 by tools/mfma_probe*.hip):
+//   f64 16x16x4 : A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], C row=(l>>4)+4r, col=l&15
+//   i8 16x16x64 : A row l&15, B col l&15, 16 B of k per lane, C row=4(l>>4)+r, col=l&15
+//   i8 32x32x32 : C row=(r&3)+8(r>>2)+4(l>>5), col=l&31
+// Reading the i8 16x16x64 A rows through the permutation pi(rho) = (rho>>2) + 4(rho&3)
+// makes its accumulator land in the f64 C layout, so the exact integer GRM counts
+// become the fp64 accumulators of the Cholesky GEMM without any data movement.
 #include "i8_tile.h"
+#include <algorithm>
 
 namespace tblup {
 
 namespace {
 
-constexpr int BKD = 16;               // fp64 K step (128 B per row)
-constexpr int STAGE = TILE * BKD;     // doubles per operand stage
-
-__device__ __forceinline__ int st_off(int row, int k) {
-  // [128 rows][16 doubles]; 16-B chunk c=k>>1 of row r stored at c ^ ((r>>1)&7):
-  // conflict-free ds_read_b64 for the f64 16x16x4 fragment pattern.
-  return row * BKD + 2 * ((k >> 1) ^ ((row >> 1) & 7)) + (k & 1);
-}
-
-__device__ __forceinline__ int t_off(int row, int col) {
-  // [128][128] doubles, 16-B chunk swizzle by (row & 15): conflict-free A-fragment reads.
-  return row * TILE + 2 * ((col >> 1) ^ (row & 15)) + (col & 1);
-}
+constexpr int BKD = 16;                // k rows per fp64 stage
+constexpr int LTS = BKD * TILE;        // doubles in one 16-row stage of an Lt tile (16 KiB)
+constexpr int TT = TILE * TILE;        // doubles per tile
+constexpr int NSX_MAX = 4;             // SYRK partials of L < J-1 (computed in the previous off-diagonal launch)
+constexpr int NSLOT = TBLUP_NSLOT;     // + one slot for the assembled tile (k_diag_prep)
+static_assert(NSLOT == NSX_MAX + 1, "slot layout");
 
 __device__ __forceinline__ v4d mfma64(double a, double b, v4d c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// acc[m][n] += sum_{k < kmax} A[64wr+16m+i][k] * Bm[64wc+16n+j][k]  (row-major, ld)
-// 256 threads, double-buffered LDS staging with register prefetch.
-// OnStage(buf_ptr, k0) is called by every thread once per staged A panel.
-template <bool SAME, typename OnStage, bool NEG_A = false>
-__device__ __forceinline__ void gemm_nt_f64(const double* __restrict__ A, const double* __restrict__ Bm, int64_t ld,
-                                            int kmax, v4d (&acc)[4][4], double* lds, OnStage on_stage) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  double* As0 = lds;
-  double* As1 = lds + (SAME ? 1 : 2) * STAGE;
-  double* Bs0 = SAME ? As0 : lds + STAGE;
-  double* Bs1 = SAME ? As1 : lds + 3 * STAGE;
-  v2d ra[4], rb[4];
-  const int nst = kmax / BKD;
-  if (nst == 0) return;
-  auto gload = [&](int k0) {
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Stage image [16 k][128 x] of an Lt tile: 16-B chunk p of row k holds source chunk
+// p ^ 8(k&1), so the fragment pattern (16 x in one k row, the next k in lanes 16-31)
+// covers all 64 banks.  One LDS-DMA instruction moves one 1 KiB k row.
+__device__ __forceinline__ int lt_off(int k, int x) { return k * TILE + 2 * ((x >> 1) ^ (8 * (k & 1))) + (x & 1); }
+
+__device__ __forceinline__ void glds_lt_stage(const double* __restrict__ src, double* stage) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = t + 256 * e, r = q >> 3, c = q & 7;
-      ra[e] = *reinterpret_cast<const v2d*>(A + (int64_t)r * ld + k0 + 2 * c);
-      if (!SAME) rb[e] = *reinterpret_cast<const v2d*>(Bm + (int64_t)r * ld + k0 + 2 * c);
-    }
-  };
-  auto swrite = [&](double* as, double* bs) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = t + 256 * e, r = q >> 3, c = q & 7;
-      const int o = r * BKD + 2 * (c ^ ((r >> 1) & 7));
-      *reinterpret_cast<v2d*>(as + o) = NEG_A ? -ra[e] : ra[e];
-      if (!SAME) *reinterpret_cast<v2d*>(bs + o) = rb[e];
-    }
-  };
-  gload(0);
-  swrite(As0, Bs0);
-  __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    const bool odd = (s & 1) != 0;
-    const double* As = odd ? As1 : As0;
-    const double* Bs = odd ? Bs1 : Bs0;
-    if (s + 1 < nst) gload((s + 1) * BKD);
-    on_stage(As, s * BKD);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * kk + (l >> 4);
-      double a[4], bv[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = As[st_off(64 * wr + 16 * m + (l & 15), k)];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bv[n] = Bs[st_off(64 * wc + 16 * n + (l & 15), k)];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma64(a[m], bv[n], acc[m][n]);
-    }
-    if (s + 1 < nst) swrite(odd ? As0 : As1, odd ? Bs0 : Bs1);
-    __syncthreads();
+  for (int e = 0; e < 4; ++e) {
+    const int k = 4 * w + e;
+    __builtin_amdgcn_global_load_lds(src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(stage + k * TILE), 16, 0,
+                                     0);
   }
 }
 
-struct NoStage {
-  __device__ void operator()(const double*, int) const {}
-};
+// ---- int8 GRM tile in the f64 accumulator layout (offdiag) ----
+// cnt[cb][ib] = sum_s A[16cb + pi-row][s] B[32w + 16ib + col][s] with A = panel rows of tile J
+// (c) and B = panel rows of tile I (i).  Panel tiles [128 rows][64 B]; A chunk swizzle
+// (row>>2)&3 and B chunk swizzle (row>>2)&2 keep both ds_read_b128 patterns conflict-free.
+__device__ __forceinline__ int i8off_a(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
+__device__ __forceinline__ int i8off_b(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 2)); }
 
-// ---- SYRK restricted to the 36 lower 16x16 blocks of a 128x128 tile ----
-// Block e (row-major over q >= s) goes to wave e % 4: 9 blocks per wave, so the
-// lower triangle costs 36 block-MFMA streams instead of the 64 of a full GEMM.
+template <int D>
+__device__ __forceinline__ void i8_tt(const int8_t* __restrict__ pa, const int8_t* __restrict__ pb, int64_t nblk,
+                                      int64_t kb_stride, int8_t* lds, v4i (&cnt)[8][2]) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = v4i{0, 0, 0, 0};
+  if (nblk <= 0) return;
+  constexpr int TB = TILE * KBLK;
+  auto issue = [&](int64_t kb) {
+    int8_t* slot = lds + (int)(kb % D) * 2 * TB;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int cblk = 2 * w + e, q = cblk * 64 + l, row = q >> 2, pos = q & 3;
+      __builtin_amdgcn_global_load_lds(pa + kb * kb_stride + row * 64 + 16 * (pos ^ ((row >> 2) & 3)),
+                                       (lds_ptr_t)(slot + cblk * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(pb + kb * kb_stride + row * 64 + 16 * (pos ^ ((row >> 2) & 2)),
+                                       (lds_ptr_t)(slot + TB + cblk * 1024), 16, 0, 0);
+    }
+  };
+  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    if (kb + D - 2 < nblk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kb + D - 1 < nblk) issue(kb + D - 1);
+    const int8_t* As = lds + (int)(kb % D) * 2 * TB;
+    const int8_t* Bs = As + TB;
+    v4i bv[2];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) bv[ib] = *reinterpret_cast<const v4i*>(Bs + i8off_b(32 * w + 16 * ib + rho, ch));
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const v4i av = *reinterpret_cast<const v4i*>(As + i8off_a(16 * cb + prow, ch));
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[ib], cnt[cb][ib], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// ---- GEMM1 of the off-diagonal kernel: acc[cb][ib] -= sum_{k < 128J} L_J[c][k] L_I[i][k] ----
+// A = Lt tiles (J, L), B = Lt tiles (I, L), L < J; LDS-DMA ring of D slots x 32 KiB.
+template <int D>
+__device__ __forceinline__ void gemm1_tt(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
+                                         double* lds, v4d (&acc)[8][2]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nst = 8 * J;
+  if (nst == 0) return;
+  auto issue = [&](int s) {
+    double* slot = lds + (s % D) * 2 * LTS;
+    const int64_t src = (int64_t)(s >> 3) * TT + (s & 7) * LTS;
+    glds_lt_stage(ltJ + src, slot);
+    glds_lt_stage(ltI + src, slot + LTS);
+  };
+  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    if (s + D - 2 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 8) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + D - 1 < nst) issue(s + D - 1);
+    const double* As = lds + (s % D) * 2 * LTS;
+    const double* Bs = As + LTS;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * kk + (l >> 4);
+      double bv[2];
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) bv[ib] = Bs[lt_off(k, 32 * w + 16 * ib + (l & 15))];
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        const double av = -As[lt_off(k, 16 * cb + (l & 15))];
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) acc[cb][ib] = mfma64(av, bv[ib], acc[cb][ib]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// ---- SYRK restricted to the 36 lower 16x16 blocks (diag kernel), A = Lt tiles (J, L) ----
 __host__ __device__ constexpr int tri_q(int e) {
   int q = 0;
   while ((q + 1) * (q + 2) / 2 <= e) ++q;
@@ -117,54 +173,36 @@ __device__ __forceinline__ void syrk_stage(const double* As, v4d (&acc)[9], int 
     const int k = 4 * kk + (l >> 4);
     double a8[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) a8[q] = As[st_off(16 * q + (l & 15), k)];
+    for (int q = 0; q < 8; ++q) a8[q] = As[lt_off(k, 16 * q + (l & 15))];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int e = W + 4 * i;
-      acc[i] = mfma64(a8[tri_q(e)], a8[tri_s(e)], acc[i]);
-    }
+    for (int i = 0; i < 9; ++i) acc[i] = mfma64(a8[tri_q(W + 4 * i)], a8[tri_s(W + 4 * i)], acc[i]);
   }
 }
 
-// acc[i] (block e = w + 4i) += sum_{k < kmax} A[16q + r][k] A[16s + c][k]; staging as gemm_nt_f64<true>.
-template <typename OnStage>
-__device__ __forceinline__ void syrk_lower_f64(const double* __restrict__ A, int64_t ld, int kmax, v4d (&acc)[9],
-                                               double* lds, OnStage on_stage) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  double* As0 = lds;
-  double* As1 = lds + STAGE;
-  v2d ra[4];
-  const int nst = kmax / BKD;
-  if (nst == 0) return;
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = t + 256 * e, r = q >> 3, c = q & 7;
-      ra[e] = *reinterpret_cast<const v2d*>(A + (int64_t)r * ld + k0 + 2 * c);
-    }
-  };
-  auto swrite = [&](double* as) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = t + 256 * e, r = q >> 3, c = q & 7;
-      *reinterpret_cast<v2d*>(as + r * BKD + 2 * (c ^ ((r >> 1) & 7))) = ra[e];
-    }
-  };
-  gload(0);
-  swrite(As0);
-  __syncthreads();
+// nst consecutive 16-row stages starting at src (the Lt tiles (J, 0..) of one tile row are
+// contiguous, so stage s of the row lives at s * LTS).
+template <int D>
+__device__ __forceinline__ void syrk_lower(const double* __restrict__ src, int nst, double* lds, v4d (&acc)[9]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (nst <= 0) return;
+  auto issue = [&](int s) { glds_lt_stage(src + (int64_t)s * LTS, lds + (s % D) * LTS); };
+  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
   for (int s = 0; s < nst; ++s) {
-    const bool odd = (s & 1) != 0;
-    const double* As = odd ? As1 : As0;
-    if (s + 1 < nst) gload((s + 1) * BKD);
-    on_stage(As, s * BKD);
+    if (s + D - 2 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + D - 1 < nst) issue(s + D - 1);
+    const double* As = lds + (s % D) * LTS;
     if (w == 0) syrk_stage<0>(As, acc, l);
     else if (w == 1) syrk_stage<1>(As, acc, l);
     else if (w == 2) syrk_stage<2>(As, acc, l);
     else syrk_stage<3>(As, acc, l);
-    if (s + 1 < nst) swrite(odd ? As0 : As1);
-    __syncthreads();
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 
 // ---- packed lower-triangular 16x16 block storage of a 128x128 tile in LDS ----
@@ -195,12 +233,21 @@ __device__ __forceinline__ v4d mma_abt(const double* A, const double* Bt, v4d ac
 //   c == j: E_ij = -T_ij / piv_j (i > j), 1 (i == j)
 //   c < j : E_ic -= (T_ij / piv_j) E_jc
 // L = L' D^{1/2}  ->  L_ij = T_ij / sqrt(piv_j);  X = D^{-1/2} E.
-__device__ __forceinline__ void factor16(double* D, double* X, int l) {
+// The per-step critical path is the shuffles, one Newton reciprocal and one FMA per
+// element (branch-free selects); column scaling by 1/sqrt(piv) is deferred to the end.
+__device__ __forceinline__ double recip(double p) {
+  double r = __builtin_amdgcn_rcp(p);
+  double e = __builtin_fma(-p, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-p, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+__device__ __forceinline__ void factor16(double* D, double* X, double* piv_sh, int l) {
   const int i = l & 15, g = l >> 4;
   double v[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) v[q] = D[bo(i, 4 * g + q)];
-  double piv_own = 1.0;
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int jg = j >> 2, jq = j & 3;
@@ -212,36 +259,42 @@ __device__ __forceinline__ void factor16(double* D, double* X, int l) {
       cc[q] = __shfl(v[jq], 4 * g + q + 16 * jg);
       ej[q] = __shfl(v[q], j + 16 * g);
     }
-    if (g == jg && i >= j) D[bo(i, j)] = ci / sqrt(piv);
-    if (i == j) piv_own = piv;
-    const double li = ci / piv;
+    if (g == jg && i >= j) D[bo(i, j)] = ci;   // raw column, scaled after the loop
+    if (l == j) piv_sh[j] = piv;
+    const double li = ci * recip(piv);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = 4 * g + q;
-      if (c > j) {
-        if (i >= c) v[q] -= li * cc[q];
-      } else if (c == j) {
-        if (i >= j) v[q] = (i == j) ? 1.0 : -li;
-      } else {
-        if (i > j) v[q] -= li * ej[q];
-      }
+      const bool upd_t = (c > j) && (i >= c);
+      const bool upd_e = (c < j) && (i > j);
+      const bool conv = (c == j) && (i >= j);
+      const double nv = __builtin_fma(-li, upd_t ? cc[q] : ej[q], v[q]);
+      const double cv = (i == j) ? 1.0 : -li;
+      v[q] = (upd_t || upd_e) ? nv : (conv ? cv : v[q]);
     }
   }
-  const double rs = 1.0 / sqrt(piv_own);
+  // deferred scaling: L_ij = T_ij / sqrt(piv_j), X_ic = E_ic / sqrt(piv_i)
+  const double rs_own = 1.0 / sqrt(piv_sh[i]);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = 4 * g + q;
-    X[bo(i, c)] = (i >= c) ? v[q] * rs : 0.0;
+    X[bo(i, c)] = (i >= c) ? v[q] * rs_own : 0.0;
+    if (i >= c) D[bo(i, c)] = D[bo(i, c)] * (1.0 / sqrt(piv_sh[c]));
   }
 }
+
 
 }  // namespace
 
 // Per-launch arguments shared by the two Cholesky kernels.
 struct CholArgs {
-  double* L;                // [B][nTp][nTp] factor (TT lower tiles)
+  double* L;                // Lt tiles [B][NT][NT][128*128]
   double* Dinv;             // [B][NT][128][128]
   double* z;                // [B][nTp]
+  double* w;                // [B][nTp] forward-substitution partial sums
+  double* S;                // [B][NSLOT][36*256] SYRK partials of a diagonal tile
+  double* Kd;               // [B][NT][36*256] GRM diagonal tiles (k_diag_grm)
+  int NSX;                  // prep: L<J-1 partials to sum; offdiag: extra SYRK workgroups per individual
   const double* yT;         // [nTp]
   const int8_t* panel;      // [B] x pstride
   int64_t pstride;
@@ -254,96 +307,183 @@ struct CholArgs {
 };
 
 // ---------------------------------------------------------------------------
-// diagonal tile: fused GRM tile, SYRK update, blocked factorisation, blocked
-// inverse, forward solve
+// Diagonal tile T_J = K_JJ - sum_{L<J} L_JL L_JL^T is assembled from pieces that are
+// computed OFF the column-to-column critical path:
+//   K_JJ            k_diag_grm, all J of the batch in one launch up front
+//   L < J-1 terms   extra workgroups of the off-diagonal launch of column J-1
+//   L = J-1 term    k_diag_prep right before the diagonal kernel (split over k)
+// Each piece is written in the packed block layout the diagonal kernel factorises in,
+// so the diagonal kernel sums them with a linear sweep.
 // ---------------------------------------------------------------------------
-//   0. K_JJ from the panel on int8 MFMA (exact counts + fp64 centring) -> packed lower blocks
-//   A. acc = sum_{L<J} L_JL L_JL^T (fp64 MFMA), w = sum_{L<J} L_JL z_L (fused)
-//   B. T = K_JJ - acc (in place, packed lower 16x16 blocks); r = y_J - mu - w
-//   C. for panel p: one wave factors T_pp (-> L_pp, X_pp = L_pp^{-1});
-//      all waves: L_qp = T_qp X_pp^T (q > p); T_qs -= L_qp L_sp^T (q >= s > p)   [MFMA]
-//   D. blocked inverse X = L^{-1}: X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
-//   E. write L (lower blocks), X to Dinv (zeros above the diagonal), z_J = X r
-__global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];  // 144 KiB: T blocks | X blocks (+staging)
-  __shared__ double rsh[TILE];
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  const int64_t b = blockIdx.x, nTp = a.nTp;
-  const int J = a.J;
-  double* Lb = a.L + b * nTp * nTp;
-  const int64_t j0 = (int64_t)J * TILE;
-  const double* zb = a.z + b * nTp;
-  const double* sc = a.scal + b * 8;
-  const double invN = sc[0], cN = sc[1], invd = sc[2], mu = sc[3], lam = sc[4];
-  const double* ub = a.u + b * a.nRp;
-  double* Tp = lds;
-  double* Xp = lds + NPACK * BLKD;   // also the staging area of steps 0 and A
-
-  // 0. fused GRM tile K_JJ (lower 16x16 blocks only)
-  if (!(a.skip & 1)) {
-    const int64_t k = a.off[b + 1] - a.off[b];
-    const int8_t* pj = a.panel + b * a.pstride + j0 * KBLK;
-    v16i ci[2][2];
-    i8_tile_gemm_ring<true, 8>(pj, pj, (k + KBLK - 1) / KBLK, a.nRp * KBLK, reinterpret_cast<int8_t*>(Xp), ci);
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int col = i8_col(wc, n, l);
-        const int64_t gj = j0 + col;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = i8_row(wr, m, r, l);
-          if ((row >> 4) >= (col >> 4)) {
-            const int64_t gi = j0 + row;
-            double v;
-            if (gi < a.nT && gj < a.nT) {
-              v = grm_value(ci[m][n][r], ub[gi], ub[gj], invN, cN, invd);
-              if (gi == gj) v += lam;
-            } else {
-              v = (gi == gj) ? 1.0 : 0.0;
-            }
-            Tp[pk(row >> 4, col >> 4) + bo(row & 15, col & 15)] = v;
-          }
-        }
-      }
-  }
-
+__device__ __forceinline__ void syrk_partial(const CholArgs& a, int64_t b, int Jt, int s0, int s1, int slot,
+                                             double* lds) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   v4d acc[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-  double wpart = 0.0;
-  auto on_stage = [&](const double* As, int k0) {
-    if (t < TILE) {
+  if (!(a.skip & 2))
+    syrk_lower<4>(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT + (int64_t)s0 * LTS, s1 - s0, lds, acc);
+  double* Pd = a.S + (b * NSLOT + slot) * (int64_t)NPACK * BLKD;
 #pragma unroll
-      for (int kk = 0; kk < BKD; ++kk) wpart += As[st_off(t, kk)] * zb[k0 + kk];
-    }
-  };
-  __syncthreads();
-  if (J > 0 && !(a.skip & 2)) syrk_lower_f64(Lb + j0 * nTp, nTp, (int)j0, acc, Xp, on_stage);
+  for (int i = 0; i < 9; ++i) {
+    const int e = w + 4 * i, q = tri_q(e), sb = tri_s(e);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Pd[pk(q, sb) + bo((l >> 4) + 4 * r, l & 15)] = -acc[i][r];
+  }
+}
 
-  // B. T = K_JJ - acc on the lower blocks (wave w holds blocks e = w + 4i)
-  if (J > 0) {
+// K_JJ for every (individual, J): int8 MFMA tile, exact counts + fp64 centring, + lambda I,
+// identity on padded rows; packed lower 16x16 blocks into Kd[b][J].
+__global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[8 * TILE * KBLK];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  const int NT = a.NT;
+  const int64_t b = blockIdx.x / NT;
+  const int J = (int)(blockIdx.x % NT);
+  const int64_t j0 = (int64_t)J * TILE;
+  const int64_t k = a.off[b + 1] - a.off[b];
+  const int8_t* pj = a.panel + b * a.pstride + j0 * KBLK;
+  const double* sc = a.scal + b * 8;
+  const double invN = sc[0], cN = sc[1], invd = sc[2], lam = sc[4];
+  const double* ub = a.u + b * a.nRp;
+  double* Kd = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
+  v16i ci[2][2];
+  if (!(a.skip & 1)) {
+    i8_tile_gemm_ring<true, 8>(pj, pj, (k + KBLK - 1) / KBLK, a.nRp * KBLK, lds, ci);
+  } else {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int e = w + 4 * i, q = tri_q(e), sb = tri_s(e);
+    for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Tp[pk(q, sb) + bo((l >> 4) + 4 * r, l & 15)] -= acc[i][r];
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ci[m][n][r] = 0;
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int col = i8_col(wc, n, l);
+      const int64_t gj = j0 + col;
+      const double uj = ub[gj];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = i8_row(wr, m, r, l);
+        if ((row >> 4) >= (col >> 4)) {
+          const int64_t gi = j0 + row;
+          const double kv = grm_value(ci[m][n][r], ub[gi], uj, invN, cN, invd);
+          const double v = (gi < a.nT && gj < a.nT) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
+          Kd[pk(row >> 4, col >> 4) + bo(row & 15, col & 15)] = v;
+        }
+      }
     }
+}
+
+// Assemble T_J = K_JJ + sum of the L < J-1 partials - L_{J,J-1} L_{J,J-1}^T into slot NSX_MAX.
+// Grid B x 4: workgroup g owns the 9 packed blocks {g + 4i}; its wave v takes k rows
+// [32v, 32v+32) of Lt tile (J, J-1) straight from global (16 lanes read one 128-B row
+// segment), the 4 waves are reduced through LDS and the sum is written once.
+template <int W>
+__device__ __forceinline__ void syrk_rows_global(const double* __restrict__ lt, int k0, v4d (&acc)[9], int l) {
+#pragma unroll 2
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = k0 + 4 * kk + (l >> 4);
+    double a8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a8[q] = lt[k * TILE + 16 * q + (l & 15)];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) acc[i] = mfma64(a8[tri_q(W + 4 * i)], a8[tri_s(W + 4 * i)], acc[i]);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void k_diag_prep(CholArgs a) {
+  __shared__ double red[4][9][BLKD];   // 72 KiB
+  const int t = threadIdx.x, l = t & 63, v = t >> 6;
+  const int J = a.J, NT = a.NT;
+  const int64_t b = blockIdx.x >> 2;
+  const int g = blockIdx.x & 3;
+  v4d acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
+  if (!(a.skip & 2)) {
+    const double* lt = a.L + ((b * NT + J) * (int64_t)NT + (J - 1)) * TT;
+    if (g == 0) syrk_rows_global<0>(lt, 32 * v, acc, l);
+    else if (g == 1) syrk_rows_global<1>(lt, 32 * v, acc, l);
+    else if (g == 2) syrk_rows_global<2>(lt, 32 * v, acc, l);
+    else syrk_rows_global<3>(lt, 32 * v, acc, l);
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[v][i][bo((l >> 4) + 4 * r, l & 15)] = acc[i][r];
+  __syncthreads();
+  const double* Kb = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
+  double* Sb = a.S + b * (int64_t)NSLOT * NPACK * BLKD;
+  const int nsx = a.NSX;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int e = g + 4 * i;
+    const int off = pk(tri_q(e), tri_s(e)) + t;
+    double sum = Kb[off];
+#pragma unroll
+    for (int q = 0; q < NSX_MAX; ++q) {
+      const double pq = Sb[q * NPACK * BLKD + off];
+      sum += (q < nsx) ? pq : 0.0;
+    }
+    sum -= (red[0][i][t] + red[1][i][t]) + (red[2][i][t] + red[3][i][t]);
+    Sb[NSX_MAX * NPACK * BLKD + off] = sum;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// diagonal tile
+//   A. T = K_JJ - sum_{L<J} L_JL L_JL^T = Kd + partials; r = y_J - mu - w_J
+//   C. for panel p: one wave factors T_pp (-> L_pp, X_pp = L_pp^{-1});
+//      all waves: L_qp = T_qp X_pp^T (q > p); T_qs -= L_qp L_sp^T (q >= s > p)   [MFMA]
+//   D. blocked inverse X = L^{-1}: X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
+//      (off-diagonal X blocks written to / re-read from Dinv, diagonal ones stay in LDS)
+//   E. write L_JJ^T (Lt tile), X_J^T (Dinv, zeros below its diagonal), z_J = X_J r
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
+  // 72 KiB of T blocks + 16 KiB of diagonal X blocks: small enough to share a CU with an
+  // off-diagonal workgroup of another stream group.  Off-diagonal X blocks live in Dinv.
+  __shared__ __attribute__((aligned(16))) double lds[(NPACK + NBLK) * BLKD];
+  __shared__ double rsh[TILE];
+  __shared__ double piv_sh[NB];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int64_t b = blockIdx.x, nTp = a.nTp;
+  const int J = a.J, NT = a.NT;
+  const int64_t j0 = (int64_t)J * TILE;
+  const double* sc = a.scal + b * 8;
+  const double mu = sc[3];
+  double* Tp = lds;
+  double* Xd = lds + NPACK * BLKD;   // X_pp, p = 0..7
+  double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;   // X^T, row-major: XT[c][i] = X[i][c]
+
+  // T = K_JJ - sum_{L<J} L_JL L_JL^T: k_diag_grm's tile for J = 0, else k_diag_prep's sum
+  {
+    const double* src = (J == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
+                                 : a.S + (b * NSLOT + NSX_MAX) * (int64_t)NPACK * BLKD;
+#pragma unroll
+    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread, LDS-DMA
+      const int chunk = (e * 4 + w) * 64;
+      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (t < TILE) {
     const int64_t gi = j0 + t;
-    rsh[t] = (gi < a.nT) ? (a.yT[gi] - mu - wpart) : 0.0;
+    const double wv = (J > 0) ? a.w[b * nTp + gi] : 0.0;
+    rsh[t] = (gi < a.nT) ? (a.yT[gi] - mu - wv) : 0.0;
   }
   __syncthreads();
 
   // C. blocked right-looking factorisation over 16-column panels
   for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
-    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xp + pk(p, p), l);
+    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xd + p * BLKD, piv_sh, l);
     __syncthreads();
     for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += 4) {
       v4d x = {0.0, 0.0, 0.0, 0.0};
-      x = mma_abt(Tp + pk(q, p), Xp + pk(p, p), x, l);
+      x = mma_abt(Tp + pk(q, p), Xd + p * BLKD, x, l);
 #pragma unroll
       for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
     }
@@ -361,181 +501,211 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
     }
     __syncthreads();
   }
+  if (a.skip & 16) return;
 
-  // D. blocked inverse, one block diagonal per round
+  // E1. X^T tile: diagonal blocks from Xd, zeros where X is zero (block row > block col of X^T)
+  for (int e = t; e < TT; e += 256) {
+    const int rr = e >> 7, cc = e & 127;
+    if ((rr >> 4) == (cc >> 4)) XT[e] = Xd[(rr >> 4) * BLKD + bo(cc & 15, rr & 15)];
+    else if ((rr >> 4) > (cc >> 4)) XT[e] = 0.0;
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  // D. blocked inverse, one block diagonal per round, off-diagonal blocks through Dinv:
+  //    X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
   for (int dd = 1; dd < ((a.skip & 8) ? 0 : NBLK); ++dd) {
     for (int jb = w; jb + dd < NBLK; jb += 4) {
       const int q = jb + dd;
       v4d sacc = {0.0, 0.0, 0.0, 0.0};
       for (int lb = jb; lb < q; ++lb) {
         const double* A = Tp + pk(q, lb);
-        const double* Xb = Xp + pk(lb, jb);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int k = 4 * kk + (l >> 4);
-          sacc = mfma64(A[bo(l & 15, k)], Xb[bo(k, l & 15)], sacc);
+          // B[k][c] = X_{lb,jb}[k][c] = XT[16jb + c][16lb + k]
+          const double xb = (lb == jb) ? Xd[jb * BLKD + bo(k, l & 15)] : XT[(16 * jb + (l & 15)) * TILE + 16 * lb + k];
+          sacc = mfma64(A[bo(l & 15, k)], xb, sacc);
         }
       }
-      // X_{q,jb} = -X_{q,q} S ; S in C layout feeds the B operand directly (k = 4kk + (l>>4))
       v4d xo = {0.0, 0.0, 0.0, 0.0};
-      const double* Xqq = Xp + pk(q, q);
+      const double* Xqq = Xd + q * BLKD;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) xo = mfma64(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Xp[pk(q, jb) + bo((l >> 4) + 4 * r, l & 15)] = -xo[r];
+      for (int r = 0; r < 4; ++r)   // X_{q,jb}[i][c] -> XT[16jb + c][16q + i]
+        XT[(16 * jb + (l & 15)) * TILE + 16 * q + (l >> 4) + 4 * r] = -xo[r];
     }
+    __threadfence_block();
     __syncthreads();
   }
 
-  // E. outputs
-  double* Db = a.Dinv + (b * a.NT + J) * (int64_t)(TILE * TILE);
-  if (a.skip & 16) return;
-  for (int e = t; e < TILE * TILE; e += 256) {
-    const int rr = e >> 7, cc = e & 127, q = rr >> 4, sb = cc >> 4;
-    double xv = 0.0;
-    if (q >= sb) {
-      xv = Xp[pk(q, sb) + bo(rr & 15, cc & 15)];
-      if (rr >= cc) Lb[(j0 + rr) * nTp + j0 + cc] = Tp[pk(q, sb) + bo(rr & 15, cc & 15)];
-    }
-    Db[e] = xv;
+  // E2. L_JJ^T into the Lt tile (J, J); z_J = X_J r  (z_i = sum_c XT[c][i] r_c)
+  double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
+  for (int e = t; e < TT; e += 256) {
+    const int rr = e >> 7, cc = e & 127;
+    Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
   }
   if (t < TILE) {
-    const int q = t >> 4;
     double acc_z = 0.0;
-    for (int sb = 0; sb <= q; ++sb) {
-      const double* Xb = Xp + pk(q, sb);
-#pragma unroll
-      for (int c = 0; c < NB; ++c) acc_z += Xb[bo(t & 15, c)] * rsh[16 * sb + c];
-    }
+    for (int c = 0; c <= t; ++c) acc_z += XT[c * TILE + t] * rsh[c];
     a.z[b * nTp + j0 + t] = acc_z;
   }
 }
 
 // ---------------------------------------------------------------------------
-// off-diagonal tiles of column J: L_IJ = (K_IJ - sum_L L_IL L_JL^T) inv(L_JJ)^T
-//   0. K_IJ from the panel (int8 MFMA) -> fp64 image in LDS -> accumulators
-//   1. acc -= sum_L L_IL L_JL^T (fp64 MFMA, A operand negated at staging)
-//   2. L_IJ = T X^T with X = inv(L_JJ) lower triangular (fp64 MFMA)
+// off-diagonal tiles of column J (one WG per individual x tile row I > J)
+//   0. cnt = A_J A_I^T on int8 MFMA, landing in the f64 layout; acc = K_JI = K_IJ^T
+//   1. acc -= sum_{L<J} L_JL L_IL^T          (acc = T^T, wave w holds all c x its 32 i)
+//   2. out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb]   (X = inv(L_JJ); acc is the B operand)
+//      -> Lt tile (I, J); w_I += L_IJ z_J
+// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_chol_offdiag(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) double lds[TILE * TILE + STAGE];  // T image + X stage (144 KiB)
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+__global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int64_t n_tiles) {
+  __shared__ __attribute__((aligned(16))) double lds[4 * LTS];   // 64 KiB
+  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[TILE];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int J = a.J, NT = a.NT;
   const int nI = NT - J - 1;
-  const int64_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
+  if ((int64_t)blockIdx.x < n_extra) {
+    // extra role (first in the grid, so it overlaps the tiles): SYRK partials of diagonal
+    // tile J+1 over L < J, all of which are final already
+    const int64_t b = blockIdx.x / a.NSX;
+    const int part = (int)(blockIdx.x % a.NSX);
+    syrk_partial(a, b, J + 1, part * 8 * J / a.NSX, (part + 1) * 8 * J / a.NSX, part, lds);
+    return;
+  }
+  const int64_t logical = xcd_remap(blockIdx.x - n_extra, n_tiles);
   const int64_t b = logical / nI;
   const int I = J + 1 + (int)(logical % nI);
   const int64_t nTp = a.nTp;
-  double* Lb = a.L + b * nTp * nTp;
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
-  double* Tl = lds;
-  double* Xs = lds + TILE * TILE;
+  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+  const double* sc = a.scal + b * 8;
+  const double invN = sc[0], cN = sc[1], invd = sc[2];
+  if (t < TILE) {
+    uj_sh[t] = a.u[b * a.nRp + j0 + t];
+    ui_sh[t] = a.u[b * a.nRp + i0 + t];
+    zj_sh[t] = a.z[b * nTp + j0 + t];
+  }
+  __syncthreads();
 
-  // 0. fused GRM tile
-  if (!(a.skip & 32)) {
+  v4d acc[8][2];
+  {
+    v4i cnt[8][2];
     const int64_t k = a.off[b + 1] - a.off[b];
     const int8_t* pb = a.panel + b * a.pstride;
-    v16i ci[2][2];
-    i8_tile_gemm_ring<false, 8>(pb + i0 * KBLK, pb + j0 * KBLK, (k + KBLK - 1) / KBLK, a.nRp * KBLK,
-                                reinterpret_cast<int8_t*>(lds), ci);
-    const double* sc = a.scal + b * 8;
-    const double invN = sc[0], cN = sc[1], invd = sc[2];
-    const double* ub = a.u + b * a.nRp;
+    if (!(a.skip & 32)) {
+      i8_tt<4>(pb + j0 * KBLK, pb + i0 * KBLK, (k + KBLK - 1) / KBLK, a.nRp * KBLK, reinterpret_cast<int8_t*>(lds),
+               cnt);
+    } else {
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+      for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int col = i8_col(wc, n, l);
-        const int64_t gj = j0 + col;
-        const double uj = ub[gj];
+        for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = v4i{0, 0, 0, 0};
+    }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = i8_row(wr, m, r, l);
-          const int64_t gi = i0 + row;
-          Tl[t_off(row, col)] = (gi < a.nT && gj < a.nT) ? grm_value(ci[m][n][r], ub[gi], uj, invN, cN, invd) : 0.0;
+    for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        const int il = 32 * w + 16 * ib + (l & 15);
+        const bool ireal = i0 + il < a.nT;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cl = 16 * cb + (l >> 4) + 4 * r;
+          const double v = grm_value(cnt[cb][ib][r], uj_sh[cl], ui_sh[il], invN, cN, invd);
+          acc[cb][ib][r] = (ireal && j0 + cl < a.nT) ? v : 0.0;
         }
       }
   }
-  __syncthreads();
-  v4d acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[m][n][r] = Tl[t_off(64 * wr + 16 * m + (l >> 4) + 4 * r, 64 * wc + 16 * n + (l & 15))];
-  __syncthreads();
-  if (J > 0 && !(a.skip & 64)) gemm_nt_f64<false, NoStage, true>(Lb + i0 * nTp, Lb + j0 * nTp, nTp, (int)j0, acc, lds, NoStage{});
-  __syncthreads();
 
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 64 * wr + 16 * m + (l >> 4) + 4 * r, col = 64 * wc + 16 * n + (l & 15);
-        Tl[t_off(row, col)] = acc[m][n][r];
-        acc[m][n][r] = 0.0;
-      }
+  // 1. T^T = K_JI - sum_L L_JL L_IL^T
+  if (J > 0 && !(a.skip & 64)) gemm1_tt<2>(Lb + (int64_t)J * NT * TT, Lb + (int64_t)I * NT * TT, J, lds, acc);
 
-  // out[i][j] = sum_c T[i][c] X[j][c], X = inv(L_JJ) lower triangular (X[j][c] = 0 for c > j)
-  const double* X = a.Dinv + (b * NT + J) * (int64_t)(TILE * TILE);
-  v2d rx[4];
-  auto gload = [&](int s) {
+  // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X^T, so
+  //    the stage for block jb (X^T[c][16jb..16jb+15], 128 rows x 128 B) lands in LDS as the
+  //    [c][j] image the A fragments want, by LDS-DMA (8 rows per wave instruction).
+  const double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;
+  double* Lout = const_cast<double*>(Lb) + ((int64_t)I * NT + J) * TT;
+  double* xs = lds;   // [2][128 c][16 j]
+  auto xissue = [&](int jb) {
+    double* slot = xs + (jb & 1) * TILE * 16;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int q = t + 256 * e, r = q >> 3, c = q & 7;
-      rx[e] = *reinterpret_cast<const v2d*>(X + r * TILE + s * BKD + 2 * c);
+      const int c = 32 * w + 8 * e + (l >> 3);
+      __builtin_amdgcn_global_load_lds(XT + c * TILE + 16 * jb + 2 * (l & 7),
+                                       (lds_ptr_t)(slot + (32 * w + 8 * e) * 16), 16, 0, 0);
     }
   };
-  gload(0);
-  for (int s = 0; s < ((a.skip & 128) ? 0 : TILE / BKD); ++s) {
-    __syncthreads();
+  double wacc[2] = {0.0, 0.0};
+  xissue(0);
+#pragma unroll 1
+  for (int jb = 0; jb < NBLK; ++jb) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (jb + 1 < NBLK) xissue(jb + 1);
+    v4d o[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+    if (!(a.skip & 128)) {
+      const double* xb = xs + (jb & 1) * TILE * 16;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = t + 256 * e, r = q >> 3, c = q & 7;
-      *reinterpret_cast<v2d*>(Xs + r * BKD + 2 * (c ^ ((r >> 1) & 7))) = rx[e];
-    }
-    __syncthreads();
-    if (s + 1 < TILE / BKD) gload(s + 1);
-    if (wc == 1 || s < (TILE / BKD) / 2) {
+      for (int cb = 0; cb < 8; ++cb) {
+        if (cb <= jb) {
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int k = 4 * kk + (l >> 4);
-        double av[4], bv[4];
+          for (int kk = 0; kk < 4; ++kk) {
+            const double av = xb[(16 * cb + 4 * kk + (l >> 4)) * 16 + (l & 15)];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) av[m] = Tl[t_off(64 * wr + 16 * m + (l & 15), s * BKD + k)];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) bv[n] = Xs[st_off(64 * wc + 16 * n + (l & 15), k)];
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) acc[m][n] = mfma64(av[m], bv[n], acc[m][n]);
+            for (int ib = 0; ib < 2; ++ib) o[ib] = mfma64(av, acc[cb][ib][kk], o[ib]);
+          }
+        }
       }
     }
-  }
-
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 64 * wr + 16 * m + (l >> 4) + 4 * r, col = 64 * wc + 16 * n + (l & 15);
-        Lb[(i0 + row) * nTp + j0 + col] = acc[m][n][r];
+        const int jl = 16 * jb + (l >> 4) + 4 * r, il = 32 * w + 16 * ib + (l & 15);
+        Lout[jl * TILE + il] = o[ib][r];
+        wacc[ib] += o[ib][r] * zj_sh[jl];
       }
+  }
+  // w_I[i] += sum_j L_IJ[i][j] z_J[j]: reduce the 4 lane groups that share a column i
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib) {
+    double v = wacc[ib];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if ((l >> 4) == 0) {
+      const int64_t gi = b * nTp + i0 + 32 * w + 16 * ib + l;
+      a.w[gi] = (J == 0) ? v : a.w[gi] + v;
+    }
+  }
+}
+
+hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
+  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.panel, c.pstride, c.off, c.u, c.scal, c.d.nT,
+             c.d.nTp, c.d.nRp, c.d.NT, 0, c.skip};
+  hipLaunchKernelGGL(k_diag_grm, dim3((unsigned)(c.B * c.d.NT)), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag) {
-  CholArgs a{c.L, c.Dinv, c.z, c.yT, c.panel, c.pstride, c.off, c.u, c.scal, c.d.nT, c.d.nTp, c.d.nRp, c.d.NT, J,
-             c.skip};
+  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.panel, c.pstride, c.off, c.u, c.scal, c.d.nT,
+             c.d.nTp, c.d.nRp, c.d.NT, J, c.skip};
   if (diag) {
+    a.NSX = (J >= 2) ? std::min(J - 1, NSX_MAX) : 0;   // written by the off-diagonal launch of J-1
+    if (J >= 1) {
+      hipLaunchKernelGGL(k_diag_prep, dim3((unsigned)(c.B * 4)), dim3(256), 0, s, a);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
   } else {
     const int nI = c.d.NT - J - 1;
     if (nI <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(c.B * nI)), dim3(256), 0, s, a);
+    a.NSX = (J >= 1 && J + 1 < c.d.NT) ? std::min(J, NSX_MAX) : 0;
+    const int64_t n_tiles = c.B * nI;
+    hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX)), dim3(256), 0, s, a, n_tiles);
   }
   return hipGetLastError();
 }

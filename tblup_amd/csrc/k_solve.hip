@@ -55,51 +55,43 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   double* e = dyn + nTp;
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
-  const double* Lb = c.L + b * nTp * nTp;
+  const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
   const double* Db = c.Dinv + b * (int64_t)NT * TILE * TILE;
   const double* sc = c.scal + b * 8;
   const double invN = sc[0], cN = sc[1], invd = sc[2], mu = sc[3];
-  const int cp = t & 63;   // column pair: columns 2cp, 2cp+1 of the tile
-  const int g = t >> 6;    // row group: rows g, g+16, ...
 
-  // alpha = L^{-T} z, block rows from the bottom, using the stored diagonal inverses
+  // alpha = L^{-T} z, block rows from the bottom, using the stored diagonal inverses.
+  // (L_JI^T alpha_J)[c] = sum_r Lt_(J,I)[c][r] alpha_J[r]: row c of the transposed tile,
+  // 8 threads per row (16 contiguous r each), reduced with lane shuffles.
+  const int rc = t >> 3, seg = t & 7;
   for (int I = NT - 1; I >= 0; --I) {
-    v2d s = {0.0, 0.0};
+    double s = 0.0;
     for (int J = I + 1; J < NT; ++J) {
-      const double* base = Lb + (int64_t)J * TILE * nTp + (int64_t)I * TILE + 2 * cp;
-      const double* al = alpha + J * TILE;
-#pragma unroll 4
-      for (int r = g; r < TILE; r += 16) {
-        const v2d x = *reinterpret_cast<const v2d*>(base + (int64_t)r * nTp);
-        s += x * al[r];
+      const double* row = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 16 * seg;
+      const double* al = alpha + J * TILE + 16 * seg;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const v2d x = *reinterpret_cast<const v2d*>(row + 2 * e);
+        s += x[0] * al[2 * e] + x[1] * al[2 * e + 1];
       }
     }
-    part[g][2 * cp] = s[0];
-    part[g][2 * cp + 1] = s[1];
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    if (seg == 0) vsh[rc] = c.z[b * nTp + (int64_t)I * TILE + rc] - s;
     __syncthreads();
-    if (t < TILE) {
-      double acc = 0.0;
+    // alpha_I = X_I^T v: Dinv holds X^T, so again row c dotted with v
+    const double* xrow = Db + (int64_t)I * TILE * TILE + rc * TILE + 16 * seg;
+    double s2 = 0.0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc += part[q][t];
-      vsh[t] = c.z[b * nTp + (int64_t)I * TILE + t] - acc;
+    for (int e = 0; e < 8; ++e) {
+      const v2d x = *reinterpret_cast<const v2d*>(xrow + 2 * e);
+      s2 += x[0] * vsh[16 * seg + 2 * e] + x[1] * vsh[16 * seg + 2 * e + 1];
     }
-    __syncthreads();
-    const double* X = Db + (int64_t)I * TILE * TILE + 2 * cp;
-    v2d s2 = {0.0, 0.0};
-#pragma unroll 8
-    for (int r = g; r < TILE; r += 16) {
-      const v2d x = *reinterpret_cast<const v2d*>(X + r * TILE);
-      s2 += x * vsh[r];
-    }
-    part[g][2 * cp] = s2[0];
-    part[g][2 * cp + 1] = s2[1];
-    __syncthreads();
-    if (t < TILE) {
-      double acc = 0.0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc += part[q][t];
-      alpha[I * TILE + t] = acc;
-    }
+    s2 += __shfl_xor(s2, 1);
+    s2 += __shfl_xor(s2, 2);
+    s2 += __shfl_xor(s2, 4);
+    if (seg == 0) alpha[I * TILE + rc] = s2;
     __syncthreads();
   }
 

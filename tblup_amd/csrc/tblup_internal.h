@@ -22,6 +22,7 @@
 namespace tblup {
 
 constexpr int TILE = 128;      // output tile edge of the GRM and Cholesky kernels
+constexpr int TBLUP_NSLOT = 5; // diagonal-tile slots per individual: 4 SYRK partials + the assembled tile
 constexpr int KBLK = 64;       // SNPs per panel block (int8 MFMA K step)
 constexpr int GATHER_ROWS = 128;
 
@@ -62,9 +63,12 @@ hipError_t launch_grm(const int8_t* panel, int64_t panel_stride, const int64_t* 
 struct CholLaunch {
   EvalDims d;
   int64_t B;
-  double* L;             // [B][nTp][nTp] Cholesky factor (TT lower tiles)
+  double* L;             // Lt tiles [B][NT][NT][128*128] (tile (I,J) holds L_IJ^T)
   double* Dinv;          // [B][NT][128][128]
   double* z;             // [B][nTp]
+  double* w;             // [B][nTp] forward-substitution partial sums
+  double* S;             // [B][TBLUP_NSLOT][36*256] SYRK partials + assembled diagonal tile
+  double* Kd;            // [B][NT][36*256] GRM diagonal tiles
   const double* yT;      // split phenotypes [nTp]
   const double* yV;      // [nV]
   const int8_t* panel;   // gathered genotypes
@@ -76,6 +80,8 @@ struct CholLaunch {
 };
 // one tile column J of the fused GRM + Cholesky: diag=true -> k_chol_diag, else k_chol_offdiag
 hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag);
+// all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
+hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s);
 
 // XCD-aware bijective remap of a 1-D block id (blocks b and b+8 share an XCD
