@@ -48,7 +48,7 @@ struct DevBuf {
 struct Split {
   int64_t nT = 0, nV = 0, nTp = 0, nVp = 0, nRp = 0;
   double meanyT = 0.0;
-  DevBuf geno, colsumT, yT, yV;
+  DevBuf geno, colsumT, xty, yT, yV;
 };
 
 enum { KC_STATS = 0, KC_GATHER, KC_GRM, KC_DIAG, KC_OFFDIAG, KC_SOLVE };
@@ -83,6 +83,7 @@ struct tblup_ctx {
   hipStream_t aux[TBLUP_MAX_GROUPS - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[TBLUP_MAX_GROUPS - 1] = {};
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
+  int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
 };
 
 namespace {
@@ -164,23 +165,30 @@ struct Carve {
   }
 };
 
-size_t chunk_bytes(const EvalDims& d, int64_t B, int64_t max_kblk, int64_t sum_k, bool with_ebv) {
+size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k, bool with_ebv) {
   size_t s = 0;
   auto add = [&](size_t x) { s = (size_t)round_up((int64_t)(s + x), 256); };
-  add((size_t)B * max_kblk * d.nRp * KBLK);                     // panel
-  add((size_t)B * d.nRp * 8);                                   // u
-  add((size_t)B * 64);                                          // scal
-  add((size_t)B * d.nTp * d.nTp * 8);                           // L
-  add((size_t)B * d.NT * TILE * TILE * 8);                      // Dinv
-  add((size_t)B * d.nTp * 8);                                   // z
-  add((size_t)B * d.nTp * 8);                                   // w
-  add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                            // SYRK partials
-  add((size_t)B * d.NT * 36 * 256 * 8);                         // diagonal GRM tiles
+  add(sd.form == FORM_DUAL ? (size_t)B * sd.cblk * sd.prow * KBLK : 0);   // panel (dual only)
+  add((size_t)B * sd.prow * 8);                                 // u
+  add((size_t)B * SCAL * 8);                                    // scal
+  add((size_t)B * sd.ns * sd.ns * 8);                           // L (Lt tiles)
+  add((size_t)B * sd.NT * TILE * TILE * 8);                     // Dinv
+  add((size_t)B * sd.ns * 8);                                   // z
+  add((size_t)B * sd.ns * 8);                                   // w
+  add((size_t)B * sd.ns * 8);                                   // rhs
+  add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // SYRK partials + assembled tile
+  add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nV * 8 : 0);                     // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
   return s + 4096;
 }
+
+// Form of the per-individual system for a batch.  The SNP-space (primal) form is what
+// sklearn's Ridge solves when k <= n_T (_ridge.py _solve_cholesky: X^T X + alpha I); it is
+// used when every individual takes the snp branch and it gives fewer 128-row tiles than the
+// kernel form.  pref: 0 auto, 1 force dual, 2 force primal (snp batches only).
+SysDims choose_sys(const tblup_ctx* c, const EvalDims& d, const int64_t* h_off, int64_t B, int branch, int pref);
 
 EvalDims dims_of(const tblup_ctx* c, const Split& sp) {
   EvalDims d;
@@ -196,42 +204,72 @@ EvalDims dims_of(const tblup_ctx* c, const Split& sp) {
   return d;
 }
 
+SysDims choose_sys(const tblup_ctx* c, const EvalDims& d, const int64_t* h_off, int64_t B, int branch, int pref) {
+  int64_t max_k = 1;
+  bool all_snp = true;
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t k = h_off[b + 1] - h_off[b];
+    max_k = std::max(max_k, k);
+    const int mode = branch ? branch : (k > c->n ? 1 : 2);   // evaluator.py:257
+    if (mode != 2) all_snp = false;
+  }
+  const int64_t kp = round_up(max_k, TILE);
+  const bool primal = all_snp && pref != 1 && (pref == 2 || kp < d.nTp);
+  SysDims sd;
+  if (primal) {
+    sd.form = FORM_PRIMAL;
+    sd.ns = kp;
+    sd.prow = kp;
+    sd.cblk = d.nRp / KBLK;
+  } else {
+    sd.form = FORM_DUAL;
+    sd.ns = d.nTp;
+    sd.prow = d.nRp;
+    sd.cblk = round_up(max_k, KBLK) / KBLK;
+  }
+  sd.NT = (int)(sd.ns / TILE);
+  return sd;
+}
+
 // Enqueue the full pipeline for one chunk whose idx/off already sit in device memory.
-int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, const int64_t* d_idx,
-              const int64_t* d_off, const int64_t* h_off, int64_t B, double h2,
+int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& sd, hipStream_t s,
+              const int64_t* d_idx, const int64_t* d_off, const int64_t* h_off, int64_t B, double h2,
               int branch, Carve& cv, double* d_fit, double* d_ebv, int stop_stage, double** K_out,
               double** z_out) {
-  int64_t max_kblk = 0;
   double grm_flops = 0.0, gather_bytes = 0.0, stats_bytes = 0.0;
   const double tri = (double)d.nT * (d.nT + 1) / 2.0 + (double)d.nV * d.nT;
   for (int64_t b = 0; b < B; ++b) {
     const int64_t k = h_off[b + 1] - h_off[b];
-    max_kblk = std::max(max_kblk, (k + KBLK - 1) / KBLK);
     grm_flops += 2.0 * (double)k * tri;
     gather_bytes += 2.0 * (double)k * (double)(d.nT + d.nV);
     stats_bytes += 16.0 * (double)k;
   }
-  const int64_t pstride = max_kblk * d.nRp * KBLK;
+  const int64_t pstride = (sd.form == FORM_DUAL) ? sd.cblk * sd.prow * KBLK : 0;
   int8_t* panel = cv.take<int8_t>((size_t)B * pstride);
-  double* u = cv.take<double>((size_t)B * d.nRp);
-  double* scal = cv.take<double>((size_t)B * 8);
-  double* L = cv.take<double>((size_t)B * d.nTp * d.nTp);
-  double* Dinv = cv.take<double>((size_t)B * d.NT * TILE * TILE);
-  double* z = cv.take<double>((size_t)B * d.nTp);
-  double* wv = cv.take<double>((size_t)B * d.nTp);
+  double* u = cv.take<double>((size_t)B * sd.prow);
+  double* scal = cv.take<double>((size_t)B * SCAL);
+  double* L = cv.take<double>((size_t)B * sd.ns * sd.ns);
+  double* Dinv = cv.take<double>((size_t)B * sd.NT * TILE * TILE);
+  double* z = cv.take<double>((size_t)B * sd.ns);
+  double* wv = cv.take<double>((size_t)B * sd.ns);
+  double* rhs = cv.take<double>((size_t)B * sd.ns);
   double* Sp = cv.take<double>((size_t)B * TBLUP_NSLOT * 36 * 256);
-  double* Kdg = cv.take<double>((size_t)B * d.NT * 36 * 256);
+  double* Kdg = cv.take<double>((size_t)B * sd.NT * 36 * 256);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
   rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
-    return launch_indiv_stats(d_idx, d_off, B, csT, csA, d, branch, sp.meanyT, h2, scal, s);
+    return launch_indiv_stats(d_idx, d_off, B, csT, csA, (const double*)sp.xty.p, d, sd, branch, sp.meanyT, h2,
+                              scal, u, rhs, s);
   });
   if (rc) return rc;
-  rc = timed(c, s, KC_GATHER, 0.0, gather_bytes, [&] {
-    return launch_gather((const int8_t*)sp.geno.p, d_idx, d_off, pstride, B, csT, csA, scal, d, panel, u, s);
-  });
-  if (rc) return rc;
+  if (sd.form == FORM_DUAL) {
+    // primal rows are read in place from the split matrix: no gather
+    rc = timed(c, s, KC_GATHER, 0.0, gather_bytes, [&] {
+      return launch_gather((const int8_t*)sp.geno.p, d_idx, d_off, pstride, B, csT, csA, scal, d, panel, u, s);
+    });
+    if (rc) return rc;
+  }
   if (z_out) *z_out = z;
   if (stop_stage == 1) {
     // parity readback only: the full K_{R,T} block of the unified form (k_grm); the
@@ -243,10 +281,12 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, c
                  [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
   }
   if (K_out) *K_out = L;
-  CholLaunch cl{d, B, L, Dinv, z, wv, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p, panel, pstride, d_off, u, scal,
+  CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p, panel, pstride, d_off,
+                (const int8_t*)sp.geno.p, d_idx, d.nRp, u, scal,
                 c->dbg_skip};
   const double T3 = (double)TILE * TILE * TILE;
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
+  const double cbar = (sd.form == FORM_PRIMAL) ? (double)d.nT : kbar;   // contraction length
   // The batch is split into groups on separate streams so that one group's latency-bound
   // diagonal-tile work overlaps another group's MFMA-bound off-diagonal tiles.
   const int G = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_groups, B / 32));
@@ -256,31 +296,32 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, c
     const int64_t b0 = B * g / G, b1 = B * (g + 1) / G;
     CholLaunch x = cl;
     x.B = b1 - b0;
-    x.L = cl.L + b0 * (int64_t)d.NT * d.NT * TILE * TILE;
-    x.Dinv = cl.Dinv + b0 * (int64_t)d.NT * TILE * TILE;
-    x.z = cl.z + b0 * d.nTp;
-    x.w = cl.w + b0 * d.nTp;
+    x.L = cl.L + b0 * sd.ns * sd.ns;
+    x.Dinv = cl.Dinv + b0 * (int64_t)sd.NT * TILE * TILE;
+    x.z = cl.z + b0 * sd.ns;
+    x.w = cl.w + b0 * sd.ns;
+    x.rhs = cl.rhs + b0 * sd.ns;
     x.S = cl.S + b0 * TBLUP_NSLOT * 36 * 256;
-    x.Kd = cl.Kd + b0 * (int64_t)d.NT * 36 * 256;
+    x.Kd = cl.Kd + b0 * (int64_t)sd.NT * 36 * 256;
     x.panel = cl.panel + b0 * pstride;
     x.off = cl.off + b0;
-    x.u = cl.u + b0 * d.nRp;
-    x.scal = cl.scal + b0 * 8;
+    x.u = cl.u + b0 * sd.prow;
+    x.scal = cl.scal + b0 * SCAL;
     gl[g] = x;
     gs[g] = (g == 0) ? s : c->aux[g - 1];
   }
   {
-    const double fg = (double)B * d.NT * 128.0 * 129.0 * kbar;   // int ops of the diagonal GRM tiles
-    rc = timed(c, s, KC_GRM, fg, (double)B * d.NT * 36 * 256 * 8.0, [&] { return launch_diag_grm(cl, s); });
+    const double fg = (double)B * sd.NT * 128.0 * 129.0 * cbar;   // int ops of the diagonal GRM tiles
+    rc = timed(c, s, KC_GRM, fg, (double)B * sd.NT * 36 * 256 * 8.0, [&] { return launch_diag_grm(cl, s); });
     if (rc) return rc;
   }
   if (G > 1) {
     HIPCHK(hipEventRecord(c->ev_fork, s));
     for (int g = 1; g < G; ++g) HIPCHK(hipStreamWaitEvent(gs[g], c->ev_fork, 0));
   }
-  for (int J = 0; J < d.NT; ++J) {
+  for (int J = 0; J < sd.NT; ++J) {
     const double jt = (double)J;
-    const int nI = d.NT - J - 1;
+    const int nI = sd.NT - J - 1;
     for (int g = 0; g < G; ++g) {
       const double Bg = (double)gl[g].B;
       // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
@@ -306,8 +347,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, hipStream_t s, c
     }
   }
   if (stop_stage == 2) return 0;
-  const double fs = (double)B * (2.0 * (double)d.nTp * d.nTp / 2.0 + 2.0 * kbar * (double)(d.nT + d.nV) + 10.0 * d.nV);
-  const double bs = (double)B * (((double)d.nTp * d.nTp / 2.0 + (double)d.NT * TILE * TILE) * 8.0 +
+  const double fs = (double)B * (2.0 * (double)sd.ns * sd.ns / 2.0 + 2.0 * kbar * (double)(d.nT + d.nV) + 10.0 * d.nV);
+  const double bs = (double)B * (((double)sd.ns * sd.ns / 2.0 + (double)sd.NT * TILE * TILE) * 8.0 +
                                  kbar * (double)(d.nT + d.nV));
   rc = timed(c, s, KC_SOLVE, fs, bs, [&] { return launch_solve(cl, d_fit, d_ebv, s); });
   return rc;
@@ -362,6 +403,8 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
   const char* dbg = getenv("TBLUP_DBG_SKIP");
   c->dbg_skip = dbg ? atoi(dbg) : 0;
+  const char* fp = getenv("TBLUP_FORM");
+  c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   const char* ns = getenv("TBLUP_STREAMS");
   c->n_groups = std::max(1, std::min(TBLUP_MAX_GROUPS, ns ? atoi(ns) : 1));
   for (int g = 0; g < TBLUP_MAX_GROUPS - 1; ++g) {
@@ -398,6 +441,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   for (auto& kv : c->splits) {
     kv.second->geno.release();
     kv.second->colsumT.release();
+    kv.second->xty.release();
     kv.second->yT.release();
     kv.second->yV.release();
   }
@@ -444,8 +488,9 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   }
   sp->meanyT = (double)(acc / (long double)nT);
   for (int64_t i = 0; i < nV; ++i) yV[i] = c->pheno[valid[i]];
-  if (int rc = dev_alloc(c, sp->geno, (size_t)c->P * sp->nRp)) return rc;
+  if (int rc = dev_alloc(c, sp->geno, (size_t)(c->P + 1) * sp->nRp)) return rc;
   if (int rc = dev_alloc(c, sp->colsumT, (size_t)c->P * 4)) return rc;
+  if (int rc = dev_alloc(c, sp->xty, (size_t)c->P * 8)) return rc;
   if (int rc = dev_alloc(c, sp->yT, (size_t)sp->nTp * 8)) return rc;
   if (int rc = dev_alloc(c, sp->yV, (size_t)nV * 8)) return rc;
   DevBuf rm;
@@ -454,13 +499,15 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   HIPCHK(hipMemcpyAsync(sp->yT.p, yT.data(), yT.size() * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(sp->yV.p, yV.data(), yV.size() * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(launch_build_split((const int8_t*)c->geno_sm.p, c->n, c->P, (const int32_t*)rm.p, sp->nRp, nT,
-                            (int8_t*)sp->geno.p, (int32_t*)sp->colsumT.p, c->stream));
+                            (const double*)sp->yT.p, sp->meanyT, (int8_t*)sp->geno.p, (int32_t*)sp->colsumT.p,
+                            (double*)sp->xty.p, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   dev_free(c, rm);
   auto it = c->splits.find(split_id);
   if (it != c->splits.end()) {
     dev_free(c, it->second->geno);
     dev_free(c, it->second->colsumT);
+    dev_free(c, it->second->xty);
     dev_free(c, it->second->yT);
     dev_free(c, it->second->yV);
   }
@@ -476,6 +523,7 @@ int tblup_drop_split(tblup_ctx* c, int split_id) {
   HIPCHK(hipStreamSynchronize(c->stream));
   dev_free(c, it->second->geno);
   dev_free(c, it->second->colsumT);
+  dev_free(c, it->second->xty);
   dev_free(c, it->second->yT);
   dev_free(c, it->second->yV);
   c->splits.erase(it);
@@ -508,21 +556,20 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
   HIPCHK(hipSetDevice(c->device));
   const EvalDims d = dims_of(c, *sp);
   const bool want_ebv = ebv != nullptr;
+  const SysDims sd = choose_sys(c, d, offsets, batch, branch, c->form_pref);
   int64_t b0 = 0;
   while (b0 < batch) {
     // grow the chunk while it fits the workspace budget
-    int64_t b1 = b0, max_kblk = 0, sum_k = 0;
+    int64_t b1 = b0, sum_k = 0;
     while (b1 < batch) {
       const int64_t k = offsets[b1 + 1] - offsets[b1];
-      const int64_t mkb = std::max(max_kblk, (k + KBLK - 1) / KBLK);
-      if (b1 > b0 && chunk_bytes(d, b1 + 1 - b0, mkb, sum_k + k, want_ebv) > c->budget) break;
+      if (b1 > b0 && chunk_bytes(d, sd, b1 + 1 - b0, sum_k + k, want_ebv) > c->budget) break;
       if (b1 - b0 >= 65535) break;
-      max_kblk = mkb;
       sum_k += k;
       ++b1;
     }
     const int64_t B = b1 - b0;
-    const size_t need = chunk_bytes(d, B, max_kblk, sum_k, want_ebv);
+    const size_t need = chunk_bytes(d, sd, B, sum_k, want_ebv);
     HIPCHK(hipStreamSynchronize(c->stream));
     if (int rc = dev_alloc(c, c->ws, need)) return rc;
     Carve cv{(char*)c->ws.p};
@@ -534,7 +581,7 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
     for (int64_t b = 0; b <= B; ++b) hoff[b] = offsets[b0 + b] - offsets[b0];
     HIPCHK(hipMemcpyAsync(d_idx, idx + offsets[b0], (size_t)sum_k * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(d_off, hoff.data(), (size_t)(B + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    if (int rc = run_chunk(c, *sp, d, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv, d_fit, d_ebv, 0,
+    if (int rc = run_chunk(c, *sp, d, sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv, d_fit, d_ebv, 0,
                            nullptr, nullptr))
       return rc;
     HIPCHK(hipMemcpyAsync(fitness + b0, d_fit, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
@@ -561,9 +608,8 @@ int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, co
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const EvalDims d = dims_of(c, *sp);
-  int64_t max_kblk = 0;
-  for (int64_t b = 0; b < batch; ++b) max_kblk = std::max(max_kblk, (h_offsets[b + 1] - h_offsets[b] + KBLK - 1) / KBLK);
-  const size_t need = chunk_bytes(d, batch, max_kblk, 0, false);
+  const SysDims sd = choose_sys(c, d, h_offsets, batch, branch, c->form_pref);
+  const size_t need = chunk_bytes(d, sd, batch, 0, false);
   if (need > c->ws.bytes) {
     // the workspace may still be in use by earlier work on either stream
     HIPCHK(hipStreamSynchronize(s));
@@ -571,8 +617,8 @@ int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, co
     if (int rc = dev_alloc(c, c->ws, need)) return rc;
   }
   Carve cv{(char*)c->ws.p};
-  return run_chunk(c, *sp, d, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness, d_ebv, 0, nullptr,
-                   nullptr);
+  return run_chunk(c, *sp, d, sd, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness, d_ebv, 0,
+                   nullptr, nullptr);
 }
 
 int tblup_set_profiling(tblup_ctx* c, int enable) {
@@ -620,9 +666,9 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
   if (!sp) return fail(TBLUP_ERR_ARG, "unknown split id");
   HIPCHK(hipSetDevice(c->device));
   const EvalDims d = dims_of(c, *sp);
-  const int64_t nkb = (k + KBLK - 1) / KBLK;
+  const SysDims sd = choose_sys(c, d, offs, 1, branch, 1);   // readback is of the kernel (dual) form
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (int rc = dev_alloc(c, c->ws, chunk_bytes(d, 1, nkb, k, false) + (size_t)d.nRp * d.nTp * 8 + 4096)) return rc;
+  if (int rc = dev_alloc(c, c->ws, chunk_bytes(d, sd, 1, k, false) + (size_t)d.nRp * d.nTp * 8 + 4096)) return rc;
   Carve cv{(char*)c->ws.p};
   int64_t* d_idx = cv.take<int64_t>((size_t)k);
   int64_t* d_off = cv.take<int64_t>(2);
@@ -630,7 +676,7 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
   HIPCHK(hipMemcpyAsync(d_idx, idx, (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d_off, offs, 16, hipMemcpyHostToDevice, c->stream));
   double *K = nullptr, *z = nullptr;
-  if (int rc = run_chunk(c, *sp, d, c->stream, d_idx, d_off, offs, 1, h2, branch, cv, d_fit, nullptr, stage,
+  if (int rc = run_chunk(c, *sp, d, sd, c->stream, d_idx, d_off, offs, 1, h2, branch, cv, d_fit, nullptr, stage,
                          &K, &z))
     return rc;
   HIPCHK(hipStreamSynchronize(c->stream));

@@ -72,14 +72,21 @@ __device__ __forceinline__ void i8_tile_gemm(const int8_t* __restrict__ a_base, 
   }
 }
 
-// Same product with an LDS-DMA ring (global_load_lds_dwordx4): D stage slots, D-1
-// stages in flight while one is consumed, one barrier per stage.  The LDS image is
-// lane-linear per wave instruction; the chunk swizzle of lds_off_i8 is applied to the
-// SOURCE address (an involution), so fragment reads use lds_off_i8 unchanged.
-// lds must hold D * (SAME ? 8 : 16) KiB.
-template <bool SAME, int D>
-__device__ __forceinline__ void i8_tile_gemm_ring(const int8_t* __restrict__ a_base, const int8_t* __restrict__ b_base,
-                                                  int64_t nblk, int64_t kb_stride, int8_t* lds, v16i (&acc)[2][2]) {
+// Same product (A = B, the symmetric diagonal tile) with an LDS-DMA ring
+// (global_load_lds_dwordx4): D stage slots, D-1 stages in flight while one is consumed,
+// one barrier per stage.  The LDS image is lane-linear per wave instruction; the chunk
+// swizzle of lds_off_i8 is applied to the SOURCE address (an involution), so fragment
+// reads use lds_off_i8 unchanged.
+// Sources are per lane: this lane's 16-B chunks of the two rows it loads (see
+// i8_ring_row), already swizzled; stage kb adds kb * kstep.  That covers both the
+// materialised panel (kstep = panel block stride) and rows read in place from the
+// SNP-major split matrix (kstep = 64).  lds must hold D * 8 KiB.
+__device__ __forceinline__ int i8_ring_row(int e) { return (2 * (threadIdx.x >> 6) + e) * 16 + ((threadIdx.x & 63) >> 2); }
+__device__ __forceinline__ int i8_ring_chunk(int row) { return 16 * ((threadIdx.x & 3) ^ ((row >> 2) & 3)); }
+
+template <int D>
+__device__ __forceinline__ void i8_tile_syrk_ring(const int8_t* const (&src)[2], int64_t nblk, int64_t kstep,
+                                                  int8_t* lds, v16i (&acc)[2][2]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -88,34 +95,24 @@ __device__ __forceinline__ void i8_tile_gemm_ring(const int8_t* __restrict__ a_b
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
   if (nblk <= 0) return;
-  constexpr int TB = TILE * KBLK;             // 8 KiB per operand tile
-  constexpr int SB = (SAME ? 1 : 2) * TB;     // bytes per stage
-  constexpr int NI = SAME ? 2 : 4;            // glds instructions per thread per stage
+  constexpr int TB = TILE * KBLK;             // 8 KiB per stage
   auto issue = [&](int64_t kb) {
-    int8_t* slot = lds + (int)(kb % D) * SB;
+    int8_t* slot = lds + (int)(kb % D) * TB;
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int cb = w * 2 + e;               // 1 KiB chunk block of the 8 KiB tile
-      const int q = cb * 64 + l, row = q >> 2, pos = q & 3;
-      const int src = row * 64 + 16 * (pos ^ ((row >> 2) & 3));
-      __builtin_amdgcn_global_load_lds(a_base + kb * kb_stride + src,
-                                       (__attribute__((address_space(3))) void*)(slot + cb * 1024), 16, 0, 0);
-      if (!SAME)
-        __builtin_amdgcn_global_load_lds(b_base + kb * kb_stride + src,
-                                         (__attribute__((address_space(3))) void*)(slot + TB + cb * 1024), 16, 0, 0);
-    }
+    for (int e = 0; e < 2; ++e)
+      __builtin_amdgcn_global_load_lds(src[e] + kb * kstep, (__attribute__((address_space(3))) void*)(slot + (2 * w + e) * 1024),
+                                       16, 0, 0);
   };
   for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
   for (int64_t kb = 0; kb < nblk; ++kb) {
     if (kb + D - 2 < nblk) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * NI) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     if (kb + D - 1 < nblk) issue(kb + D - 1);   // into the slot consumed at kb-1
-    const int8_t* As = lds + (int)(kb % D) * SB;
-    const int8_t* Bs = SAME ? As : As + TB;
+    const int8_t* As = lds + (int)(kb % D) * TB;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = (l >> 5) + 2 * kk;
@@ -123,7 +120,7 @@ __device__ __forceinline__ void i8_tile_gemm_ring(const int8_t* __restrict__ a_b
 #pragma unroll
       for (int m = 0; m < 2; ++m) a[m] = *reinterpret_cast<const v4i*>(As + lds_off_i8(64 * wr + 32 * m + (l & 31), chunk));
 #pragma unroll
-      for (int n = 0; n < 2; ++n) bb[n] = *reinterpret_cast<const v4i*>(Bs + lds_off_i8(64 * wc + 32 * n + (l & 31), chunk));
+      for (int n = 0; n < 2; ++n) bb[n] = *reinterpret_cast<const v4i*>(As + lds_off_i8(64 * wc + 32 * n + (l & 31), chunk));
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -138,9 +135,12 @@ __device__ __forceinline__ void i8_tile_gemm_ring(const int8_t* __restrict__ a_b
 __device__ __forceinline__ int i8_row(int wr, int m, int r, int l) { return 64 * wr + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
 __device__ __forceinline__ int i8_col(int wc, int n, int l) { return 64 * wc + 32 * n + (l & 31); }
 
-// K value of the unified form from the exact integer count c = (A A^T)_ij.
-__device__ __forceinline__ double grm_value(int32_t c, double ui, double uj, double invN, double cN, double invd) {
-  return ((double)c - (ui + uj) * invN + cN) * invd;
+// System value from the exact integer count c = (A A^T)_ij:
+//   dual   (c - (u_i + u_j)/N + q/N^2) / d       (sm = 0)
+//   primal (c - s_a s_b / n_T) / d                (sa = cN = 0, sm = 1/n_T)
+__device__ __forceinline__ double grm_value(int32_t c, double ui, double uj, double sa, double cN, double invd,
+                                            double sm) {
+  return ((double)c - (ui + uj) * sa - ui * uj * sm + cN) * invd;
 }
 
 }  // namespace tblup

@@ -68,9 +68,12 @@ __device__ __forceinline__ void glds_lt_stage(const double* __restrict__ src, do
 __device__ __forceinline__ int i8off_a(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
 __device__ __forceinline__ int i8off_b(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 2)); }
 
+// Sources are per lane (rows 16(2w+e) + (l>>2), chunk l&3, swizzle applied), stage kb at + kb*kstep.
+__device__ __forceinline__ int i8_tt_row(int e) { return (2 * (threadIdx.x >> 6) + e) * 16 + ((threadIdx.x & 63) >> 2); }
+
 template <int D>
-__device__ __forceinline__ void i8_tt(const int8_t* __restrict__ pa, const int8_t* __restrict__ pb, int64_t nblk,
-                                      int64_t kb_stride, int8_t* lds, v4i (&cnt)[8][2]) {
+__device__ __forceinline__ void i8_tt(const int8_t* const (&sa)[2], const int8_t* const (&sb)[2], int64_t nblk,
+                                      int64_t kstep, int8_t* lds, v4i (&cnt)[8][2]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb)
@@ -82,11 +85,9 @@ __device__ __forceinline__ void i8_tt(const int8_t* __restrict__ pa, const int8_
     int8_t* slot = lds + (int)(kb % D) * 2 * TB;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int cblk = 2 * w + e, q = cblk * 64 + l, row = q >> 2, pos = q & 3;
-      __builtin_amdgcn_global_load_lds(pa + kb * kb_stride + row * 64 + 16 * (pos ^ ((row >> 2) & 3)),
-                                       (lds_ptr_t)(slot + cblk * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(pb + kb * kb_stride + row * 64 + 16 * (pos ^ ((row >> 2) & 2)),
-                                       (lds_ptr_t)(slot + TB + cblk * 1024), 16, 0, 0);
+      const int cblk = 2 * w + e;
+      __builtin_amdgcn_global_load_lds(sa[e] + kb * kstep, (lds_ptr_t)(slot + cblk * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(sb[e] + kb * kstep, (lds_ptr_t)(slot + TB + cblk * 1024), 16, 0, 0);
     }
   };
   for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
@@ -290,21 +291,44 @@ __device__ __forceinline__ void factor16(double* D, double* X, double* piv_sh, i
 struct CholArgs {
   double* L;                // Lt tiles [B][NT][NT][128*128]
   double* Dinv;             // [B][NT][128][128]
-  double* z;                // [B][nTp]
-  double* w;                // [B][nTp] forward-substitution partial sums
+  double* z;                // [B][ns]
+  double* w;                // [B][ns] forward-substitution partial sums
   double* S;                // [B][NSLOT][36*256] SYRK partials of a diagonal tile
   double* Kd;               // [B][NT][36*256] GRM diagonal tiles (k_diag_grm)
   int NSX;                  // prep: L<J-1 partials to sum; offdiag: extra SYRK workgroups per individual
-  const double* yT;         // [nTp]
+  const double* yT;         // [nTp] dual right-hand side (y_T - mu, on the fly)
+  const double* rhs;        // [B][ns] primal right-hand side
   const int8_t* panel;      // [B] x pstride
   int64_t pstride;
-  const int64_t* off;       // [B+1]
-  const double* u;          // [B][nRp]
-  const double* scal;       // [B][8]
-  int64_t nT, nTp, nRp;
+  const double* u;          // [B][prow]
+  const double* scal;       // [B][SCAL]
+  int64_t ns, prow;         // padded system size, panel rows per contraction block
+  int form;
+  // primal form: rows read in place from the split's SNP-major matrix (row P is zero)
+  const int8_t* gs;
+  const int64_t* idx;
+  const int64_t* off;
+  int64_t gs_row, P;
   int NT, J;
   int skip;                 // diagnostic ablation mask (TBLUP_DBG_SKIP); 0 in production
 };
+
+// Address of system row r's contraction block 0 for individual b: the gathered panel
+// (dual) or the selected SNP row of the split matrix itself (primal; padding rows -> the
+// zero row P).  Stage kb is at + kb * row_kstep(a).
+__device__ __forceinline__ const int8_t* row_base(const CholArgs& a, int64_t b, int64_t r) {
+  if (a.form == FORM_PRIMAL) {
+    const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
+    int64_t p = a.P;
+    if (r < k) {
+      p = a.idx[o0 + r];
+      p = p < 0 ? 0 : (p >= a.P ? a.P - 1 : p);
+    }
+    return a.gs + p * a.gs_row;
+  }
+  return a.panel + b * a.pstride + r * KBLK;
+}
+__device__ __forceinline__ int64_t row_kstep(const CholArgs& a) { return a.form == FORM_PRIMAL ? KBLK : a.prow * KBLK; }
 
 // ---------------------------------------------------------------------------
 // Diagonal tile T_J = K_JJ - sum_{L<J} L_JL L_JL^T is assembled from pieces that are
@@ -341,15 +365,20 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
   const int64_t b = blockIdx.x / NT;
   const int J = (int)(blockIdx.x % NT);
   const int64_t j0 = (int64_t)J * TILE;
-  const int64_t k = a.off[b + 1] - a.off[b];
-  const int8_t* pj = a.panel + b * a.pstride + j0 * KBLK;
-  const double* sc = a.scal + b * 8;
-  const double invN = sc[0], cN = sc[1], invd = sc[2], lam = sc[4];
-  const double* ub = a.u + b * a.nRp;
+  const double* sc = a.scal + b * SCAL;
+  const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
+  const int64_t nrow = (int64_t)sc[SC_NROW], nblk = (int64_t)sc[SC_CBLK];
+  const double* ub = a.u + b * a.prow;
   double* Kd = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
   v16i ci[2][2];
   if (!(a.skip & 1)) {
-    i8_tile_gemm_ring<true, 8>(pj, pj, (k + KBLK - 1) / KBLK, a.nRp * KBLK, lds, ci);
+    const int8_t* src[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = i8_ring_row(e);
+      src[e] = row_base(a, b, j0 + row) + i8_ring_chunk(row);
+    }
+    i8_tile_syrk_ring<8>(src, nblk, row_kstep(a), lds, ci);
   } else {
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -370,8 +399,8 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
         const int row = i8_row(wr, m, r, l);
         if ((row >> 4) >= (col >> 4)) {
           const int64_t gi = j0 + row;
-          const double kv = grm_value(ci[m][n][r], ub[gi], uj, invN, cN, invd);
-          const double v = (gi < a.nT && gj < a.nT) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
+          const double kv = grm_value(ci[m][n][r], ub[gi], uj, sa, cN, invd, sm);
+          const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
           Kd[pk(row >> 4, col >> 4) + bo(row & 15, col & 15)] = v;
         }
       }
@@ -450,11 +479,12 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   __shared__ double rsh[TILE];
   __shared__ double piv_sh[NB];
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int64_t b = blockIdx.x, nTp = a.nTp;
+  const int64_t b = blockIdx.x, ns = a.ns;
   const int J = a.J, NT = a.NT;
   const int64_t j0 = (int64_t)J * TILE;
-  const double* sc = a.scal + b * 8;
-  const double mu = sc[3];
+  const double* sc = a.scal + b * SCAL;
+  const double mu = sc[SC_MU];
+  const int64_t nrow = (int64_t)sc[SC_NROW];
   double* Tp = lds;
   double* Xd = lds + NPACK * BLKD;   // X_pp, p = 0..7
   double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;   // X^T, row-major: XT[c][i] = X[i][c]
@@ -472,8 +502,9 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   }
   if (t < TILE) {
     const int64_t gi = j0 + t;
-    const double wv = (J > 0) ? a.w[b * nTp + gi] : 0.0;
-    rsh[t] = (gi < a.nT) ? (a.yT[gi] - mu - wv) : 0.0;
+    const double wv = (J > 0) ? a.w[b * ns + gi] : 0.0;
+    const double rv = (a.form == FORM_PRIMAL) ? a.rhs[b * ns + gi] : a.yT[gi] - mu;
+    rsh[t] = (gi < nrow) ? (rv - wv) : 0.0;
   }
   __syncthreads();
 
@@ -549,7 +580,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   if (t < TILE) {
     double acc_z = 0.0;
     for (int c = 0; c <= t; ++c) acc_z += XT[c * TILE + t] * rsh[c];
-    a.z[b * nTp + j0 + t] = acc_z;
+    a.z[b * ns + j0 + t] = acc_z;
   }
 }
 
@@ -579,25 +610,32 @@ __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int64_t n_t
   const int64_t logical = xcd_remap(blockIdx.x - n_extra, n_tiles);
   const int64_t b = logical / nI;
   const int I = J + 1 + (int)(logical % nI);
-  const int64_t nTp = a.nTp;
+  const int64_t ns = a.ns;
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
   const double* Lb = a.L + b * (int64_t)NT * NT * TT;
-  const double* sc = a.scal + b * 8;
-  const double invN = sc[0], cN = sc[1], invd = sc[2];
+  const double* sc = a.scal + b * SCAL;
+  const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], sm = sc[SC_SM];
+  const int64_t nrow = (int64_t)sc[SC_NROW];
   if (t < TILE) {
-    uj_sh[t] = a.u[b * a.nRp + j0 + t];
-    ui_sh[t] = a.u[b * a.nRp + i0 + t];
-    zj_sh[t] = a.z[b * nTp + j0 + t];
+    uj_sh[t] = a.u[b * a.prow + j0 + t];
+    ui_sh[t] = a.u[b * a.prow + i0 + t];
+    zj_sh[t] = a.z[b * ns + j0 + t];
   }
   __syncthreads();
 
   v4d acc[8][2];
   {
     v4i cnt[8][2];
-    const int64_t k = a.off[b + 1] - a.off[b];
-    const int8_t* pb = a.panel + b * a.pstride;
+    const int64_t nblk = (int64_t)sc[SC_CBLK];
     if (!(a.skip & 32)) {
-      i8_tt<4>(pb + j0 * KBLK, pb + i0 * KBLK, (k + KBLK - 1) / KBLK, a.nRp * KBLK, reinterpret_cast<int8_t*>(lds),
+      const int8_t *sa[2], *sb[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int row = i8_tt_row(e), pos = l & 3;
+        sa[e] = row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3));
+        sb[e] = row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2));
+      }
+      i8_tt<4>(sa, sb, nblk, row_kstep(a), reinterpret_cast<int8_t*>(lds),
                cnt);
     } else {
 #pragma unroll
@@ -610,12 +648,12 @@ __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int64_t n_t
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib) {
         const int il = 32 * w + 16 * ib + (l & 15);
-        const bool ireal = i0 + il < a.nT;
+        const bool ireal = i0 + il < nrow;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int cl = 16 * cb + (l >> 4) + 4 * r;
-          const double v = grm_value(cnt[cb][ib][r], uj_sh[cl], ui_sh[il], invN, cN, invd);
-          acc[cb][ib][r] = (ireal && j0 + cl < a.nT) ? v : 0.0;
+          const double v = grm_value(cnt[cb][ib][r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
+          acc[cb][ib][r] = (ireal && j0 + cl < nrow) ? v : 0.0;
         }
       }
   }
@@ -676,22 +714,22 @@ __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int64_t n_t
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
     if ((l >> 4) == 0) {
-      const int64_t gi = b * nTp + i0 + 32 * w + 16 * ib + l;
+      const int64_t gi = b * ns + i0 + 32 * w + 16 * ib + l;
       a.w[gi] = (J == 0) ? v : a.w[gi] + v;
     }
   }
 }
 
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
-  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.panel, c.pstride, c.off, c.u, c.scal, c.d.nT,
-             c.d.nTp, c.d.nRp, c.d.NT, 0, c.skip};
-  hipLaunchKernelGGL(k_diag_grm, dim3((unsigned)(c.B * c.d.NT)), dim3(256), 0, s, a);
+  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
+             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, 0, c.skip};
+  hipLaunchKernelGGL(k_diag_grm, dim3((unsigned)(c.B * c.sd.NT)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag) {
-  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.panel, c.pstride, c.off, c.u, c.scal, c.d.nT,
-             c.d.nTp, c.d.nRp, c.d.NT, J, c.skip};
+  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
+             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, J, c.skip};
   if (diag) {
     a.NSX = (J >= 2) ? std::min(J - 1, NSX_MAX) : 0;   // written by the off-diagonal launch of J-1
     if (J >= 1) {
@@ -701,9 +739,9 @@ hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag) {
     }
     hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
   } else {
-    const int nI = c.d.NT - J - 1;
+    const int nI = c.sd.NT - J - 1;
     if (nI <= 0) return hipSuccess;
-    a.NSX = (J >= 1 && J + 1 < c.d.NT) ? std::min(J, NSX_MAX) : 0;
+    a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? std::min(J, NSX_MAX) : 0;
     const int64_t n_tiles = c.B * nI;
     hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX)), dim3(256), 0, s, a, n_tiles);
   }

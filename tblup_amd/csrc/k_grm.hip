@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void k_grm(const int8_t* __restrict__ panel, i
                nRp * KBLK, lds, acc);
 
   // epilogue: exact-integer centring in fp64, padding rows/cols -> identity
-  const double* sc = scal + b * 8;
+  const double* sc = scal + b * SCAL;
   const double invN = sc[0], cN = sc[1], invd = sc[2], lam = sc[4];
   const double* ub = u + b * nRp;
   double* Kb = K + b * nRp * nTp;

@@ -81,28 +81,45 @@ hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ g, int64_t n, int64_t P,
                                                      const int32_t* __restrict__ rowmap, int64_t nRp, int64_t nT,
-                                                     int8_t* __restrict__ out, int32_t* __restrict__ csT) {
+                                                     const double* __restrict__ yT, double meanyT,
+                                                     int8_t* __restrict__ out, int32_t* __restrict__ csT,
+                                                     double* __restrict__ xty) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * 4 + w;
-  if (p >= P) return;
-  const int8_t* row = g + p * n;
+  if (p > P) return;
   int8_t* orow = out + p * nRp;
+  if (p == P) {   // the zero row
+    for (int64_t r = l; r < nRp; r += 64) orow[r] = 0;
+    return;
+  }
+  const int8_t* row = g + p * n;
   int s = 0;
+  double dot = 0.0;
   for (int64_t r = l; r < nRp; r += 64) {
     const int32_t src = rowmap[r];
     const int8_t v = src >= 0 ? row[src] : (int8_t)0;
     orow[r] = v;
-    if (r < nT) s += v;
+    if (r < nT) {
+      s += v;
+      dot += (double)v * (yT[r] - meanyT);
+    }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (l == 0) csT[p] = s;
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    dot += __shfl_xor(dot, o);
+  }
+  if (l == 0) {
+    csT[p] = s;
+    xty[p] = dot;
+  }
 }
 
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap, int64_t nRp,
-                              int64_t nT, int8_t* geno_split, int32_t* colsum_T, hipStream_t s) {
-  hipLaunchKernelGGL(k_build_split, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, s, geno_sm, n, P, rowmap, nRp,
-                     nT, geno_split, colsum_T);
+                              int64_t nT, const double* yT, double meanyT, int8_t* geno_split, int32_t* colsum_T,
+                              double* xty, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_split, dim3((unsigned)((P + 1 + 3) / 4)), dim3(256), 0, s, geno_sm, n, P, rowmap, nRp,
+                     nT, yT, meanyT, geno_split, colsum_T, xty);
   return hipGetLastError();
 }
 
@@ -113,14 +130,17 @@ __device__ __forceinline__ int64_t clamp_idx(int64_t p, int64_t P) { return p < 
 
 __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ csT,
-                                                     const int32_t* __restrict__ csA, int64_t n, int64_t nT,
-                                                     int64_t P, int branch, double meanyT, double h2,
-                                                     double* __restrict__ scal) {
+                                                     const int32_t* __restrict__ csA, const double* __restrict__ xty,
+                                                     int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
+                                                     int64_t ns, int branch, double meanyT, double h2,
+                                                     double* __restrict__ scal, double* __restrict__ u,
+                                                     double* __restrict__ rhs) {
   const int64_t b = blockIdx.x;
   const int64_t o0 = off[b], k = off[b + 1] - o0;
   int mode = branch;
   if (mode == 0) mode = (k > n) ? 1 : 2;  // evaluator.py:257
   const int32_t* cs = (mode == 1) ? csA : csT;
+  const bool primal = form == FORM_PRIMAL;   // snp branch only (host guarantees)
   int64_t m1 = 0, q = 0;
   for (int64_t s = threadIdx.x; s < k; s += 256) {
     const int64_t m = cs[clamp_idx(idx[o0 + s], P)];
@@ -128,6 +148,7 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
     q += m * m;
   }
   __shared__ int64_t r1[256], r2[256];
+  __shared__ double invd_sh;
   r1[threadIdx.x] = m1;
   r2[threadIdx.x] = q;
   __syncthreads();
@@ -142,23 +163,40 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
     const double N = (mode == 1) ? (double)n : (double)nT;
     const double M1 = (double)r1[0], Q = (double)r2[0];
     const double d = M1 / N - Q / (2.0 * N * N);  // 2 sum p(1-p)
-    double* sc = scal + b * 8;
-    sc[0] = 1.0 / N;
-    sc[1] = Q / (N * N);
-    sc[2] = 1.0 / d;
-    sc[3] = (mode == 2) ? meanyT : 0.0;
-    sc[4] = (1.0 - h2) / h2;
-    sc[5] = d;
-    sc[6] = (double)mode;
-    sc[7] = (double)k;
+    double* sc = scal + b * SCAL;
+    // primal (SNP-space) form: C_ab = (X^T X)_ab - s_a s_b / n_T over train rows
+    sc[SC_SA] = primal ? 0.0 : 1.0 / N;
+    sc[SC_CN] = primal ? 0.0 : Q / (N * N);
+    sc[SC_INVD] = 1.0 / d;
+    sc[SC_MU] = (mode == 2) ? meanyT : 0.0;
+    sc[SC_LAM] = (1.0 - h2) / h2;
+    sc[SC_D] = d;
+    sc[SC_MODE] = (double)mode;
+    sc[SC_K] = (double)k;
+    sc[SC_SM] = primal ? 1.0 / (double)nT : 0.0;
+    sc[SC_NROW] = primal ? (double)k : (double)nT;
+    sc[SC_CBLK] = primal ? (double)(nTp / KBLK) : (double)((k + KBLK - 1) / KBLK);
+    invd_sh = 1.0 / d;
+  }
+  if (!primal) return;
+  __syncthreads();
+  // u_a = s_a (train allele count), rhs_a = X_c^T (y_T - mu) / d = xty[p_a] / d
+  // (the sklearn primal right-hand side in 1/d units); zero on padding rows
+  const double invd = invd_sh;
+  for (int64_t a = threadIdx.x; a < ns; a += 256) {
+    const bool real = a < k;
+    const int64_t p = real ? clamp_idx(idx[o0 + a], P) : 0;
+    u[b * ns + a] = real ? (double)csT[p] : 0.0;
+    rhs[b * ns + a] = real ? xty[p] * invd : 0.0;
   }
 }
 
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
-                              const int32_t* colsum_all, const EvalDims& d, int branch, double meanyT, double h2,
-                              double* scal, hipStream_t s) {
-  hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, colsum_T, colsum_all, d.n, d.nT,
-                     d.P, branch, meanyT, h2, scal);
+                              const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
+                              int branch, double meanyT, double h2, double* scal, double* u, double* rhs,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, colsum_T, colsum_all, xty, d.n,
+                     d.nT, d.nTp, d.P, sd.form, sd.ns, branch, meanyT, h2, scal, u, rhs);
   return hipGetLastError();
 }
 
@@ -181,7 +219,7 @@ __global__ __launch_bounds__(128) void k_gather(const int8_t* __restrict__ gs, c
   const int64_t b = blockIdx.y;
   const int64_t r0 = (int64_t)blockIdx.x * GATHER_ROWS;
   const int64_t o0 = off[b], k = off[b + 1] - o0;
-  const int mode = (int)scal[b * 8 + 6];
+  const int mode = (int)scal[b * SCAL + SC_MODE];
   const int32_t* cs = (mode == 1) ? csA : csT;
   const int64_t nblk = (k + KBLK - 1) / KBLK;
   int8_t* pb = panel + b * panel_stride;

@@ -1,8 +1,10 @@
 // Back substitution, prediction and fitness, one 1024-thread workgroup per individual.
 //
-//   alpha = L^{-T} z                       (z = L^{-1}(y_T - mu) from k_chol_diag)
-//   EBV_V = K_VT alpha + mu, K_VT applied in factored form from the int8 panel                gblup: evaluator.py:284 (G[:,T] Ginv y_T, mu = 0)
+//   alpha = L^{-T} z                       (z = L^{-1} rhs from k_chol_diag)
+//   dual:   EBV_V = K_VT alpha + mu, K_VT applied in factored form from the int8 panel
+//                                          gblup: evaluator.py:284 (G[:,T] Ginv y_T, mu = 0)
 //                                          snp:   evaluator.py:314 (clf.predict, intercept mean(y_T))
+//   primal: EBV_V = (X_V - 2p) beta + mean(y_T), beta = alpha (sklearn primal Ridge coef_)
 //   fitness = |pearsonr(EBV_V, y_V)|       evaluator.py:286 / :314, scipy 1.15.3 pearsonr:
 //            exact-equality constant input -> NaN; mean-centre; max-abs scaled
 //            norms; clip to [-1, 1]; round when n == 2.
@@ -43,22 +45,22 @@ __device__ double block_max(double v, double* red) {
 }  // namespace
 
 __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict__ fit, double* __restrict__ ebv) {
-  extern __shared__ double dyn[];  // alpha[nTp] then e[nV]
+  extern __shared__ double dyn[];  // alpha[ns] then e[nV]
   __shared__ double part[NTH / 64][2 * TILE];   // back-substitution partials; reused as [64][64]
   __shared__ double vsh[TILE];
   __shared__ double wblk[KBLK];
   __shared__ double red[NTH / 64];
-  const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, nRp = c.d.nRp;
+  const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, ns = c.sd.ns, prow = c.sd.prow;
   const double* yV = c.yV;
-  const int NT = c.d.NT;
+  const int NT = c.sd.NT;
   double* alpha = dyn;
-  double* e = dyn + nTp;
+  double* e = dyn + ns;
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
   const double* Db = c.Dinv + b * (int64_t)NT * TILE * TILE;
-  const double* sc = c.scal + b * 8;
-  const double invN = sc[0], cN = sc[1], invd = sc[2], mu = sc[3];
+  const double* sc = c.scal + b * SCAL;
+  const double invN = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], mu = sc[SC_MU];
 
   // alpha = L^{-T} z, block rows from the bottom, using the stored diagonal inverses.
   // (L_JI^T alpha_J)[c] = sum_r Lt_(J,I)[c][r] alpha_J[r]: row c of the transposed tile,
@@ -78,7 +80,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     s += __shfl_xor(s, 1);
     s += __shfl_xor(s, 2);
     s += __shfl_xor(s, 4);
-    if (seg == 0) vsh[rc] = c.z[b * nTp + (int64_t)I * TILE + rc] - s;
+    if (seg == 0) vsh[rc] = c.z[b * ns + (int64_t)I * TILE + rc] - s;
     __syncthreads();
     // alpha_I = X_I^T v: Dinv holds X^T, so again row c dotted with v
     const double* xrow = Db + (int64_t)I * TILE * TILE + rc * TILE + 16 * seg;
@@ -95,61 +97,96 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     __syncthreads();
   }
 
-  // EBV_V = K_VT alpha + mu without materialising K_VT (exact-integer factored form):
-  //   sum_t K_vt alpha_t = [sum_s a_vs w_s - u_v S/N - (u_T . alpha)/N + cN S] / d,
-  //   w_s = sum_t a_ts alpha_t,  S = sum_t alpha_t
-  const double* ub = c.u + b * nRp;
-  double s_a = 0.0, s_ua = 0.0;
-  for (int64_t r = t; r < nT; r += NTH) {
-    s_a += alpha[r];
-    s_ua += ub[r] * alpha[r];
-  }
-  const double S = block_sum(s_a, red);
-  const double UA = block_sum(s_ua, red);
-  for (int64_t v = t; v < nV; v += NTH) e[v] = 0.0;
-  const int64_t k = c.off[b + 1] - c.off[b];
-  const int64_t nblk = (k + KBLK - 1) / KBLK;
+  const double* ub = c.u + b * prow;
   const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
-  const int dq = t & 15, rg = t >> 4;   // dword (4 SNPs) within a 64-SNP row block, row group (64)
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    const uint32_t* blk = pb + kb * nRp * (KBLK / 4);
-    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-    for (int64_t r = rg; r < nT; r += NTH / 16) {
-      const uint32_t x = blk[r * (KBLK / 4) + dq];
-      const double ar = alpha[r];
-      p0 += (double)(x & 0xff) * ar;
-      p1 += (double)((x >> 8) & 0xff) * ar;
-      p2 += (double)((x >> 16) & 0xff) * ar;
-      p3 += (double)(x >> 24) * ar;
-    }
-    __syncthreads();
-    double* pw = &part[0][0];   // [64 row groups][64 SNPs]
-    pw[rg * KBLK + 4 * dq + 0] = p0;
-    pw[rg * KBLK + 4 * dq + 1] = p1;
-    pw[rg * KBLK + 4 * dq + 2] = p2;
-    pw[rg * KBLK + 4 * dq + 3] = p3;
-    __syncthreads();
-    if (t < KBLK) {
-      double acc = 0.0;
-      for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
-      wblk[t] = acc;
-    }
-    __syncthreads();
-    for (int64_t v = t; v < nV; v += NTH) {
-      const uint32_t* row = blk + (nTp + v) * (KBLK / 4);
-      double acc = 0.0;
-#pragma unroll 4
-      for (int d4 = 0; d4 < KBLK / 4; ++d4) {
-        const uint32_t x = row[d4];
-        acc += (double)(x & 0xff) * wblk[4 * d4] + (double)((x >> 8) & 0xff) * wblk[4 * d4 + 1] +
-               (double)((x >> 16) & 0xff) * wblk[4 * d4 + 2] + (double)(x >> 24) * wblk[4 * d4 + 3];
+  const int dq = t & 15, rg = t >> 4;   // dword (4 bytes) within a 64-wide block row, row group (64)
+  double* pw = &part[0][0];             // [64 row groups][64]
+  if (c.sd.form == FORM_PRIMAL) {
+    // EBV_v = sum_a x_va beta_a - sum_a (s_a / n_T) beta_a + mu, reduced over a by row groups
+    const int64_t kk = (int64_t)sc[SC_K];
+    double s_ub = 0.0;
+    for (int64_t r = t; r < kk; r += NTH) s_ub += ub[r] * alpha[r];
+    const double MB = block_sum(s_ub, red) * sc[SC_SM];
+    // X_V read in place from the split's SNP-major rows (V animals start at byte nTp)
+    const int64_t o0 = c.off[b];
+    const int64_t nvb = (nV + KBLK - 1) / KBLK;
+    for (int64_t vb = 0; vb < nvb; ++vb) {
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+      for (int64_t r = rg; r < kk; r += NTH / 16) {
+        int64_t p = c.idx[o0 + r];
+        p = p < 0 ? 0 : (p >= c.d.P ? c.d.P - 1 : p);
+        const uint32_t x = reinterpret_cast<const uint32_t*>(c.gs + p * c.gs_row + nTp + vb * KBLK)[dq];
+        const double ar = alpha[r];
+        p0 += (double)(x & 0xff) * ar;
+        p1 += (double)((x >> 8) & 0xff) * ar;
+        p2 += (double)((x >> 16) & 0xff) * ar;
+        p3 += (double)(x >> 24) * ar;
       }
-      e[v] += acc;
+      __syncthreads();
+      pw[rg * KBLK + 4 * dq + 0] = p0;
+      pw[rg * KBLK + 4 * dq + 1] = p1;
+      pw[rg * KBLK + 4 * dq + 2] = p2;
+      pw[rg * KBLK + 4 * dq + 3] = p3;
+      __syncthreads();
+      if (t < KBLK && vb * KBLK + t < nV) {
+        double acc = 0.0;
+        for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
+        e[vb * KBLK + t] = acc - MB + mu;
+      }
     }
+    __syncthreads();
+  } else {
+    // EBV_V = K_VT alpha + mu without materialising K_VT (exact-integer factored form):
+    //   sum_t K_vt alpha_t = [sum_s a_vs w_s - u_v S/N - (u_T . alpha)/N + cN S] / d,
+    //   w_s = sum_t a_ts alpha_t,  S = sum_t alpha_t
+    double s_a = 0.0, s_ua = 0.0;
+    for (int64_t r = t; r < nT; r += NTH) {
+      s_a += alpha[r];
+      s_ua += ub[r] * alpha[r];
+    }
+    const double S = block_sum(s_a, red);
+    const double UA = block_sum(s_ua, red);
+    for (int64_t v = t; v < nV; v += NTH) e[v] = 0.0;
+    const int64_t nblk = (int64_t)sc[SC_CBLK];
+    for (int64_t kb = 0; kb < nblk; ++kb) {
+      const uint32_t* blk = pb + kb * prow * (KBLK / 4);
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+      for (int64_t r = rg; r < nT; r += NTH / 16) {
+        const uint32_t x = blk[r * (KBLK / 4) + dq];
+        const double ar = alpha[r];
+        p0 += (double)(x & 0xff) * ar;
+        p1 += (double)((x >> 8) & 0xff) * ar;
+        p2 += (double)((x >> 16) & 0xff) * ar;
+        p3 += (double)(x >> 24) * ar;
+      }
+      __syncthreads();
+      pw[rg * KBLK + 4 * dq + 0] = p0;
+      pw[rg * KBLK + 4 * dq + 1] = p1;
+      pw[rg * KBLK + 4 * dq + 2] = p2;
+      pw[rg * KBLK + 4 * dq + 3] = p3;
+      __syncthreads();
+      if (t < KBLK) {
+        double acc = 0.0;
+        for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
+        wblk[t] = acc;
+      }
+      __syncthreads();
+      for (int64_t v = t; v < nV; v += NTH) {
+        const uint32_t* row = blk + (nTp + v) * (KBLK / 4);
+        double acc = 0.0;
+#pragma unroll 4
+        for (int d4 = 0; d4 < KBLK / 4; ++d4) {
+          const uint32_t x = row[d4];
+          acc += (double)(x & 0xff) * wblk[4 * d4] + (double)((x >> 8) & 0xff) * wblk[4 * d4 + 1] +
+                 (double)((x >> 16) & 0xff) * wblk[4 * d4 + 2] + (double)(x >> 24) * wblk[4 * d4 + 3];
+        }
+        e[v] += acc;
+      }
+    }
+    __syncthreads();
+    for (int64_t v = t; v < nV; v += NTH) e[v] = (e[v] - ub[nTp + v] * S * invN - UA * invN + cN * S) * invd + mu;
+    __syncthreads();
   }
-  __syncthreads();
-  for (int64_t v = t; v < nV; v += NTH) e[v] = (e[v] - ub[nTp + v] * S * invN - UA * invN + cN * S) * invd + mu;
-  __syncthreads();
 
   // Pearson correlation (scipy.stats.pearsonr restated), fitness = |r|
   const double yb = yV[0], eb = e[0];
@@ -194,7 +231,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 }
 
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s) {
-  const size_t shm = (size_t)(c.d.nTp + c.d.nV) * sizeof(double);
+  const size_t shm = (size_t)(c.sd.ns + c.d.nV) * sizeof(double);
   if (shm > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     if (e != hipSuccess) return e;

@@ -4,16 +4,24 @@
 //   geno_sm   int8  [P][n]        SNP-major genotypes, built once (transpose of the .npy)
 //   colsum_all int32 [P]          per-SNP allele count over all n animals (gblup p)
 //   per split s (train T, valid V; nTp/nVp = sizes rounded up to 128):
-//     geno      int8 [P][nRp]     SNP-major rows permuted to [T | 0-pad | V | 0-pad], nRp = nTp+nVp
+//     geno      int8 [P+1][nRp]   SNP-major rows permuted to [T | 0-pad | V | 0-pad], nRp = nTp+nVp;
+//                                 row P is all zero (padding rows of the primal form)
 //     colsum_T  int32 [P]         allele counts over T (snp p)
+//     xty       f64  [P]          sum_t x_tp (y_t - mean y_T): the primal right-hand side, per SNP
 //     yT        f64 [nTp]         phenotypes of T (0 in padding), yV f64 [nV]
 //   per evaluation chunk of B individuals (workspace):
-//     panel  int8 [b][kblk][nRp][64]  gathered genotypes, animal-major 64-SNP blocks (stride = max kblk)
-//     u      f64  [B][nRp]            u_i = sum_s m_s a_is (exact integers)
-//     scal   f64  [B][8]              1/N, q/N^2, 1/d, mu, lambda, d, branch, k
-//     K      f64  [B][nRp][nTp]       GRM block K_{R,T}; TT lower triangle overwritten by L
-//     Dinv   f64  [B][NT][128][128]   inverse of each diagonal Cholesky tile
-//     z      f64  [B][nTp]            L^{-1}(y_T - mu)
+//   Two equivalent forms of the per-individual system (chosen per chunk, see SysDims):
+//     kernel (dual) form   rows = train animals (ns = nTp), contraction over the k SNPs
+//     SNP (primal) form    rows = the k selected SNPs (ns = round_up(k)), contraction over
+//                          the train animals -- sklearn Ridge's own choice when k <= n_T
+//     panel  int8 [b][cblk][prow][64]  gathered genotypes: 64-wide contraction blocks of
+//                                      prow rows (dual: animals x 64 SNPs, prow = nRp;
+//                                      primal: SNPs x 64 animals, prow = ns, T then V blocks)
+//     u      f64  [B][prow]            centring sums (dual: u_i = sum_s m_s a_is; primal: s_a)
+//     scal   f64  [B][16]              see SC_* below
+//     L      f64  [B][NT][NT][128^2]   Lt tiles (tile (I,J) holds L_IJ^T)
+//     Dinv   f64  [B][NT][128][128]    X^T of each diagonal tile, X = L_JJ^{-1}
+//     z      f64  [B][ns]              L^{-1} rhs
 //     fit    f64  [B]
 #pragma once
 #include <hip/hip_runtime.h>
@@ -25,6 +33,32 @@ constexpr int TILE = 128;      // output tile edge of the GRM and Cholesky kerne
 constexpr int TBLUP_NSLOT = 5; // diagonal-tile slots per individual: 4 SYRK partials + the assembled tile
 constexpr int KBLK = 64;       // SNPs per panel block (int8 MFMA K step)
 constexpr int GATHER_ROWS = 128;
+
+// per-individual scalars scal[b][SCAL]
+constexpr int SCAL = 16;
+enum {
+  SC_SA = 0,    // additive centring coefficient (dual 1/N, primal 0)
+  SC_CN = 1,    // constant centring term (dual q/N^2, primal 0)
+  SC_INVD = 2,  // 1/d
+  SC_MU = 3,    // intercept (snp: mean y_T, gblup: 0)
+  SC_LAM = 4,   // lambda = (1-h2)/h2
+  SC_D = 5,     // d = 2 sum p(1-p)
+  SC_MODE = 6,  // branch: 1 gblup, 2 snp
+  SC_K = 7,     // selected SNPs
+  SC_SM = 8,    // multiplicative centring coefficient (dual 0, primal 1/n_T)
+  SC_NROW = 9,  // real system rows (dual n_T, primal k); the rest is identity padding
+  SC_CBLK = 10, // contraction blocks of 64 for the system matrix
+};
+enum { FORM_DUAL = 0, FORM_PRIMAL = 1 };
+
+// System dimensions of one chunk.
+struct SysDims {
+  int form;          // FORM_DUAL / FORM_PRIMAL
+  int64_t ns;        // padded system size (multiple of TILE)
+  int NT;            // ns / TILE
+  int64_t prow;      // panel rows per contraction block
+  int64_t cblk;      // contraction blocks per individual in the panel (max over the chunk)
+};
 
 typedef double v2d __attribute__((ext_vector_type(2)));
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -45,11 +79,13 @@ struct EvalDims {
 hipError_t launch_transpose_geno(const int8_t* src, int8_t* dst, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap,
-                              int64_t nRp, int64_t nT, int8_t* geno_split, int32_t* colsum_T,
-                              hipStream_t s);
+                              int64_t nRp, int64_t nT, const double* yT, double meanyT, int8_t* geno_split,
+                              int32_t* colsum_T, double* xty, hipStream_t s);
+// primal form (sd.form): also u[b][a] = s_a and rhs[b][a] = xty[p_a] / d over the ns rows
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
-                              const int32_t* colsum_all, const EvalDims& d, int branch, double meanyT,
-                              double h2, double* scal, hipStream_t s);
+                              const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
+                              int branch, double meanyT, double h2, double* scal, double* u, double* rhs,
+                              hipStream_t s);
 hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int64_t* off,
                          int64_t panel_stride, int64_t B, const int32_t* colsum_T,
                          const int32_t* colsum_all, const double* scal, const EvalDims& d,
@@ -62,11 +98,13 @@ hipError_t launch_grm(const int8_t* panel, int64_t panel_stride, const int64_t* 
 // ---- launchers (k_chol.hip, k_solve.hip) ----
 struct CholLaunch {
   EvalDims d;
+  SysDims sd;
   int64_t B;
   double* L;             // Lt tiles [B][NT][NT][128*128] (tile (I,J) holds L_IJ^T)
   double* Dinv;          // [B][NT][128][128]
-  double* z;             // [B][nTp]
-  double* w;             // [B][nTp] forward-substitution partial sums
+  double* z;             // [B][ns]
+  double* w;             // [B][ns] forward-substitution partial sums
+  const double* rhs;     // [B][ns] primal right-hand side (dual: y_T - mu on the fly)
   double* S;             // [B][TBLUP_NSLOT][36*256] SYRK partials + assembled diagonal tile
   double* Kd;            // [B][NT][36*256] GRM diagonal tiles
   const double* yT;      // split phenotypes [nTp]
@@ -74,8 +112,11 @@ struct CholLaunch {
   const int8_t* panel;   // gathered genotypes
   int64_t pstride;       // panel bytes per individual
   const int64_t* off;    // [B+1] device offsets
-  const double* u;       // [B][nRp]
-  const double* scal;    // [B][8]
+  const int8_t* gs;      // split SNP-major matrix [P+1][gs_row] (row P zero): primal rows in place
+  const int64_t* idx;    // device SNP indices of the chunk
+  int64_t gs_row;        // bytes per split row (nRp)
+  const double* u;       // [B][prow]
+  const double* scal;    // [B][SCAL]
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
 };
 // one tile column J of the fused GRM + Cholesky: diag=true -> k_chol_diag, else k_chol_offdiag

@@ -214,3 +214,66 @@ def test_config2_gblup_branch_sample(config2):
         f, e = O.blup_grm_form(g, c["T"], c["V"], c["geno"], c["pheno"], 0.4)
         assert abs(fit[i] - f) <= FIT_ATOL
         assert _relmax(ebv[i], e) <= EBV_RTOL
+
+
+# ---------------------------------------------------------------------------
+# SNP-space (primal) form: sklearn's own Ridge solve when k <= n_T.  Forced with
+# TBLUP_FORM=2 on the golden cases (mixed k, k = 1, duplicates, k > n_T), and
+# selected automatically at config-2 shape (k = 1000 < n_T = 1280).
+# ---------------------------------------------------------------------------
+def _snp_cases(z):
+    return [(i, name, idx) for i, (name, idx) in enumerate(_cases(z)) if str(z["branch"][i]) == "snp"]
+
+
+@pytest.mark.parametrize("form", ["1", "2"])
+def test_forced_form_matches_goldens(golden_dir, gpu, monkeypatch, form):
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_200x1000.npz")
+    monkeypatch.setenv("TBLUP_FORM", form)
+    cases = _snp_cases(z)
+    assert len(cases) >= 6
+    with GpuBlupEngine(z["geno"], z["pheno"]) as eng:
+        fit, ebv = eng.evaluate([c[2] for c in cases], z["T"], z["V"], float(z["h2"]), return_ebv=True)
+        TV = np.concatenate([z["T"], z["V"]])
+        tfit, tebv = eng.evaluate([c[2] for c in cases], TV, z["X"], float(z["h2"]), return_ebv=True)
+    for j, (i, name, _) in enumerate(cases):
+        assert abs(fit[j] - z["fitness"][i]) <= FIT_ATOL, name
+        assert _relmax(ebv[j], z["ebv"][i]) <= EBV_RTOL, name
+        assert abs(tfit[j] - z["test_fitness"][i]) <= FIT_ATOL, name
+        assert _relmax(tebv[j], z["test_ebv"][i]) <= EBV_RTOL, name
+
+
+def test_forced_primal_degenerate_panels(golden_dir, gpu, monkeypatch):
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_edge.npz")
+    monkeypatch.setenv("TBLUP_FORM", "2")
+    with GpuBlupEngine(z["geno"], z["pheno"]) as eng:
+        f = eng.evaluate([np.arange(10, 20), np.arange(0, 10)], z["T"], z["V"], 0.4, branch="snp")
+        assert np.all(np.isnan(f)), f
+
+
+def test_config2_shape_golden_primal(golden_dir, gpu):
+    """The three snp genomes alone: auto-selects the primal form (k = 1000 < n_T = 1280)."""
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_2000x4000.npz")
+    geno = O.synth_geno(np.random.default_rng(int(z["seed"])), int(z["n"]), int(z["p"]))
+    genomes = [z["idx"][z["offsets"][i]:z["offsets"][i + 1]] for i in range(3)]
+    assert all(len(g) <= len(z["T"]) - 128 for g in genomes)
+    with GpuBlupEngine(geno, z["pheno"]) as eng:
+        fit, ebv = eng.evaluate(genomes, z["T"], z["V"], 0.4, return_ebv=True)
+    for i in range(3):
+        assert abs(fit[i] - z["fitness"][i]) <= FIT_ATOL
+        assert _relmax(ebv[i], z["ebv"][i]) <= EBV_RTOL
+
+
+def test_config2_forms_agree(config2, monkeypatch):
+    """Kernel (dual) form vs the auto-selected SNP (primal) form at full size."""
+    from tblup_amd.engine import GpuBlupEngine
+    c = config2
+    monkeypatch.setenv("TBLUP_FORM", "1")
+    sel = [c["genomes"][i] for i in range(0, 256, 32)]
+    with GpuBlupEngine(c["geno"], c["pheno"]) as eng:
+        fit, ebv = eng.evaluate(sel, c["T"], c["V"], 0.4, return_ebv=True)
+    for j, i in enumerate(range(0, 256, 32)):
+        assert abs(fit[j] - c["fit"][i]) <= FIT_ATOL
+        assert _relmax(ebv[j], c["ebv"][i]) <= EBV_RTOL
