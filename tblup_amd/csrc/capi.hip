@@ -283,7 +283,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   if (K_out) *K_out = L;
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p, panel, pstride, d_off,
                 (const int8_t*)sp.geno.p, d_idx, d.nRp, u, scal,
-                c->dbg_skip};
+                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0)};
   const double T3 = (double)TILE * TILE * TILE;
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
   const double cbar = (sd.form == FORM_PRIMAL) ? (double)d.nT : kbar;   // contraction length

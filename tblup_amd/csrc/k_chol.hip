@@ -37,8 +37,8 @@ constexpr int BKD = 16;                // k rows per fp64 stage
 constexpr int LTS = BKD * TILE;        // doubles in one 16-row stage of an Lt tile (16 KiB)
 constexpr int TT = TILE * TILE;        // doubles per tile
 constexpr int NSX_MAX = 4;             // SYRK partials of L < J-1 (computed in the previous off-diagonal launch)
-constexpr int NSLOT = TBLUP_NSLOT;     // + one slot for the assembled tile (k_diag_prep)
-static_assert(NSLOT == NSX_MAX + 1, "slot layout");
+constexpr int NSLOT = TBLUP_NSLOT;
+static_assert(NSLOT == NSX_MAX, "slot layout");
 
 __device__ __forceinline__ v4d mfma64(double a, double b, v4d c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -407,10 +407,8 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
     }
 }
 
-// Assemble T_J = K_JJ + sum of the L < J-1 partials - L_{J,J-1} L_{J,J-1}^T into slot NSX_MAX.
-// Grid B x 4: workgroup g owns the 9 packed blocks {g + 4i}; its wave v takes k rows
-// [32v, 32v+32) of Lt tile (J, J-1) straight from global (16 lanes read one 128-B row
-// segment), the 4 waves are reduced through LDS and the sum is written once.
+// SYRK of 32 k rows of an Lt tile for the 9 packed blocks {W + 4i}, straight from global
+// (16 lanes read one 128-B row segment).
 template <int W>
 __device__ __forceinline__ void syrk_rows_global(const double* __restrict__ lt, int k0, v4d (&acc)[9], int l) {
 #pragma unroll 2
@@ -421,45 +419,6 @@ __device__ __forceinline__ void syrk_rows_global(const double* __restrict__ lt, 
     for (int q = 0; q < 8; ++q) a8[q] = lt[k * TILE + 16 * q + (l & 15)];
 #pragma unroll
     for (int i = 0; i < 9; ++i) acc[i] = mfma64(a8[tri_q(W + 4 * i)], a8[tri_s(W + 4 * i)], acc[i]);
-  }
-}
-
-__global__ __launch_bounds__(256, 2) void k_diag_prep(CholArgs a) {
-  __shared__ double red[4][9][BLKD];   // 72 KiB
-  const int t = threadIdx.x, l = t & 63, v = t >> 6;
-  const int J = a.J, NT = a.NT;
-  const int64_t b = blockIdx.x >> 2;
-  const int g = blockIdx.x & 3;
-  v4d acc[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-  if (!(a.skip & 2)) {
-    const double* lt = a.L + ((b * NT + J) * (int64_t)NT + (J - 1)) * TT;
-    if (g == 0) syrk_rows_global<0>(lt, 32 * v, acc, l);
-    else if (g == 1) syrk_rows_global<1>(lt, 32 * v, acc, l);
-    else if (g == 2) syrk_rows_global<2>(lt, 32 * v, acc, l);
-    else syrk_rows_global<3>(lt, 32 * v, acc, l);
-  }
-#pragma unroll
-  for (int i = 0; i < 9; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[v][i][bo((l >> 4) + 4 * r, l & 15)] = acc[i][r];
-  __syncthreads();
-  const double* Kb = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
-  double* Sb = a.S + b * (int64_t)NSLOT * NPACK * BLKD;
-  const int nsx = a.NSX;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int e = g + 4 * i;
-    const int off = pk(tri_q(e), tri_s(e)) + t;
-    double sum = Kb[off];
-#pragma unroll
-    for (int q = 0; q < NSX_MAX; ++q) {
-      const double pq = Sb[q * NPACK * BLKD + off];
-      sum += (q < nsx) ? pq : 0.0;
-    }
-    sum -= (red[0][i][t] + red[1][i][t]) + (red[2][i][t] + red[3][i][t]);
-    Sb[NSX_MAX * NPACK * BLKD + off] = sum;
   }
 }
 
@@ -489,16 +448,44 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   double* Xd = lds + NPACK * BLKD;   // X_pp, p = 0..7
   double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;   // X^T, row-major: XT[c][i] = X[i][c]
 
-  // T = K_JJ - sum_{L<J} L_JL L_JL^T: k_diag_grm's tile for J = 0, else k_diag_prep's sum
+  // T = K_JJ - sum_{L<J} L_JL L_JL^T = Kd (k_diag_grm) + the L < J-1 partials (previous
+  // off-diagonal launch) - L_{J,J-1} L_{J,J-1}^T (here: wave w takes the packed blocks
+  // {w + 4i} over all 128 k rows of Lt tile (J, J-1), straight from global)
   {
-    const double* src = (J == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
-                                 : a.S + (b * NSLOT + NSX_MAX) * (int64_t)NPACK * BLKD;
+    const double* Kb = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
+    const double* Pb = a.S + b * (int64_t)NSLOT * NPACK * BLKD;
+    const int nsx = a.NSX;
+#pragma unroll 2
+    for (int e = 2 * t; e < NPACK * BLKD; e += 512) {
+      v2d sum = *reinterpret_cast<const v2d*>(Kb + e);
 #pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread, LDS-DMA
-      const int chunk = (e * 4 + w) * 64;
-      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
+      for (int q = 0; q < NSX_MAX; ++q) {
+        const v2d pq = *reinterpret_cast<const v2d*>(Pb + q * NPACK * BLKD + e);
+        sum[0] += (q < nsx) ? pq[0] : 0.0;
+        sum[1] += (q < nsx) ? pq[1] : 0.0;
+      }
+      *reinterpret_cast<v2d*>(Tp + e) = sum;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (J >= 1 && !(a.skip & 2)) {
+      v4d acc[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
+      const double* lt = a.L + ((b * NT + J) * (int64_t)NT + (J - 1)) * TT;
+      for (int k0 = 0; k0 < TILE; k0 += 32) {
+        if (w == 0) syrk_rows_global<0>(lt, k0, acc, l);
+        else if (w == 1) syrk_rows_global<1>(lt, k0, acc, l);
+        else if (w == 2) syrk_rows_global<2>(lt, k0, acc, l);
+        else syrk_rows_global<3>(lt, k0, acc, l);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int e = w + 4 * i;
+        double* blk = Tp + pk(tri_q(e), tri_s(e));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) blk[bo((l >> 4) + 4 * r, l & 15)] -= acc[i][r];
+      }
+    }
   }
   if (t < TILE) {
     const int64_t gi = j0 + t;
@@ -534,11 +521,11 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   }
   if (a.skip & 16) return;
 
-  // E1. X^T tile: diagonal blocks from Xd, zeros where X is zero (block row > block col of X^T)
-  for (int e = t; e < TT; e += 256) {
-    const int rr = e >> 7, cc = e & 127;
-    if ((rr >> 4) == (cc >> 4)) XT[e] = Xd[(rr >> 4) * BLKD + bo(cc & 15, rr & 15)];
-    else if ((rr >> 4) > (cc >> 4)) XT[e] = 0.0;
+  // E1. X^T tile: diagonal blocks from Xd.  Blocks below the diagonal of X^T (X = 0 there)
+  //     are never written and never read (k_solve and the off-diagonal GEMM2 skip them).
+  for (int e = t; e < NBLK * BLKD; e += 256) {
+    const int pb = e >> 8, rr = (e >> 4) & 15, cc = e & 15;
+    XT[(16 * pb + rr) * TILE + 16 * pb + cc] = Xd[pb * BLKD + bo(cc, rr)];
   }
   __threadfence_block();
   __syncthreads();
@@ -572,10 +559,14 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   }
 
   // E2. L_JJ^T into the Lt tile (J, J); z_J = X_J r  (z_i = sum_c XT[c][i] r_c)
-  double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
-  for (int e = t; e < TT; e += 256) {
-    const int rr = e >> 7, cc = e & 127;
-    Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
+  //     (L_JJ itself is read by nothing downstream -- only X is -- so it is written only
+  //     for the debug readback)
+  if (a.skip & FLAG_WRITE_LJJ) {
+    double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
+    for (int e = t; e < TT; e += 256) {
+      const int rr = e >> 7, cc = e & 127;
+      Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
+    }
   }
   if (t < TILE) {
     double acc_z = 0.0;
@@ -732,11 +723,6 @@ hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag) {
              c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, J, c.skip};
   if (diag) {
     a.NSX = (J >= 2) ? std::min(J - 1, NSX_MAX) : 0;   // written by the off-diagonal launch of J-1
-    if (J >= 1) {
-      hipLaunchKernelGGL(k_diag_prep, dim3((unsigned)(c.B * 4)), dim3(256), 0, s, a);
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
     hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
   } else {
     const int nI = c.sd.NT - J - 1;

@@ -83,12 +83,15 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     if (seg == 0) vsh[rc] = c.z[b * ns + (int64_t)I * TILE + rc] - s;
     __syncthreads();
     // alpha_I = X_I^T v: Dinv holds X^T, so again row c dotted with v
+    // (blocks with seg < rc/16 are zero in X^T and are never stored)
     const double* xrow = Db + (int64_t)I * TILE * TILE + rc * TILE + 16 * seg;
     double s2 = 0.0;
+    if (seg >= (rc >> 4)) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const v2d x = *reinterpret_cast<const v2d*>(xrow + 2 * e);
-      s2 += x[0] * vsh[16 * seg + 2 * e] + x[1] * vsh[16 * seg + 2 * e + 1];
+      for (int e = 0; e < 8; ++e) {
+        const v2d x = *reinterpret_cast<const v2d*>(xrow + 2 * e);
+        s2 += x[0] * vsh[16 * seg + 2 * e] + x[1] * vsh[16 * seg + 2 * e + 1];
+      }
     }
     s2 += __shfl_xor(s2, 1);
     s2 += __shfl_xor(s2, 2);

@@ -30,7 +30,7 @@
 namespace tblup {
 
 constexpr int TILE = 128;      // output tile edge of the GRM and Cholesky kernels
-constexpr int TBLUP_NSLOT = 5; // diagonal-tile slots per individual: 4 SYRK partials + the assembled tile
+constexpr int TBLUP_NSLOT = 4; // SYRK partials of a diagonal tile per individual
 constexpr int KBLK = 64;       // SNPs per panel block (int8 MFMA K step)
 constexpr int GATHER_ROWS = 128;
 
@@ -50,6 +50,7 @@ enum {
   SC_CBLK = 10, // contraction blocks of 64 for the system matrix
 };
 enum { FORM_DUAL = 0, FORM_PRIMAL = 1 };
+constexpr int FLAG_WRITE_LJJ = 1 << 16;   // CholLaunch::skip: also store L_JJ (debug readback only)
 
 // System dimensions of one chunk.
 struct SysDims {
