@@ -52,7 +52,6 @@ struct Split {
 };
 
 enum { KC_STATS = 0, KC_GATHER, KC_GRM, KC_DIAG, KC_OFFDIAG, KC_SOLVE };
-#define TBLUP_MAX_GROUPS 4
 
 struct EventPair {
   int cls;
@@ -79,9 +78,7 @@ struct tblup_ctx {
   double flops[TBLUP_N_KCLASS] = {0};
   double bytes[TBLUP_N_KCLASS] = {0};
   int64_t mem_in_use = 0;
-  int n_groups = 2;   // TBLUP_STREAMS: concurrent stream groups for the Cholesky
-  hipStream_t aux[TBLUP_MAX_GROUPS - 1] = {};
-  hipEvent_t ev_fork = nullptr, ev_join[TBLUP_MAX_GROUPS - 1] = {};
+
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
   int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
 };
@@ -176,7 +173,7 @@ size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_
   add((size_t)B * sd.ns * 8);                                   // z
   add((size_t)B * sd.ns * 8);                                   // w
   add((size_t)B * sd.ns * 8);                                   // rhs
-  add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // SYRK partials + assembled tile
+  add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // next diagonal tile (minus its last SYRK term)
   add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nV * 8 : 0);                     // ebv
@@ -287,63 +284,32 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const double T3 = (double)TILE * TILE * TILE;
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
   const double cbar = (sd.form == FORM_PRIMAL) ? (double)d.nT : kbar;   // contraction length
-  // The batch is split into groups on separate streams so that one group's latency-bound
-  // diagonal-tile work overlaps another group's MFMA-bound off-diagonal tiles.
-  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_groups, B / 32));
-  hipStream_t gs[TBLUP_MAX_GROUPS];
-  CholLaunch gl[TBLUP_MAX_GROUPS];
-  for (int g = 0; g < G; ++g) {
-    const int64_t b0 = B * g / G, b1 = B * (g + 1) / G;
-    CholLaunch x = cl;
-    x.B = b1 - b0;
-    x.L = cl.L + b0 * sd.ns * sd.ns;
-    x.Dinv = cl.Dinv + b0 * (int64_t)sd.NT * TILE * TILE;
-    x.z = cl.z + b0 * sd.ns;
-    x.w = cl.w + b0 * sd.ns;
-    x.rhs = cl.rhs + b0 * sd.ns;
-    x.S = cl.S + b0 * TBLUP_NSLOT * 36 * 256;
-    x.Kd = cl.Kd + b0 * (int64_t)sd.NT * 36 * 256;
-    x.panel = cl.panel + b0 * pstride;
-    x.off = cl.off + b0;
-    x.u = cl.u + b0 * sd.prow;
-    x.scal = cl.scal + b0 * SCAL;
-    gl[g] = x;
-    gs[g] = (g == 0) ? s : c->aux[g - 1];
-  }
   {
     const double fg = (double)B * sd.NT * 128.0 * 129.0 * cbar;   // int ops of the diagonal GRM tiles
     rc = timed(c, s, KC_GRM, fg, (double)B * sd.NT * 36 * 256 * 8.0, [&] { return launch_diag_grm(cl, s); });
     if (rc) return rc;
   }
-  if (G > 1) {
-    HIPCHK(hipEventRecord(c->ev_fork, s));
-    for (int g = 1; g < G; ++g) HIPCHK(hipStreamWaitEvent(gs[g], c->ev_fork, 0));
-  }
+  // Column loop.  (A look-ahead schedule -- tile (J+1, J) and diagonal tile J+1 on a
+  // high-priority stream beside the rest of column J -- measured slower on MI355X: the
+  // chip is already full during the off-diagonal launches, and sharing CUs slows the
+  // critical path more than it hides.)
+  const double Bd = (double)B;
   for (int J = 0; J < sd.NT; ++J) {
     const double jt = (double)J;
+    // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
+    // forward-substitution GEMV (the int8 GRM tiles are counted under KC_GRM)
+    const double fd = Bd * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
+    const double bd = Bd * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
+    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, s); });
+    if (rc) return rc;
     const int nI = sd.NT - J - 1;
-    for (int g = 0; g < G; ++g) {
-      const double Bg = (double)gl[g].B;
-      // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
-      // forward-substitution GEMV (the int8 GRM tiles are counted under KC_GRM)
-      const double fd = Bg * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
-      const double bd = Bg * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
-      rc = timed(c, gs[g], KC_DIAG, fd, bd, [&] { return launch_chol(gl[g], J, gs[g], true); });
+    if (nI > 0) {
+      // per tile: GEMM update 2*128^3*J, triangular solve 128^3 (fused GRM tile int-ops excluded);
+      // plus the preparation of diagonal tile J+1: 128^3 per L < J (lower half stored)
+      const double fo = Bd * nI * (2.0 * T3 * jt + T3) + Bd * T3 * jt;
+      const double bo = Bd * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * Bd * TILE * TILE * jt * 8.0;
+      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(cl, J, s); });
       if (rc) return rc;
-      if (nI > 0) {
-        // per tile: GEMM update 2*128^3*J, triangular solve 128^3 (fused GRM tile int-ops excluded);
-        // plus the L < J SYRK terms of diagonal tile J+1 (128^3 per L, lower half stored)
-        const double fo = Bg * nI * (2.0 * T3 * jt + T3) + Bg * T3 * jt;
-        const double bo = Bg * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * Bg * TILE * TILE * jt * 8.0;
-        rc = timed(c, gs[g], KC_OFFDIAG, fo, bo, [&] { return launch_chol(gl[g], J, gs[g], false); });
-        if (rc) return rc;
-      }
-    }
-  }
-  if (G > 1) {
-    for (int g = 1; g < G; ++g) {
-      HIPCHK(hipEventRecord(c->ev_join[g - 1], gs[g]));
-      HIPCHK(hipStreamWaitEvent(s, c->ev_join[g - 1], 0));
     }
   }
   if (stop_stage == 2) return 0;
@@ -405,13 +371,6 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->dbg_skip = dbg ? atoi(dbg) : 0;
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
-  const char* ns = getenv("TBLUP_STREAMS");
-  c->n_groups = std::max(1, std::min(TBLUP_MAX_GROUPS, ns ? atoi(ns) : 1));
-  for (int g = 0; g < TBLUP_MAX_GROUPS - 1; ++g) {
-    HIPCHK(hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_join[g], hipEventDisableTiming));
-  }
-  HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   const size_t gbytes = (size_t)n * (size_t)P;
   if (int rc = dev_alloc(c.get(), c->geno_sm, gbytes)) return rc;
   if (int rc = dev_alloc(c.get(), c->colsum_all, (size_t)P * 4)) return rc;
@@ -449,11 +408,6 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->colsum_all.release();
   c->scratch.release();
   c->ws.release();
-  for (int g = 0; g < TBLUP_MAX_GROUPS - 1; ++g) {
-    if (c->aux[g]) (void)hipStreamDestroy(c->aux[g]);
-    if (c->ev_join[g]) (void)hipEventDestroy(c->ev_join[g]);
-  }
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;

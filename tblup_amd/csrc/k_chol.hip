@@ -36,13 +36,12 @@ namespace {
 constexpr int BKD = 16;                // k rows per fp64 stage
 constexpr int LTS = BKD * TILE;        // doubles in one 16-row stage of an Lt tile (16 KiB)
 constexpr int TT = TILE * TILE;        // doubles per tile
-constexpr int NSX_MAX = 4;             // SYRK partials of L < J-1 (computed in the previous off-diagonal launch)
-constexpr int NSLOT = TBLUP_NSLOT;
-static_assert(NSLOT == NSX_MAX, "slot layout");
 
 __device__ __forceinline__ v4d mfma64(double a, double b, v4d c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+
+constexpr int NSLOT = TBLUP_NSLOT;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -293,9 +292,9 @@ struct CholArgs {
   double* Dinv;             // [B][NT][128][128]
   double* z;                // [B][ns]
   double* w;                // [B][ns] forward-substitution partial sums
-  double* S;                // [B][NSLOT][36*256] SYRK partials of a diagonal tile
+  double* S;                // [B][2][36*256] K_JJ - sum_{L<J-1} L_JL L_JL^T, slot J&1
   double* Kd;               // [B][NT][36*256] GRM diagonal tiles (k_diag_grm)
-  int NSX;                  // prep: L<J-1 partials to sum; offdiag: extra SYRK workgroups per individual
+  int NSX;                  // off-diagonal launch: diagonal-preparation workgroups per individual (0 or 1)
   const double* yT;         // [nTp] dual right-hand side (y_T - mu, on the fly)
   const double* rhs;        // [B][ns] primal right-hand side
   const int8_t* panel;      // [B] x pstride
@@ -339,20 +338,24 @@ __device__ __forceinline__ int64_t row_kstep(const CholArgs& a) { return a.form 
 // Each piece is written in the packed block layout the diagonal kernel factorises in,
 // so the diagonal kernel sums them with a linear sweep.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void syrk_partial(const CholArgs& a, int64_t b, int Jt, int s0, int s1, int slot,
-                                             double* lds) {
+// S[b][Jt&1] = K_{Jt,Jt} - sum_{L < nterm} L_{Jt,L} L_{Jt,L}^T (packed blocks), by one
+// workgroup through the LDS-DMA stage ring.
+__device__ __forceinline__ void syrk_partial(const CholArgs& a, int64_t b, int Jt, int nterm, double* lds) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   v4d acc[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-  if (!(a.skip & 2))
-    syrk_lower<4>(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT + (int64_t)s0 * LTS, s1 - s0, lds, acc);
-  double* Pd = a.S + (b * NSLOT + slot) * (int64_t)NPACK * BLKD;
+  if (!(a.skip & 2)) syrk_lower<4>(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc);
+  const double* Kb = a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD;
+  double* Pd = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int e = w + 4 * i, q = tri_q(e), sb = tri_s(e);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Pd[pk(q, sb) + bo((l >> 4) + 4 * r, l & 15)] = -acc[i][r];
+    for (int r = 0; r < 4; ++r) {
+      const int o = pk(q, sb) + bo((l >> 4) + 4 * r, l & 15);
+      Pd[o] = Kb[o] - acc[i][r];
+    }
   }
 }
 
@@ -431,15 +434,14 @@ __device__ __forceinline__ void syrk_rows_global(const double* __restrict__ lt, 
 //      (off-diagonal X blocks written to / re-read from Dinv, diagonal ones stay in LDS)
 //   E. write L_JJ^T (Lt tile), X_J^T (Dinv, zeros below its diagonal), z_J = X_J r
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
-  // 72 KiB of T blocks + 16 KiB of diagonal X blocks: small enough to share a CU with an
-  // off-diagonal workgroup of another stream group.  Off-diagonal X blocks live in Dinv.
-  __shared__ __attribute__((aligned(16))) double lds[(NPACK + NBLK) * BLKD];
-  __shared__ double rsh[TILE];
-  __shared__ double piv_sh[NB];
+// Diagonal tile J of individual b.  T = S - sum_{L0 <= L < J} L_JL L_JL^T where S is
+// K_JJ - sum_{L < L0} (the buffer slot J&1 left by an earlier off-diagonal launch) when
+// L0 > 0, else k_diag_grm's K_JJ.  lds >= (NPACK + NBLK) * BLKD doubles.
+__device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, int L0, double* lds, double* rsh,
+                                          double* piv_sh) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int64_t b = blockIdx.x, ns = a.ns;
-  const int J = a.J, NT = a.NT;
+  const int64_t ns = a.ns;
+  const int NT = a.NT;
   const int64_t j0 = (int64_t)J * TILE;
   const double* sc = a.scal + b * SCAL;
   const double mu = sc[SC_MU];
@@ -448,35 +450,28 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   double* Xd = lds + NPACK * BLKD;   // X_pp, p = 0..7
   double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;   // X^T, row-major: XT[c][i] = X[i][c]
 
-  // T = K_JJ - sum_{L<J} L_JL L_JL^T = Kd (k_diag_grm) + the L < J-1 partials (previous
-  // off-diagonal launch) - L_{J,J-1} L_{J,J-1}^T (here: wave w takes the packed blocks
-  // {w + 4i} over all 128 k rows of Lt tile (J, J-1), straight from global)
+  // T = S - sum_{L0 <= L < J} L_JL L_JL^T, wave w taking the packed blocks {w + 4i} over
+  // the 128 k rows of each Lt tile (J, L), straight from global.
   {
-    const double* Kb = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
-    const double* Pb = a.S + b * (int64_t)NSLOT * NPACK * BLKD;
-    const int nsx = a.NSX;
-#pragma unroll 2
-    for (int e = 2 * t; e < NPACK * BLKD; e += 512) {
-      v2d sum = *reinterpret_cast<const v2d*>(Kb + e);
+    const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
+                                  : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
 #pragma unroll
-      for (int q = 0; q < NSX_MAX; ++q) {
-        const v2d pq = *reinterpret_cast<const v2d*>(Pb + q * NPACK * BLKD + e);
-        sum[0] += (q < nsx) ? pq[0] : 0.0;
-        sum[1] += (q < nsx) ? pq[1] : 0.0;
-      }
-      *reinterpret_cast<v2d*>(Tp + e) = sum;
+    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread, LDS-DMA
+      const int chunk = (e * 4 + w) * 64;
+      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
     }
-    if (J >= 1 && !(a.skip & 2)) {
+    if (J > L0 && !(a.skip & 2)) {
       v4d acc[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-      const double* lt = a.L + ((b * NT + J) * (int64_t)NT + (J - 1)) * TT;
-      for (int k0 = 0; k0 < TILE; k0 += 32) {
+      const double* lt = a.L + ((b * NT + J) * (int64_t)NT + L0) * TT;
+      for (int k0 = 0; k0 < TILE * (J - L0); k0 += 32) {
         if (w == 0) syrk_rows_global<0>(lt, k0, acc, l);
         else if (w == 1) syrk_rows_global<1>(lt, k0, acc, l);
         else if (w == 2) syrk_rows_global<2>(lt, k0, acc, l);
         else syrk_rows_global<3>(lt, k0, acc, l);
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
@@ -486,6 +481,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
         for (int r = 0; r < 4; ++r) blk[bo((l >> 4) + 4 * r, l & 15)] -= acc[i][r];
       }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (t < TILE) {
     const int64_t gi = j0 + t;
@@ -575,6 +571,15 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   }
 }
 
+// Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
+// K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
+__global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
+  __shared__ __attribute__((aligned(16))) double lds[(NPACK + NBLK) * BLKD];
+  __shared__ double rsh[TILE];
+  __shared__ double piv_sh[NB];
+  diag_tile(a, blockIdx.x, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh, piv_sh);
+}
+
 // ---------------------------------------------------------------------------
 // off-diagonal tiles of column J (one WG per individual x tile row I > J)
 //   0. cnt = A_J A_I^T on int8 MFMA, landing in the f64 layout; acc = K_JI = K_IJ^T
@@ -583,24 +588,10 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
 //      -> Lt tile (I, J); w_I += L_IJ z_J
 // LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int64_t n_tiles) {
-  __shared__ __attribute__((aligned(16))) double lds[4 * LTS];   // 64 KiB
-  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[TILE];
+__device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I, double* lds, double* uj_sh,
+                                             double* ui_sh, double* zj_sh) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int J = a.J, NT = a.NT;
-  const int nI = NT - J - 1;
-  const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
-  if ((int64_t)blockIdx.x < n_extra) {
-    // extra role (first in the grid, so it overlaps the tiles): SYRK partials of diagonal
-    // tile J+1 over L < J, all of which are final already
-    const int64_t b = blockIdx.x / a.NSX;
-    const int part = (int)(blockIdx.x % a.NSX);
-    syrk_partial(a, b, J + 1, part * 8 * J / a.NSX, (part + 1) * 8 * J / a.NSX, part, lds);
-    return;
-  }
-  const int64_t logical = xcd_remap(blockIdx.x - n_extra, n_tiles);
-  const int64_t b = logical / nI;
-  const int I = J + 1 + (int)(logical % nI);
   const int64_t ns = a.ns;
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
   const double* Lb = a.L + b * (int64_t)NT * NT * TT;
@@ -711,6 +702,22 @@ __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int64_t n_t
   }
 }
 
+// Off-diagonal tiles (I, J) for I0 <= I < I0 + nI, plus (first in the grid, so they
+// overlap the tiles) one workgroup per individual preparing diagonal tile J+1 except its
+// L = J term: S[(J+1)&1] = K - sum_{L<J} (those tiles are final already).
+// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
+__global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
+  __shared__ __attribute__((aligned(16))) double lds[4 * LTS];   // 64 KiB
+  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[TILE];
+  const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
+  if ((int64_t)blockIdx.x < n_extra) {
+    syrk_partial(a, blockIdx.x, a.J + 1, a.J, lds);
+    return;
+  }
+  const int64_t logical = xcd_remap(blockIdx.x - n_extra, n_tiles);
+  offdiag_tile(a, logical / nI, I0 + (int)(logical % nI), lds, uj_sh, ui_sh, zj_sh);
+}
+
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, 0, c.skip};
@@ -718,19 +725,21 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag) {
+hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, J, c.skip};
-  if (diag) {
-    a.NSX = (J >= 2) ? std::min(J - 1, NSX_MAX) : 0;   // written by the off-diagonal launch of J-1
-    hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
-  } else {
-    const int nI = c.sd.NT - J - 1;
-    if (nI <= 0) return hipSuccess;
-    a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? std::min(J, NSX_MAX) : 0;
-    const int64_t n_tiles = c.B * nI;
-    hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX)), dim3(256), 0, s, a, n_tiles);
-  }
+  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
+  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
+             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, J, c.skip};
+  const int I0 = J + 1, nI = c.sd.NT - I0;
+  if (nI <= 0) return hipSuccess;
+  a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;
+  const int64_t n_tiles = c.B * nI;
+  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX)), dim3(256), 0, s, a, I0, nI, n_tiles);
   return hipGetLastError();
 }
 

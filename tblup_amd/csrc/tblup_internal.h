@@ -30,7 +30,7 @@
 namespace tblup {
 
 constexpr int TILE = 128;      // output tile edge of the GRM and Cholesky kernels
-constexpr int TBLUP_NSLOT = 4; // SYRK partials of a diagonal tile per individual
+constexpr int TBLUP_NSLOT = 2; // diagonal-tile preparation buffers per individual (slot J&1)
 constexpr int KBLK = 64;       // SNPs per panel block (int8 MFMA K step)
 constexpr int GATHER_ROWS = 128;
 
@@ -106,7 +106,7 @@ struct CholLaunch {
   double* z;             // [B][ns]
   double* w;             // [B][ns] forward-substitution partial sums
   const double* rhs;     // [B][ns] primal right-hand side (dual: y_T - mu on the fly)
-  double* S;             // [B][TBLUP_NSLOT][36*256] SYRK partials + assembled diagonal tile
+  double* S;             // [B][2][36*256] diagonal-tile preparation, slot J&1
   double* Kd;            // [B][NT][36*256] GRM diagonal tiles
   const double* yT;      // split phenotypes [nTp]
   const double* yV;      // [nV]
@@ -120,8 +120,10 @@ struct CholLaunch {
   const double* scal;    // [B][SCAL]
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
 };
-// one tile column J of the fused GRM + Cholesky: diag=true -> k_chol_diag, else k_chol_offdiag
-hipError_t launch_chol(const CholLaunch& c, int J, hipStream_t s, bool diag);
+// Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
+// then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.
+hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s);
+hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s);
 // all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s);
