@@ -226,15 +226,15 @@ __device__ __forceinline__ v4d mma_abt(const double* A, const double* Bt, v4d ac
 }
 
 // Factor the 16x16 SPD block D in place with ONE wave (no barriers): D <- L (lower),
-// X <- L^{-1} (lower, zeros above).  Lane l holds row i = l&15, columns 4g..4g+3
-// (g = l>>4).  Right-looking elimination with unscaled pivots; a column, once
-// eliminated, turns into the matching column of E = L'^{-1} (row operations on I):
-//   c > j : T_ic -= T_ij T_cj / piv_j
-//   c == j: E_ij = -T_ij / piv_j (i > j), 1 (i == j)
-//   c < j : E_ic -= (T_ij / piv_j) E_jc
-// L = L' D^{1/2}  ->  L_ij = T_ij / sqrt(piv_j);  X = D^{-1/2} E.
-// The per-step critical path is the shuffles, one Newton reciprocal and one FMA per
-// element (branch-free selects); column scaling by 1/sqrt(piv) is deferred to the end.
+// X <- L^{-1} (lower, zeros above).  Lane l holds the whole row i = l&15 of the symmetric
+// block (the four 16-lane groups hold identical copies), so the pivot row j of step j is
+// one lane's registers: it is broadcast with v_readlane (uniform, no LDS traffic).
+// Right-looking elimination with unscaled pivots; E = L'^{-1} is built by row operations
+// on I alongside (L = L' D^{1/2}, X = D^{-1/2} E):
+//   c > j : T_ic -= (T_ij / piv_j) T_jc       (every lane; the rows i <= j only touch
+//                                              their upper part, which is never read again)
+//   i > j : E_ic -= (T_ij / piv_j) E_jc (c < j),  E_ij = -T_ij / piv_j
+// Column scaling by 1/sqrt(piv) is deferred to the end.
 __device__ __forceinline__ double recip(double p) {
   double r = __builtin_amdgcn_rcp(p);
   double e = __builtin_fma(-p, r, 1.0);
@@ -243,43 +243,52 @@ __device__ __forceinline__ double recip(double p) {
   return __builtin_fma(r, e, r);
 }
 
-__device__ __forceinline__ void factor16(double* D, double* X, double* piv_sh, int l) {
+__device__ __forceinline__ double rdlane(double x, int lane) {
+  const long long bits = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)bits, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ void factor16(double* D, double* X, int l) {
   const int i = l & 15, g = l >> 4;
-  double v[4];
+  double v[NB], e[NB], pv[NB];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = D[bo(i, 4 * g + q)];
+  for (int c = 0; c < NB; ++c) {
+    v[c] = (c <= i) ? D[bo(i, c)] : D[bo(c, i)];   // symmetric row from the lower triangle
+    e[c] = (c == i) ? 1.0 : 0.0;
+  }
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int jg = j >> 2, jq = j & 3;
-    const double ci = __shfl(v[jq], i + 16 * jg);
-    const double piv = __shfl(v[jq], j + 16 * jg);
-    double cc[4], ej[4];
+    const double piv = rdlane(v[j], j);
+    pv[j] = piv;
+    double r[NB], ej[NB];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      cc[q] = __shfl(v[jq], 4 * g + q + 16 * jg);
-      ej[q] = __shfl(v[q], j + 16 * g);
-    }
-    if (g == jg && i >= j) D[bo(i, j)] = ci;   // raw column, scaled after the loop
-    if (l == j) piv_sh[j] = piv;
-    const double li = ci * recip(piv);
+    for (int c = j + 1; c < NB; ++c) r[c] = rdlane(v[c], j);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = 4 * g + q;
-      const bool upd_t = (c > j) && (i >= c);
-      const bool upd_e = (c < j) && (i > j);
-      const bool conv = (c == j) && (i >= j);
-      const double nv = __builtin_fma(-li, upd_t ? cc[q] : ej[q], v[q]);
-      const double cv = (i == j) ? 1.0 : -li;
-      v[q] = (upd_t || upd_e) ? nv : (conv ? cv : v[q]);
-    }
+    for (int c = 0; c < j; ++c) ej[c] = rdlane(e[c], j);
+    const double li = v[j] * recip(piv);
+#pragma unroll
+    for (int c = j + 1; c < NB; ++c) v[c] = __builtin_fma(-li, r[c], v[c]);
+    const bool below = i > j;
+#pragma unroll
+    for (int c = 0; c < j; ++c) e[c] = below ? __builtin_fma(-li, ej[c], e[c]) : e[c];
+    e[j] = below ? -li : e[j];
   }
-  // deferred scaling: L_ij = T_ij / sqrt(piv_j), X_ic = E_ic / sqrt(piv_i)
-  const double rs_own = 1.0 / sqrt(piv_sh[i]);
+  // deferred scaling: L_ic = T_ic / sqrt(piv_c), X_ic = E_ic / sqrt(piv_i)
+  const double rs_own = 1.0 / sqrt(v[i]);   // v[i] = piv_i
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = 4 * g + q;
-    X[bo(i, c)] = (i >= c) ? v[q] * rs_own : 0.0;
-    if (i >= c) D[bo(i, c)] = D[bo(i, c)] * (1.0 / sqrt(piv_sh[c]));
+    double vc = v[0], ec = e[0], pc = pv[0];
+#pragma unroll
+    for (int cc = 1; cc < NB; ++cc) {
+      vc = (c == cc) ? v[cc] : vc;
+      ec = (c == cc) ? e[cc] : ec;
+      pc = (c == cc) ? pv[cc] : pc;
+    }
+    X[bo(i, c)] = (i >= c) ? ec * rs_own : 0.0;
+    if (i >= c) D[bo(i, c)] = vc * (1.0 / sqrt(pc));
   }
 }
 
@@ -493,7 +502,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 
   // C. blocked right-looking factorisation over 16-column panels
   for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
-    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xd + p * BLKD, piv_sh, l);
+    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xd + p * BLKD, l);
     __syncthreads();
     for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += 4) {
       v4d x = {0.0, 0.0, 0.0, 0.0};
