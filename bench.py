@@ -1,10 +1,11 @@
 """Benchmark: GBLUP fitness evals/s on BASELINE config 2 (2000 animals x 50k SNPs,
 panel k = 1000, DE population 256 per GPU), one process per GPU.
 
-A "step" is one generation's fitness evaluation of the population: every
-individual's selected-SNP gather, exact-integer GRM block on int8 MFMA, fp64
-tile Cholesky of (K_TT + lambda I), back substitution, prediction and Pearson
-fitness, plus (N > 1) the RCCL all-gather of the fp64 fitness vector.  Inputs
+A "step" is one generation's fitness evaluation of the population: for every
+individual the exact-integer system tiles on int8 MFMA (SNP-space form at k < n_T,
+as sklearn's Ridge solves it; kernel/GRM form otherwise), the fused fp64 tile
+Cholesky, back substitution, prediction and Pearson fitness, plus (N > 1) the RCCL
+all-gather of the fp64 fitness vector.  Inputs
 (genotypes, split, the population's decoded index sets) are resident in HBM
 before timing starts.  Weak scaling: every rank evaluates its own 256
 individuals.
@@ -29,6 +30,9 @@ CONFIGS = {
     "config1": (200, 1000, 100, 32, 128, 32),
     "config4": (5000, 600_000, 5000, 256, 3200, 800),
 }
+
+# BASELINE.json's metric, verbatim
+METRIC = "GBLUP fitness evals/sec (whole node), 2k\u00d750k SNP, DE pop=256; 1/2/4/8 GPUs"
 
 # gfx950 peaks (MI355X_MICROARCH.md chip table; fp64 and int8 dense from the AMD MI355X spec sheet)
 PEAKS = {
@@ -203,7 +207,7 @@ def main():
                        "elapsed_s": elapsed}, f, indent=1)
     if rank == 0:
         line = {
-            "metric": "GBLUP fitness evals/sec (whole node), 2k x 50k SNP, DE pop=256 per GPU",
+            "metric": METRIC,
             "value": round(value, 2), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

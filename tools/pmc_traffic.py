@@ -10,8 +10,8 @@ import csv
 import json
 from collections import defaultdict
 
-CLASSES = {"k_indiv_stats": "stats", "k_gather": "gather", "k_grm": "grm", "k_chol_diag": "chol_diag",
-           "k_chol_offdiag": "chol_offdiag", "k_solve": "solve"}
+CLASSES = {"k_indiv_stats": "stats", "k_gather": "gather", "k_grm": "grm", "k_diag_grm": "grm",
+           "k_chol_diag": "chol_diag", "k_chol_offdiag": "chol_offdiag", "k_solve": "solve"}
 
 
 def per_class(path, counter):
