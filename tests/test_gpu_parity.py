@@ -277,3 +277,27 @@ def test_config2_forms_agree(config2, monkeypatch):
     for j, i in enumerate(range(0, 256, 32)):
         assert abs(fit[j] - c["fit"][i]) <= FIT_ATOL
         assert _relmax(ebv[j], c["ebv"][i]) <= EBV_RTOL
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config-4 shape (5000 animals, k = 5000 > n_T = 3200: the kernel form at 25
+# tile columns), on a 50k-SNP panel (the 600k-SNP panel only adds HBM, not arithmetic)
+# ---------------------------------------------------------------------------
+def test_config4_shape_sample_vs_oracle(gpu):
+    from tblup_amd.engine import GpuBlupEngine
+    rng = np.random.default_rng(44)
+    n, P = 5000, 50_000
+    geno = O.synth_geno(rng, n, P)
+    pheno = rng.standard_normal(n)
+    perm = np.random.default_rng(45).permutation(n)
+    T, V = perm[:3200], perm[3200:4000]
+    genomes = [np.sort(rng.choice(P, 5000, replace=False)), rng.choice(P, 5000, replace=True),
+               rng.choice(P, 5200, replace=False)]            # snp, snp with duplicates, gblup (k > n)
+    with GpuBlupEngine(geno, pheno) as eng:
+        fit, ebv = eng.evaluate(genomes, T, V, 0.4, return_ebv=True)
+        again = eng.evaluate(genomes[:1], T, V, 0.4)
+    assert again[0] == fit[0]
+    for i, g in enumerate(genomes):
+        f, e = O.blup_grm_form(g, T, V, geno, pheno, 0.4)
+        assert abs(fit[i] - f) <= FIT_ATOL
+        assert _relmax(ebv[i], e) <= EBV_RTOL
