@@ -29,7 +29,9 @@ CONFIGS = {
     "config2": (2000, 50_000, 1000, 256, 1280, 320),
     "config1": (200, 1000, 100, 32, 128, 32),
     "config4": (5000, 600_000, 5000, 256, 3200, 800),
+    "config5": (2000, 50_000, 1000, 256, 1280, 320),   # 3 traits (BASELINE config 5, build-defined)
 }
+TRAITS = {"config5": 3}
 
 # BASELINE.json's metric, verbatim
 METRIC = "GBLUP fitness evals/sec (whole node), 2k\u00d750k SNP, DE pop=256; 1/2/4/8 GPUs"
@@ -59,12 +61,12 @@ def parse():
     return ap.parse_args()
 
 
-def make_workload(cfg, seed, rank, pop):
+def make_workload(cfg, seed, rank, pop, traits=1):
     n, P, k, _, nT, nV = cfg
     rng = np.random.default_rng(seed)
     maf = rng.uniform(0.05, 0.5, size=P)                  # SURVEY.md section 8d synthetic panel
     geno = rng.binomial(2, maf, size=(n, P)).astype(np.int8)
-    pheno = rng.standard_normal(n)
+    pheno = rng.standard_normal(n) if traits == 1 else rng.standard_normal((n, traits))
     perm = np.random.default_rng(seed + 1).permutation(n)
     T, V = perm[:nT], perm[nT:nT + nV]
     keys = np.random.default_rng(seed + 100 + rank).uniform(size=(pop, P))
@@ -84,7 +86,12 @@ def _cpu_init():
 def _cpu_eval(i):
     from oracle.blup_oracle import blup
     d = _CPU
-    return blup(d["genomes"][i % len(d["genomes"])], d["T"], d["V"], d["data"], d["pheno"], d["h2"])
+    y = d["pheno"]
+    g = d["genomes"][i % len(d["genomes"])]
+    if y.ndim == 1:
+        return blup(g, d["T"], d["V"], d["data"], y, d["h2"])
+    # multi-trait: the reference is single-trait, so one eval = one blup per trait
+    return float(np.mean([blup(g, d["T"], d["V"], d["data"], y[:, t], d["h2"]) for t in range(y.shape[1])]))
 
 
 def cpu_baseline(geno, pheno, T, V, genomes, h2, target_s):
@@ -100,7 +107,7 @@ def cpu_baseline(geno, pheno, T, V, genomes, h2, target_s):
     with threadpool_limits(1):
         t0 = time.perf_counter()
         for i in range(2):
-            blup(genomes[i], T, V, _CPU["data"], pheno, h2)
+            _cpu_eval(i)
         per_eval = (time.perf_counter() - t0) / 2
     count = int(max(cores, min(20_000, target_s * cores / max(per_eval, 1e-6))))
     ctx = mp.get_context("fork")
@@ -111,7 +118,9 @@ def cpu_baseline(geno, pheno, T, V, genomes, h2, target_s):
         dt = time.perf_counter() - t0
     _CPU.clear()
     return {"value": count / dt, "unit": "evals/s", "cores": cores, "kind": "port",
-            "sample": f"{count} evaluations of the config workload (k={genomes.shape[1]}) by the numpy oracle "
+            "sample": f"{count} evaluations of the config workload (k={genomes.shape[1]}"
+                      + (f", {pheno.shape[1]} traits: one blup per trait" if pheno.ndim == 2 else "")
+                      + ") by the numpy oracle "
                       f"port of BlupParallelEvaluator.blup, {cores} single-threaded worker processes, {dt:.1f} s"}
 
 
@@ -125,7 +134,8 @@ def main():
     n, P, k, pop_default, nT, nV = cfg
     pop = args.pop or pop_default
 
-    geno, pheno, T, V, genomes = make_workload(cfg, args.seed, rank, pop)
+    traits = TRAITS.get(args.config, 1)
+    geno, pheno, T, V, genomes = make_workload(cfg, args.seed, rank, pop, traits)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(geno, pheno, T, V, genomes, args.h2, args.cpu_seconds)
@@ -214,7 +224,8 @@ def main():
             "dtype": "int8 GRM (exact int32 accumulate) + f64 Cholesky/solve",
             "data": "synthetic (Binomial(2, U(0.05,0.5)) genotypes, N(0,1) phenotype, RandomKey individuals)",
             "config": {"workload": f"{args.config}: {n} animals x {P} SNPs, panel k={k}, pop {pop} per GPU, "
-                                   f"n_train={nT}, n_valid={nV}, h2={args.h2}",
+                                   f"n_train={nT}, n_valid={nV}, h2={args.h2}"
+                                   + (f", {traits} traits (one Cholesky, {traits} RHS)" if traits > 1 else ""),
                        "parallelism": f"population sharded over {world} GPU(s), RCCL fitness all-gather"},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -80,6 +80,21 @@ int tblup_set_split(tblup_ctx* ctx, int split_id, const int64_t* train, int64_t 
 int tblup_drop_split(tblup_ctx* ctx, int split_id);
 
 /*
+ * Multi-trait evaluation (BASELINE config 5; build-defined, the reference is
+ * single-trait): replace the context's phenotypes with an n_animals x n_traits
+ * row-major matrix, 1 <= n_traits <= TBLUP_MAX_TRAITS.  Independent traits with
+ * a shared G decouple (G (x) I + lambda I), so one Cholesky per individual
+ * serves every trait's right-hand side; each trait's EBVs are exactly the
+ * single-trait blup() of that phenotype column (evaluator.py:244-314), and
+ * fitness = mean over traits of |pearson(EBV_V,t, y_V,t)|; ebv outputs become
+ * batch x n_traits x n_valid.  Drops every registered split (they hold
+ * per-trait phenotype vectors): call tblup_set_split again afterwards.
+ */
+#define TBLUP_MAX_TRAITS 4
+int tblup_set_traits(tblup_ctx* ctx, const double* pheno, int64_t n_traits);
+int tblup_get_traits(tblup_ctx* ctx, int64_t* n_traits);
+
+/*
  * Evaluate `batch` individuals (one blup() call each, evaluator.py:244-314).
  *   idx      : concatenated selected SNP column indices (duplicates allowed,
  *              any order), length offsets[batch]
@@ -88,6 +103,7 @@ int tblup_drop_split(tblup_ctx* ctx, int split_id);
  *   branch   : TBLUP_BRANCH_*
  *   fitness  : out, batch doubles, |pearson(EBV_V, y_V)| (NaN when undefined)
  *   ebv      : optional out (may be NULL), batch x n_valid predicted breeding values
+ *              (batch x n_traits x n_valid after tblup_set_traits)
  * Synchronous; host pointers.
  */
 int tblup_eval_batch(tblup_ctx* ctx, int split_id, const int64_t* idx, const int64_t* offsets,

@@ -14,6 +14,7 @@ BRANCH = {"auto": 0, "gblup": 1, "snp": 2}
 LAYOUT_ANIMAL_MAJOR = 0
 LAYOUT_SNP_MAJOR = 1
 N_KCLASS = 6
+MAX_TRAITS = 4
 KCLASS_NAMES = ("stats", "gather", "grm", "chol_diag", "chol_offdiag", "solve")
 
 # Every symbol of include/tblup_gpu.h with (restype, argtypes).
@@ -29,6 +30,8 @@ SIGNATURES = {
     "tblup_ctx_destroy": (_c.c_int, [_P]),
     "tblup_set_split": (_c.c_int, [_P, _c.c_int, _I64P, _c.c_int64, _I64P, _c.c_int64]),
     "tblup_drop_split": (_c.c_int, [_P, _c.c_int]),
+    "tblup_set_traits": (_c.c_int, [_P, _DP, _c.c_int64]),
+    "tblup_get_traits": (_c.c_int, [_P, _I64P]),
     "tblup_eval_batch": (_c.c_int, [_P, _c.c_int, _I64P, _I64P, _c.c_int64, _c.c_double, _c.c_int, _DP, _DP]),
     "tblup_eval_batch_device": (_c.c_int, [_P, _c.c_int, _P, _P, _I64P, _c.c_int64, _c.c_double, _c.c_int, _P, _P,
                                            _P]),

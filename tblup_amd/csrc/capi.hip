@@ -47,8 +47,8 @@ struct DevBuf {
 
 struct Split {
   int64_t nT = 0, nV = 0, nTp = 0, nVp = 0, nRp = 0;
-  double meanyT = 0.0;
-  DevBuf geno, colsumT, xty, yT, yV;
+  std::vector<double> meanyT;   // [nt]
+  DevBuf geno, colsumT, xty, yT, yV, ymu;
 };
 
 enum { KC_STATS = 0, KC_GATHER, KC_GRM, KC_DIAG, KC_OFFDIAG, KC_SOLVE };
@@ -65,7 +65,8 @@ struct tblup_ctx {
   hipStream_t stream = nullptr;
   int64_t n = 0, P = 0;
   DevBuf geno_sm, colsum_all, scratch;
-  std::vector<double> pheno;
+  std::vector<double> pheno;   // [n][nt] animal-major
+  int nt = 1;                  // traits (tblup_set_traits)
   std::map<int, std::unique_ptr<Split>> splits;
   DevBuf ws;
   size_t budget = 0;
@@ -170,13 +171,13 @@ size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_
   add((size_t)B * SCAL * 8);                                    // scal
   add((size_t)B * sd.ns * sd.ns * 8);                           // L (Lt tiles)
   add((size_t)B * sd.NT * TILE * TILE * 8);                     // Dinv
-  add((size_t)B * sd.ns * 8);                                   // z
-  add((size_t)B * sd.ns * 8);                                   // w
-  add((size_t)B * sd.ns * 8);                                   // rhs
+  add((size_t)B * d.nt * sd.ns * 8);                            // z
+  add((size_t)B * d.nt * sd.ns * 8);                            // w
+  add((size_t)B * d.nt * sd.ns * 8);                            // rhs
   add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // next diagonal tile (minus its last SYRK term)
   add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
   add((size_t)B * 8);                                           // fitness
-  add(with_ebv ? (size_t)B * d.nV * 8 : 0);                     // ebv
+  add(with_ebv ? (size_t)B * d.nt * d.nV * 8 : 0);              // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
   return s + 4096;
 }
@@ -198,6 +199,7 @@ EvalDims dims_of(const tblup_ctx* c, const Split& sp) {
   d.nRp = sp.nRp;
   d.NT = (int)(sp.nTp / TILE);
   d.NR = (int)(sp.nRp / TILE);
+  d.nt = c->nt;
   return d;
 }
 
@@ -247,16 +249,16 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* scal = cv.take<double>((size_t)B * SCAL);
   double* L = cv.take<double>((size_t)B * sd.ns * sd.ns);
   double* Dinv = cv.take<double>((size_t)B * sd.NT * TILE * TILE);
-  double* z = cv.take<double>((size_t)B * sd.ns);
-  double* wv = cv.take<double>((size_t)B * sd.ns);
-  double* rhs = cv.take<double>((size_t)B * sd.ns);
+  double* z = cv.take<double>((size_t)B * d.nt * sd.ns);
+  double* wv = cv.take<double>((size_t)B * d.nt * sd.ns);
+  double* rhs = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* Sp = cv.take<double>((size_t)B * TBLUP_NSLOT * 36 * 256);
   double* Kdg = cv.take<double>((size_t)B * sd.NT * 36 * 256);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
   rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
-    return launch_indiv_stats(d_idx, d_off, B, csT, csA, (const double*)sp.xty.p, d, sd, branch, sp.meanyT, h2,
+    return launch_indiv_stats(d_idx, d_off, B, csT, csA, (const double*)sp.xty.p, d, sd, branch, h2,
                               scal, u, rhs, s);
   });
   if (rc) return rc;
@@ -278,7 +280,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
                  [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
   }
   if (K_out) *K_out = L;
-  CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p, panel, pstride, d_off,
+  CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
+                (const double*)sp.ymu.p, panel, pstride, d_off,
                 (const int8_t*)sp.geno.p, d_idx, d.nRp, u, scal,
                 c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0)};
   const double T3 = (double)TILE * TILE * TILE;
@@ -364,6 +367,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->n = n;
   c->P = P;
   c->pheno.assign(pheno, pheno + n);
+  c->nt = 1;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   const char* env = getenv("TBLUP_WORKSPACE_MB");
   c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
@@ -403,6 +407,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
     kv.second->xty.release();
     kv.second->yT.release();
     kv.second->yV.release();
+    kv.second->ymu.release();
   }
   c->geno_sm.release();
   c->colsum_all.release();
@@ -418,7 +423,6 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;
   if (!train || !valid || nT < 1 || nV < 2) return fail(TBLUP_ERR_ARG, "split needs >= 1 train and >= 2 valid rows");
-  std::vector<char> seen_t(c->n, 0);
   for (int64_t i = 0; i < nT; ++i)
     if (train[i] < 0 || train[i] >= c->n) return fail(TBLUP_ERR_ARG, "train index out of range");
   for (int64_t i = 0; i < nV; ++i)
@@ -433,28 +437,35 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   std::vector<int32_t> rowmap(sp->nRp, -1);
   for (int64_t i = 0; i < nT; ++i) rowmap[i] = (int32_t)train[i];
   for (int64_t i = 0; i < nV; ++i) rowmap[sp->nTp + i] = (int32_t)valid[i];
-  std::vector<double> yT(sp->nTp, 0.0), yV(nV);
-  // mean(y_T) as numpy computes it for Ridge's y_offset (pairwise summation differs only in rounding)
-  long double acc = 0.0L;
-  for (int64_t i = 0; i < nT; ++i) {
-    yT[i] = c->pheno[train[i]];
-    acc += yT[i];
+  const int nt = c->nt;
+  std::vector<double> yT((size_t)nt * sp->nTp, 0.0), yV((size_t)nt * nV);
+  sp->meanyT.assign(nt, 0.0);
+  for (int t = 0; t < nt; ++t) {
+    // mean(y_T) as numpy computes it for Ridge's y_offset (pairwise summation differs only in rounding)
+    long double acc = 0.0L;
+    for (int64_t i = 0; i < nT; ++i) {
+      const double y = c->pheno[train[i] * nt + t];
+      yT[t * sp->nTp + i] = y;
+      acc += y;
+    }
+    sp->meanyT[t] = (double)(acc / (long double)nT);
+    for (int64_t i = 0; i < nV; ++i) yV[t * nV + i] = c->pheno[valid[i] * nt + t];
   }
-  sp->meanyT = (double)(acc / (long double)nT);
-  for (int64_t i = 0; i < nV; ++i) yV[i] = c->pheno[valid[i]];
   if (int rc = dev_alloc(c, sp->geno, (size_t)(c->P + 1) * sp->nRp)) return rc;
   if (int rc = dev_alloc(c, sp->colsumT, (size_t)c->P * 4)) return rc;
-  if (int rc = dev_alloc(c, sp->xty, (size_t)c->P * 8)) return rc;
-  if (int rc = dev_alloc(c, sp->yT, (size_t)sp->nTp * 8)) return rc;
-  if (int rc = dev_alloc(c, sp->yV, (size_t)nV * 8)) return rc;
+  if (int rc = dev_alloc(c, sp->xty, (size_t)nt * c->P * 8)) return rc;
+  if (int rc = dev_alloc(c, sp->yT, yT.size() * 8)) return rc;
+  if (int rc = dev_alloc(c, sp->yV, yV.size() * 8)) return rc;
+  if (int rc = dev_alloc(c, sp->ymu, (size_t)nt * 8)) return rc;
   DevBuf rm;
   if (int rc = dev_alloc(c, rm, rowmap.size() * 4)) return rc;
   HIPCHK(hipMemcpyAsync(rm.p, rowmap.data(), rowmap.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(sp->yT.p, yT.data(), yT.size() * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(sp->yV.p, yV.data(), yV.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(sp->ymu.p, sp->meanyT.data(), (size_t)nt * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(launch_build_split((const int8_t*)c->geno_sm.p, c->n, c->P, (const int32_t*)rm.p, sp->nRp, nT,
-                            (const double*)sp->yT.p, sp->meanyT, (int8_t*)sp->geno.p, (int32_t*)sp->colsumT.p,
-                            (double*)sp->xty.p, c->stream));
+                            (const double*)sp->yT.p, (const double*)sp->ymu.p, nt, (int8_t*)sp->geno.p,
+                            (int32_t*)sp->colsumT.p, (double*)sp->xty.p, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   dev_free(c, rm);
   auto it = c->splits.find(split_id);
@@ -464,8 +475,35 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
     dev_free(c, it->second->xty);
     dev_free(c, it->second->yT);
     dev_free(c, it->second->yV);
+    dev_free(c, it->second->ymu);
   }
   c->splits[split_id] = std::move(sp);
+  return 0;
+}
+
+int tblup_set_traits(tblup_ctx* c, const double* pheno, int64_t n_traits) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (!pheno || n_traits < 1 || n_traits > MAXT) return fail(TBLUP_ERR_ARG, "need 1 <= n_traits <= 4 and phenotypes");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (auto& kv : c->splits) {   // splits hold per-trait phenotype vectors
+    dev_free(c, kv.second->geno);
+    dev_free(c, kv.second->colsumT);
+    dev_free(c, kv.second->xty);
+    dev_free(c, kv.second->yT);
+    dev_free(c, kv.second->yV);
+    dev_free(c, kv.second->ymu);
+  }
+  c->splits.clear();
+  c->nt = (int)n_traits;
+  c->pheno.assign(pheno, pheno + c->n * n_traits);
+  return 0;
+}
+
+int tblup_get_traits(tblup_ctx* c, int64_t* n_traits) {
+  if (int rc = check_ctx(c)) return rc;
+  if (n_traits) *n_traits = c->nt;
   return 0;
 }
 
@@ -480,6 +518,7 @@ int tblup_drop_split(tblup_ctx* c, int split_id) {
   dev_free(c, it->second->xty);
   dev_free(c, it->second->yT);
   dev_free(c, it->second->yV);
+  dev_free(c, it->second->ymu);
   c->splits.erase(it);
   return 0;
 }
@@ -530,7 +569,7 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
     int64_t* d_idx = cv.take<int64_t>((size_t)sum_k);
     int64_t* d_off = cv.take<int64_t>((size_t)B + 1);
     double* d_fit = cv.take<double>((size_t)B);
-    double* d_ebv = want_ebv ? cv.take<double>((size_t)B * d.nV) : nullptr;
+    double* d_ebv = want_ebv ? cv.take<double>((size_t)B * d.nt * d.nV) : nullptr;
     std::vector<int64_t> hoff(B + 1);
     for (int64_t b = 0; b <= B; ++b) hoff[b] = offsets[b0 + b] - offsets[b0];
     HIPCHK(hipMemcpyAsync(d_idx, idx + offsets[b0], (size_t)sum_k * 8, hipMemcpyHostToDevice, c->stream));
@@ -540,7 +579,8 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
       return rc;
     HIPCHK(hipMemcpyAsync(fitness + b0, d_fit, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
     if (want_ebv)
-      HIPCHK(hipMemcpyAsync(ebv + b0 * d.nV, d_ebv, (size_t)B * d.nV * 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(ebv + b0 * d.nt * d.nV, d_ebv, (size_t)B * d.nt * d.nV * 8, hipMemcpyDeviceToHost,
+                            c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     b0 = b1;
   }
@@ -654,7 +694,7 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
     }
   }
   if (z_out) {
-    std::vector<double> zz(d.nTp);
+    std::vector<double> zz(d.nTp);   // trait 0
     HIPCHK(hipMemcpy(zz.data(), z, (size_t)d.nTp * 8, hipMemcpyDeviceToHost));
     std::memcpy(z_out, zz.data(), (size_t)d.nT * 8);
   }

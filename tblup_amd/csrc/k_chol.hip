@@ -356,13 +356,13 @@ __device__ __forceinline__ void factor16(double* D, double* X, int l) {
 struct CholArgs {
   double* L;                // Lt tiles [B][NT][NT][128*128]
   double* Dinv;             // [B][NT][128][128]
-  double* z;                // [B][ns]
-  double* w;                // [B][ns] forward-substitution partial sums
+  double* z;                // [B][nt][ns]
+  double* w;                // [B][nt][ns] forward-substitution partial sums
   double* S;                // [B][2][36*256] K_JJ - sum_{L<J-1} L_JL L_JL^T, slot J&1
   double* Kd;               // [B][NT][36*256] GRM diagonal tiles (k_diag_grm)
   int NSX;                  // off-diagonal launch: diagonal-preparation workgroups per individual (0 or 1)
-  const double* yT;         // [nTp] dual right-hand side (y_T - mu, on the fly)
-  const double* rhs;        // [B][ns] primal right-hand side
+  const double* yT;         // [nt][ytp] dual right-hand sides (y_T - mu, on the fly)
+  const double* rhs;        // [B][nt][ns] primal right-hand sides
   const int8_t* panel;      // [B] x pstride
   int64_t pstride;
   const double* u;          // [B][prow]
@@ -374,6 +374,9 @@ struct CholArgs {
   const int64_t* idx;
   const int64_t* off;
   int64_t gs_row, P;
+  const double* ymu;        // [nt] mean(y_T) per trait
+  int64_t ytp;              // yT stride (nTp)
+  int nt;                   // traits (right-hand sides)
   int NT, J;
   int skip;                 // diagnostic ablation mask (TBLUP_DBG_SKIP); 0 in production
 };
@@ -503,15 +506,16 @@ __device__ __forceinline__ void syrk_rows_global(const double* __restrict__ lt, 
 // Diagonal tile J of individual b.  T = S - sum_{L0 <= L < J} L_JL L_JL^T where S is
 // K_JJ - sum_{L < L0} (the buffer slot J&1 left by an earlier off-diagonal launch) when
 // L0 > 0, else k_diag_grm's K_JJ.  lds >= (NPACK + NBLK) * BLKD doubles.
-__device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, int L0, double* lds, double* rsh,
-                                          double* piv_sh) {
+__device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, int L0, double* lds,
+                                          double (*rsh)[TILE]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int64_t ns = a.ns;
   const int NT = a.NT;
   const int64_t j0 = (int64_t)J * TILE;
   const double* sc = a.scal + b * SCAL;
-  const double mu = sc[SC_MU];
+  const double muf = sc[SC_MUF];
   const int64_t nrow = (int64_t)sc[SC_NROW];
+  const int nt = a.nt;
   double* Tp = lds;
   double* Xd = lds + NPACK * BLKD;   // X_pp, p = 0..7
   double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;   // X^T, row-major: XT[c][i] = X[i][c]
@@ -551,9 +555,17 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   }
   if (t < TILE) {
     const int64_t gi = j0 + t;
-    const double wv = (J > 0) ? a.w[b * ns + gi] : 0.0;
-    const double rv = (a.form == FORM_PRIMAL) ? a.rhs[b * ns + gi] : a.yT[gi] - mu;
-    rsh[t] = (gi < nrow) ? (rv - wv) : 0.0;
+#pragma unroll
+    for (int tr = 0; tr < MAXT; ++tr) {
+      if (tr < nt) {
+        const int64_t o = (b * nt + tr) * ns + gi;
+        const double wv = (J > 0) ? a.w[o] : 0.0;
+        const double rv = (a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ymu[tr];
+        rsh[tr][t] = (gi < nrow) ? (rv - wv) : 0.0;
+      } else {
+        rsh[tr][t] = 0.0;
+      }
+    }
   }
   __syncthreads();
 
@@ -631,9 +643,15 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     }
   }
   if (t < TILE) {
-    double acc_z = 0.0;
-    for (int c = 0; c <= t; ++c) acc_z += XT[c * TILE + t] * rsh[c];
-    a.z[b * ns + j0 + t] = acc_z;
+    double acc_z[MAXT] = {0.0, 0.0, 0.0, 0.0};
+    for (int c = 0; c <= t; ++c) {
+      const double xc = XT[c * TILE + t];
+#pragma unroll
+      for (int tr = 0; tr < MAXT; ++tr) acc_z[tr] += xc * rsh[tr][c];
+    }
+#pragma unroll
+    for (int tr = 0; tr < MAXT; ++tr)
+      if (tr < nt) a.z[(b * nt + tr) * ns + j0 + t] = acc_z[tr];
   }
 }
 
@@ -641,9 +659,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 // K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
 __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
   __shared__ __attribute__((aligned(16))) double lds[(NPACK + NBLK) * BLKD];
-  __shared__ double rsh[TILE];
-  __shared__ double piv_sh[NB];
-  diag_tile(a, blockIdx.x, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh, piv_sh);
+  __shared__ double rsh[MAXT][TILE];
+  diag_tile(a, blockIdx.x, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
 }
 
 // ---------------------------------------------------------------------------
@@ -655,7 +672,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
 // LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I, double* lds, double* uj_sh,
-                                             double* ui_sh, double* zj_sh) {
+                                             double* ui_sh, double (*zj_sh)[TILE]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int J = a.J, NT = a.NT;
   const int64_t ns = a.ns;
@@ -667,7 +684,9 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   if (t < TILE) {
     uj_sh[t] = a.u[b * a.prow + j0 + t];
     ui_sh[t] = a.u[b * a.prow + i0 + t];
-    zj_sh[t] = a.z[b * ns + j0 + t];
+#pragma unroll
+    for (int tr = 0; tr < MAXT; ++tr)
+      zj_sh[tr][t] = (tr < a.nt) ? a.z[(b * a.nt + tr) * ns + j0 + t] : 0.0;
   }
   __syncthreads();
 
@@ -724,7 +743,7 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
                                        (lds_ptr_t)(slot + (32 * w + 8 * e) * 16), 16, 0, 0);
     }
   };
-  double wacc[2] = {0.0, 0.0};
+  double wacc[MAXT][2] = {};
   xissue(0);
 #pragma unroll 1
   for (int jb = 0; jb < NBLK; ++jb) {
@@ -752,18 +771,24 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
       for (int r = 0; r < 4; ++r) {
         const int jl = 16 * jb + (l >> 4) + 4 * r, il = 32 * w + 16 * ib + (l & 15);
         Lout[jl * TILE + il] = o[ib][r];
-        wacc[ib] += o[ib][r] * zj_sh[jl];
+#pragma unroll
+        for (int tr = 0; tr < MAXT; ++tr) wacc[tr][ib] += o[ib][r] * zj_sh[tr][jl];
       }
   }
   // w_I[i] += sum_j L_IJ[i][j] z_J[j]: reduce the 4 lane groups that share a column i
 #pragma unroll
-  for (int ib = 0; ib < 2; ++ib) {
-    double v = wacc[ib];
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    if ((l >> 4) == 0) {
-      const int64_t gi = b * ns + i0 + 32 * w + 16 * ib + l;
-      a.w[gi] = (J == 0) ? v : a.w[gi] + v;
+  for (int tr = 0; tr < MAXT; ++tr) {
+    if (tr < a.nt) {
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        double v = wacc[tr][ib];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if ((l >> 4) == 0) {
+          const int64_t gi = (b * a.nt + tr) * ns + i0 + 32 * w + 16 * ib + l;
+          a.w[gi] = (J == 0) ? v : a.w[gi] + v;
+        }
+      }
     }
   }
 }
@@ -774,7 +799,7 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
 // LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
 __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
   __shared__ __attribute__((aligned(16))) double lds[4 * LTS];   // 64 KiB
-  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[TILE];
+  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
   const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
   if ((int64_t)blockIdx.x < n_extra) {
     syrk_partial(a, blockIdx.x, a.J + 1, a.J, lds);
@@ -786,21 +811,21 @@ __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int I0, int
 
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, 0, c.skip};
+             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip};
   hipLaunchKernelGGL(k_diag_grm, dim3((unsigned)(c.B * c.sd.NT)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, J, c.skip};
+             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.sd.NT, J, c.skip};
+             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
   const int I0 = J + 1, nI = c.sd.NT - I0;
   if (nI <= 0) return hipSuccess;
   a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;

@@ -81,8 +81,8 @@ hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ g, int64_t n, int64_t P,
                                                      const int32_t* __restrict__ rowmap, int64_t nRp, int64_t nT,
-                                                     const double* __restrict__ yT, double meanyT,
-                                                     int8_t* __restrict__ out, int32_t* __restrict__ csT,
+                                                     const double* __restrict__ yT, const double* __restrict__ ymu,
+                                                     int nt, int8_t* __restrict__ out, int32_t* __restrict__ csT,
                                                      double* __restrict__ xty) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * 4 + w;
@@ -93,33 +93,39 @@ __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ 
     return;
   }
   const int8_t* row = g + p * n;
+  const int64_t nTp = (nT + TILE - 1) / TILE * TILE;
   int s = 0;
-  double dot = 0.0;
+  double dot[MAXT] = {0.0, 0.0, 0.0, 0.0};
   for (int64_t r = l; r < nRp; r += 64) {
     const int32_t src = rowmap[r];
     const int8_t v = src >= 0 ? row[src] : (int8_t)0;
     orow[r] = v;
     if (r < nT) {
       s += v;
-      dot += (double)v * (yT[r] - meanyT);
+#pragma unroll
+      for (int t = 0; t < MAXT; ++t)
+        if (t < nt) dot[t] += (double)v * (yT[t * nTp + r] - ymu[t]);
     }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_xor(s, o);
-    dot += __shfl_xor(dot, o);
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) dot[t] += __shfl_xor(dot[t], o);
   }
   if (l == 0) {
     csT[p] = s;
-    xty[p] = dot;
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (t < nt) xty[t * P + p] = dot[t];
   }
 }
 
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap, int64_t nRp,
-                              int64_t nT, const double* yT, double meanyT, int8_t* geno_split, int32_t* colsum_T,
-                              double* xty, hipStream_t s) {
+                              int64_t nT, const double* yT, const double* ymu, int nt, int8_t* geno_split,
+                              int32_t* colsum_T, double* xty, hipStream_t s) {
   hipLaunchKernelGGL(k_build_split, dim3((unsigned)((P + 1 + 3) / 4)), dim3(256), 0, s, geno_sm, n, P, rowmap, nRp,
-                     nT, yT, meanyT, geno_split, colsum_T, xty);
+                     nT, yT, ymu, nt, geno_split, colsum_T, xty);
   return hipGetLastError();
 }
 
@@ -132,7 +138,7 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
                                                      const int32_t* __restrict__ csT,
                                                      const int32_t* __restrict__ csA, const double* __restrict__ xty,
                                                      int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
-                                                     int64_t ns, int branch, double meanyT, double h2,
+                                                     int64_t ns, int nt, int branch, double h2,
                                                      double* __restrict__ scal, double* __restrict__ u,
                                                      double* __restrict__ rhs) {
   const int64_t b = blockIdx.x;
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
     sc[SC_SA] = primal ? 0.0 : 1.0 / N;
     sc[SC_CN] = primal ? 0.0 : Q / (N * N);
     sc[SC_INVD] = 1.0 / d;
-    sc[SC_MU] = (mode == 2) ? meanyT : 0.0;
+    sc[SC_MUF] = (mode == 2) ? 1.0 : 0.0;
     sc[SC_LAM] = (1.0 - h2) / h2;
     sc[SC_D] = d;
     sc[SC_MODE] = (double)mode;
@@ -180,23 +186,22 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
   }
   if (!primal) return;
   __syncthreads();
-  // u_a = s_a (train allele count), rhs_a = X_c^T (y_T - mu) / d = xty[p_a] / d
+  // u_a = s_a (train allele count), rhs_ta = X_c^T (y_T,t - mu_t) / d = xty[t][p_a] / d
   // (the sklearn primal right-hand side in 1/d units); zero on padding rows
   const double invd = invd_sh;
   for (int64_t a = threadIdx.x; a < ns; a += 256) {
     const bool real = a < k;
     const int64_t p = real ? clamp_idx(idx[o0 + a], P) : 0;
     u[b * ns + a] = real ? (double)csT[p] : 0.0;
-    rhs[b * ns + a] = real ? xty[p] * invd : 0.0;
+    for (int t = 0; t < nt; ++t) rhs[(b * nt + t) * ns + a] = real ? xty[t * P + p] * invd : 0.0;
   }
 }
 
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
                               const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
-                              int branch, double meanyT, double h2, double* scal, double* u, double* rhs,
-                              hipStream_t s) {
+                              int branch, double h2, double* scal, double* u, double* rhs, hipStream_t s) {
   hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, colsum_T, colsum_all, xty, d.n,
-                     d.nT, d.nTp, d.P, sd.form, sd.ns, branch, meanyT, h2, scal, u, rhs);
+                     d.nT, d.nTp, d.P, sd.form, sd.ns, d.nt, branch, h2, scal, u, rhs);
   return hipGetLastError();
 }
 

@@ -5,7 +5,8 @@
 //                                          gblup: evaluator.py:284 (G[:,T] Ginv y_T, mu = 0)
 //                                          snp:   evaluator.py:314 (clf.predict, intercept mean(y_T))
 //   primal: EBV_V = (X_V - 2p) beta + mean(y_T), beta = alpha (sklearn primal Ridge coef_)
-//   fitness = |pearsonr(EBV_V, y_V)|       evaluator.py:286 / :314, scipy 1.15.3 pearsonr:
+//   fitness = |pearsonr(EBV_V, y_V)|       evaluator.py:286 / :314, scipy 1.15.3 pearsonr
+//            (multi-trait, BASELINE config 5: the mean over traits of |r|; build-defined):
 //            exact-equality constant input -> NaN; mean-centre; max-abs scaled
 //            norms; clip to [-1, 1]; round when n == 2.
 #include "tblup_internal.h"
@@ -16,7 +17,7 @@ namespace {
 
 constexpr int NTH = 1024;
 
-__device__ double block_sum(double v, double* red) {
+__device__ __forceinline__ double block_sum(double v, double* red) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -29,7 +30,7 @@ __device__ double block_sum(double v, double* red) {
   return s;
 }
 
-__device__ double block_max(double v, double* red) {
+__device__ __forceinline__ double block_max(double v, double* red) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -44,154 +45,8 @@ __device__ double block_max(double v, double* red) {
 
 }  // namespace
 
-__global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict__ fit, double* __restrict__ ebv) {
-  extern __shared__ double dyn[];  // alpha[ns] then e[nV]
-  __shared__ double part[NTH / 64][2 * TILE];   // back-substitution partials; reused as [64][64]
-  __shared__ double vsh[TILE];
-  __shared__ double wblk[KBLK];
-  __shared__ double red[NTH / 64];
-  const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, ns = c.sd.ns, prow = c.sd.prow;
-  const double* yV = c.yV;
-  const int NT = c.sd.NT;
-  double* alpha = dyn;
-  double* e = dyn + ns;
+__device__ __forceinline__ double pearson_abs(const double* e, const double* yV, int64_t nV, double* red) {
   const int t = threadIdx.x;
-  const int64_t b = blockIdx.x;
-  const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
-  const double* Db = c.Dinv + b * (int64_t)NT * TILE * TILE;
-  const double* sc = c.scal + b * SCAL;
-  const double invN = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], mu = sc[SC_MU];
-
-  // alpha = L^{-T} z, block rows from the bottom, using the stored diagonal inverses.
-  // (L_JI^T alpha_J)[c] = sum_r Lt_(J,I)[c][r] alpha_J[r]: row c of the transposed tile,
-  // 8 threads per row (16 contiguous r each), reduced with lane shuffles.
-  const int rc = t >> 3, seg = t & 7;
-  for (int I = NT - 1; I >= 0; --I) {
-    double s = 0.0;
-    for (int J = I + 1; J < NT; ++J) {
-      const double* row = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 16 * seg;
-      const double* al = alpha + J * TILE + 16 * seg;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const v2d x = *reinterpret_cast<const v2d*>(row + 2 * e);
-        s += x[0] * al[2 * e] + x[1] * al[2 * e + 1];
-      }
-    }
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 4);
-    if (seg == 0) vsh[rc] = c.z[b * ns + (int64_t)I * TILE + rc] - s;
-    __syncthreads();
-    // alpha_I = X_I^T v: Dinv holds X^T, so again row c dotted with v
-    // (blocks with seg < rc/16 are zero in X^T and are never stored)
-    const double* xrow = Db + (int64_t)I * TILE * TILE + rc * TILE + 16 * seg;
-    double s2 = 0.0;
-    if (seg >= (rc >> 4)) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const v2d x = *reinterpret_cast<const v2d*>(xrow + 2 * e);
-        s2 += x[0] * vsh[16 * seg + 2 * e] + x[1] * vsh[16 * seg + 2 * e + 1];
-      }
-    }
-    s2 += __shfl_xor(s2, 1);
-    s2 += __shfl_xor(s2, 2);
-    s2 += __shfl_xor(s2, 4);
-    if (seg == 0) alpha[I * TILE + rc] = s2;
-    __syncthreads();
-  }
-
-  const double* ub = c.u + b * prow;
-  const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
-  const int dq = t & 15, rg = t >> 4;   // dword (4 bytes) within a 64-wide block row, row group (64)
-  double* pw = &part[0][0];             // [64 row groups][64]
-  if (c.sd.form == FORM_PRIMAL) {
-    // EBV_v = sum_a x_va beta_a - sum_a (s_a / n_T) beta_a + mu, reduced over a by row groups
-    const int64_t kk = (int64_t)sc[SC_K];
-    double s_ub = 0.0;
-    for (int64_t r = t; r < kk; r += NTH) s_ub += ub[r] * alpha[r];
-    const double MB = block_sum(s_ub, red) * sc[SC_SM];
-    // X_V read in place from the split's SNP-major rows (V animals start at byte nTp)
-    const int64_t o0 = c.off[b];
-    const int64_t nvb = (nV + KBLK - 1) / KBLK;
-    for (int64_t vb = 0; vb < nvb; ++vb) {
-      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-      for (int64_t r = rg; r < kk; r += NTH / 16) {
-        int64_t p = c.idx[o0 + r];
-        p = p < 0 ? 0 : (p >= c.d.P ? c.d.P - 1 : p);
-        const uint32_t x = reinterpret_cast<const uint32_t*>(c.gs + p * c.gs_row + nTp + vb * KBLK)[dq];
-        const double ar = alpha[r];
-        p0 += (double)(x & 0xff) * ar;
-        p1 += (double)((x >> 8) & 0xff) * ar;
-        p2 += (double)((x >> 16) & 0xff) * ar;
-        p3 += (double)(x >> 24) * ar;
-      }
-      __syncthreads();
-      pw[rg * KBLK + 4 * dq + 0] = p0;
-      pw[rg * KBLK + 4 * dq + 1] = p1;
-      pw[rg * KBLK + 4 * dq + 2] = p2;
-      pw[rg * KBLK + 4 * dq + 3] = p3;
-      __syncthreads();
-      if (t < KBLK && vb * KBLK + t < nV) {
-        double acc = 0.0;
-        for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
-        e[vb * KBLK + t] = acc - MB + mu;
-      }
-    }
-    __syncthreads();
-  } else {
-    // EBV_V = K_VT alpha + mu without materialising K_VT (exact-integer factored form):
-    //   sum_t K_vt alpha_t = [sum_s a_vs w_s - u_v S/N - (u_T . alpha)/N + cN S] / d,
-    //   w_s = sum_t a_ts alpha_t,  S = sum_t alpha_t
-    double s_a = 0.0, s_ua = 0.0;
-    for (int64_t r = t; r < nT; r += NTH) {
-      s_a += alpha[r];
-      s_ua += ub[r] * alpha[r];
-    }
-    const double S = block_sum(s_a, red);
-    const double UA = block_sum(s_ua, red);
-    for (int64_t v = t; v < nV; v += NTH) e[v] = 0.0;
-    const int64_t nblk = (int64_t)sc[SC_CBLK];
-    for (int64_t kb = 0; kb < nblk; ++kb) {
-      const uint32_t* blk = pb + kb * prow * (KBLK / 4);
-      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-      for (int64_t r = rg; r < nT; r += NTH / 16) {
-        const uint32_t x = blk[r * (KBLK / 4) + dq];
-        const double ar = alpha[r];
-        p0 += (double)(x & 0xff) * ar;
-        p1 += (double)((x >> 8) & 0xff) * ar;
-        p2 += (double)((x >> 16) & 0xff) * ar;
-        p3 += (double)(x >> 24) * ar;
-      }
-      __syncthreads();
-      pw[rg * KBLK + 4 * dq + 0] = p0;
-      pw[rg * KBLK + 4 * dq + 1] = p1;
-      pw[rg * KBLK + 4 * dq + 2] = p2;
-      pw[rg * KBLK + 4 * dq + 3] = p3;
-      __syncthreads();
-      if (t < KBLK) {
-        double acc = 0.0;
-        for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
-        wblk[t] = acc;
-      }
-      __syncthreads();
-      for (int64_t v = t; v < nV; v += NTH) {
-        const uint32_t* row = blk + (nTp + v) * (KBLK / 4);
-        double acc = 0.0;
-#pragma unroll 4
-        for (int d4 = 0; d4 < KBLK / 4; ++d4) {
-          const uint32_t x = row[d4];
-          acc += (double)(x & 0xff) * wblk[4 * d4] + (double)((x >> 8) & 0xff) * wblk[4 * d4 + 1] +
-                 (double)((x >> 16) & 0xff) * wblk[4 * d4 + 2] + (double)(x >> 24) * wblk[4 * d4 + 3];
-        }
-        e[v] += acc;
-      }
-    }
-    __syncthreads();
-    for (int64_t v = t; v < nV; v += NTH) e[v] = (e[v] - ub[nTp + v] * S * invN - UA * invN + cN * S) * invd + mu;
-    __syncthreads();
-  }
-
-  // Pearson correlation (scipy.stats.pearsonr restated), fitness = |r|
   const double yb = yV[0], eb = e[0];
   double sx = 0.0, sy = 0.0, ncx = 0.0, ncy = 0.0;
   for (int64_t v = t; v < nV; v += NTH) {
@@ -222,25 +77,202 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   double rr = 0.0;
   for (int64_t v = t; v < nV; v += NTH) rr += ((e[v] - mx) / nx) * ((yV[v] - my) / ny);
   double r = block_sum(rr, red);
-  if (t == 0) {
-    if (r == r) r = fmin(fmax(r, -1.0), 1.0);  // np.clip keeps NaN (fmin/fmax would drop it)
-    if (nonconst_x == 0.0 || nonconst_y == 0.0) r = __builtin_nan("");
-    if (nV == 2) r = rint(r);
-    fit[b] = fabs(r);
+  if (r == r) r = fmin(fmax(r, -1.0), 1.0);  // np.clip keeps NaN (fmin/fmax would drop it)
+  if (nonconst_x == 0.0 || nonconst_y == 0.0) r = __builtin_nan("");
+  if (nV == 2) r = rint(r);
+  return fabs(r);
+}
+
+template <int NTR>
+__global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict__ fit, double* __restrict__ ebv) {
+  extern __shared__ double dyn[];  // alpha[nt][ns] then e[nt][nV]
+  __shared__ double part[NTH / 64][2 * TILE];   // reused as [64][64]
+  __shared__ double vsh[MAXT][TILE];
+  __shared__ double wblk[KBLK];
+  __shared__ double red[NTH / 64];
+  const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, ns = c.sd.ns, prow = c.sd.prow;
+  const int NT = c.sd.NT;
+  constexpr int nt = NTR;
+  double* alpha = dyn;
+  double* eall = dyn + nt * ns;
+  const int t = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
+  const double* Db = c.Dinv + b * (int64_t)NT * TILE * TILE;
+  const double* sc = c.scal + b * SCAL;
+  const double invN = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], muf = sc[SC_MUF];
+
+  // alpha = L^{-T} z for every trait in one pass over L, block rows from the bottom, using
+  // the stored diagonal inverses.  (L_JI^T alpha_J)[c] = sum_r Lt_(J,I)[c][r] alpha_J[r]:
+  // row c of the transposed tile, 8 threads per row (16 contiguous r each), lane shuffles.
+  const int rc = t >> 3, seg = t & 7;
+  for (int I = NT - 1; I >= 0; --I) {
+    double s[NTR] = {};
+    for (int J = I + 1; J < NT; ++J) {
+      const double* row = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 16 * seg;
+      constexpr int EU = NTR > 1 ? 2 : 8;
+#pragma unroll EU
+      for (int e = 0; e < 8; ++e) {
+        const v2d x = *reinterpret_cast<const v2d*>(row + 2 * e);
+#pragma unroll
+        for (int tr = 0; tr < NTR; ++tr) {
+          const double* al = alpha + tr * ns + J * TILE + 16 * seg;
+          s[tr] += x[0] * al[2 * e] + x[1] * al[2 * e + 1];
+        }
+      }
+    }
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr) {
+      s[tr] += __shfl_xor(s[tr], 1);
+      s[tr] += __shfl_xor(s[tr], 2);
+      s[tr] += __shfl_xor(s[tr], 4);
+      if (seg == 0) vsh[tr][rc] = c.z[(b * nt + tr) * ns + (int64_t)I * TILE + rc] - s[tr];
+    }
+    __syncthreads();
+    // alpha_I = X_I^T v: Dinv holds X^T, so again row c dotted with v
+    // (blocks with seg < rc/16 are zero in X^T and are never stored)
+    const double* xrow = Db + (int64_t)I * TILE * TILE + rc * TILE + 16 * seg;
+    double s2[NTR] = {};
+    if (seg >= (rc >> 4)) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const v2d x = *reinterpret_cast<const v2d*>(xrow + 2 * e);
+#pragma unroll
+        for (int tr = 0; tr < NTR; ++tr) s2[tr] += x[0] * vsh[tr][16 * seg + 2 * e] + x[1] * vsh[tr][16 * seg + 2 * e + 1];
+      }
+    }
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr) {
+      s2[tr] += __shfl_xor(s2[tr], 1);
+      s2[tr] += __shfl_xor(s2[tr], 2);
+      s2[tr] += __shfl_xor(s2[tr], 4);
+      if (seg == 0) alpha[tr * ns + I * TILE + rc] = s2[tr];
+    }
+    __syncthreads();
   }
-  if (ebv != nullptr) {
-    for (int64_t v = t; v < nV; v += NTH) ebv[b * nV + v] = e[v];
+
+  const double* ub = c.u + b * prow;
+  const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
+  const int dq = t & 15, rg = t >> 4;   // dword (4 bytes) within a 64-wide block row, row group (64)
+  double* pw = &part[0][0];             // [64 row groups][64]
+  double fsum = 0.0;
+  for (int tr = 0; tr < nt; ++tr) {
+    const double* al = alpha + tr * ns;
+    double* e = eall + tr * nV;
+    const double* yV = c.yV + tr * nV;
+    const double mu = muf * c.ymu[tr];
+    if (c.sd.form == FORM_PRIMAL) {
+      // EBV_v = sum_a x_va beta_a - sum_a (s_a / n_T) beta_a + mu, reduced over a by row groups
+      const int64_t kk = (int64_t)sc[SC_K];
+      double s_ub = 0.0;
+      for (int64_t r = t; r < kk; r += NTH) s_ub += ub[r] * al[r];
+      const double MB = block_sum(s_ub, red) * sc[SC_SM];
+      // X_V read in place from the split's SNP-major rows (V animals start at byte nTp)
+      const int64_t o0 = c.off[b];
+      const int64_t nvb = (nV + KBLK - 1) / KBLK;
+      for (int64_t vb = 0; vb < nvb; ++vb) {
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+        for (int64_t r = rg; r < kk; r += NTH / 16) {
+          int64_t p = c.idx[o0 + r];
+          p = p < 0 ? 0 : (p >= c.d.P ? c.d.P - 1 : p);
+          const uint32_t x = reinterpret_cast<const uint32_t*>(c.gs + p * c.gs_row + nTp + vb * KBLK)[dq];
+          const double ar = al[r];
+          p0 += (double)(x & 0xff) * ar;
+          p1 += (double)((x >> 8) & 0xff) * ar;
+          p2 += (double)((x >> 16) & 0xff) * ar;
+          p3 += (double)(x >> 24) * ar;
+        }
+        __syncthreads();
+        pw[rg * KBLK + 4 * dq + 0] = p0;
+        pw[rg * KBLK + 4 * dq + 1] = p1;
+        pw[rg * KBLK + 4 * dq + 2] = p2;
+        pw[rg * KBLK + 4 * dq + 3] = p3;
+        __syncthreads();
+        if (t < KBLK && vb * KBLK + t < nV) {
+          double acc = 0.0;
+          for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
+          e[vb * KBLK + t] = acc - MB + mu;
+        }
+      }
+      __syncthreads();
+    } else {
+      // EBV_V = K_VT alpha + mu without materialising K_VT (exact-integer factored form):
+      //   sum_t K_vt alpha_t = [sum_s a_vs w_s - u_v S/N - (u_T . alpha)/N + cN S] / d,
+      //   w_s = sum_t a_ts alpha_t,  S = sum_t alpha_t
+      double s_a = 0.0, s_ua = 0.0;
+      for (int64_t r = t; r < nT; r += NTH) {
+        s_a += al[r];
+        s_ua += ub[r] * al[r];
+      }
+      const double S = block_sum(s_a, red);
+      const double UA = block_sum(s_ua, red);
+      for (int64_t v = t; v < nV; v += NTH) e[v] = 0.0;
+      const int64_t nblk = (int64_t)sc[SC_CBLK];
+      for (int64_t kb = 0; kb < nblk; ++kb) {
+        const uint32_t* blk = pb + kb * prow * (KBLK / 4);
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+        for (int64_t r = rg; r < nT; r += NTH / 16) {
+          const uint32_t x = blk[r * (KBLK / 4) + dq];
+          const double ar = al[r];
+          p0 += (double)(x & 0xff) * ar;
+          p1 += (double)((x >> 8) & 0xff) * ar;
+          p2 += (double)((x >> 16) & 0xff) * ar;
+          p3 += (double)(x >> 24) * ar;
+        }
+        __syncthreads();
+        pw[rg * KBLK + 4 * dq + 0] = p0;
+        pw[rg * KBLK + 4 * dq + 1] = p1;
+        pw[rg * KBLK + 4 * dq + 2] = p2;
+        pw[rg * KBLK + 4 * dq + 3] = p3;
+        __syncthreads();
+        if (t < KBLK) {
+          double acc = 0.0;
+          for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
+          wblk[t] = acc;
+        }
+        __syncthreads();
+        for (int64_t v = t; v < nV; v += NTH) {
+          const uint32_t* row = blk + (nTp + v) * (KBLK / 4);
+          double acc = 0.0;
+#pragma unroll 4
+          for (int d4 = 0; d4 < KBLK / 4; ++d4) {
+            const uint32_t x = row[d4];
+            acc += (double)(x & 0xff) * wblk[4 * d4] + (double)((x >> 8) & 0xff) * wblk[4 * d4 + 1] +
+                   (double)((x >> 16) & 0xff) * wblk[4 * d4 + 2] + (double)(x >> 24) * wblk[4 * d4 + 3];
+          }
+          e[v] += acc;
+        }
+      }
+      __syncthreads();
+      for (int64_t v = t; v < nV; v += NTH) e[v] = (e[v] - ub[nTp + v] * S * invN - UA * invN + cN * S) * invd + mu;
+      __syncthreads();
+    }
+    // Pearson correlation (scipy.stats.pearsonr restated); multi-trait fitness is the mean |r|
+    fsum += pearson_abs(e, yV, nV, red);
+    if (ebv != nullptr) {
+      for (int64_t v = t; v < nV; v += NTH) ebv[(b * nt + tr) * nV + v] = e[v];
+    }
   }
+  if (t == 0) fit[b] = (nt == 1) ? fsum : fsum / (double)nt;
 }
 
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s) {
-  const size_t shm = (size_t)(c.sd.ns + c.d.nV) * sizeof(double);
-  if (shm > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    if (e != hipSuccess) return e;
+  const size_t shm = (size_t)c.d.nt * (size_t)(c.sd.ns + c.d.nV) * sizeof(double);
+  auto launch = [&](const void* fn, auto kernel) -> hipError_t {
+    if (shm > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kernel, dim3((unsigned)c.B), dim3(NTH), shm, s, c, fitness, ebv);
+    return hipGetLastError();
+  };
+  switch (c.d.nt) {
+    case 1: return launch((const void*)k_solve<1>, k_solve<1>);
+    case 2: return launch((const void*)k_solve<2>, k_solve<2>);
+    case 3: return launch((const void*)k_solve<3>, k_solve<3>);
+    case 4: return launch((const void*)k_solve<4>, k_solve<4>);
+    default: return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(k_solve, dim3((unsigned)c.B), dim3(NTH), shm, s, c, fitness, ebv);
-  return hipGetLastError();
 }
 
 }  // namespace tblup

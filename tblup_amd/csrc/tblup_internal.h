@@ -7,7 +7,7 @@
 //     geno      int8 [P+1][nRp]   SNP-major rows permuted to [T | 0-pad | V | 0-pad], nRp = nTp+nVp;
 //                                 row P is all zero (padding rows of the primal form)
 //     colsum_T  int32 [P]         allele counts over T (snp p)
-//     xty       f64  [P]          sum_t x_tp (y_t - mean y_T): the primal right-hand side, per SNP
+//     xty       f64  [nt][P]      sum_t x_tp (y_t - mean y_T): the primal right-hand side, per SNP and trait
 //     yT        f64 [nTp]         phenotypes of T (0 in padding), yV f64 [nV]
 //   per evaluation chunk of B individuals (workspace):
 //   Two equivalent forms of the per-individual system (chosen per chunk, see SysDims):
@@ -32,6 +32,7 @@ namespace tblup {
 constexpr int TILE = 128;      // output tile edge of the GRM and Cholesky kernels
 constexpr int TBLUP_NSLOT = 2; // diagonal-tile preparation buffers per individual (slot J&1)
 constexpr int KBLK = 64;       // SNPs per panel block (int8 MFMA K step)
+constexpr int MAXT = 4;        // traits per context (multi-trait: one Cholesky, MAXT right-hand sides)
 constexpr int GATHER_ROWS = 128;
 
 // per-individual scalars scal[b][SCAL]
@@ -40,7 +41,7 @@ enum {
   SC_SA = 0,    // additive centring coefficient (dual 1/N, primal 0)
   SC_CN = 1,    // constant centring term (dual q/N^2, primal 0)
   SC_INVD = 2,  // 1/d
-  SC_MU = 3,    // intercept (snp: mean y_T, gblup: 0)
+  SC_MUF = 3,   // intercept flag: 1 = snp branch (intercept mean(y_T) of each trait), 0 = gblup
   SC_LAM = 4,   // lambda = (1-h2)/h2
   SC_D = 5,     // d = 2 sum p(1-p)
   SC_MODE = 6,  // branch: 1 gblup, 2 snp
@@ -74,19 +75,19 @@ struct EvalDims {
   int64_t nRp;      // nTp + nVp
   int NT;           // nTp / TILE
   int NR;           // nRp / TILE
+  int nt;           // traits
 };
 
 // ---- launchers (k_prep.hip) ----
 hipError_t launch_transpose_geno(const int8_t* src, int8_t* dst, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap,
-                              int64_t nRp, int64_t nT, const double* yT, double meanyT, int8_t* geno_split,
-                              int32_t* colsum_T, double* xty, hipStream_t s);
-// primal form (sd.form): also u[b][a] = s_a and rhs[b][a] = xty[p_a] / d over the ns rows
+                              int64_t nRp, int64_t nT, const double* yT, const double* ymu, int nt,
+                              int8_t* geno_split, int32_t* colsum_T, double* xty, hipStream_t s);
+// primal form (sd.form): also u[b][a] = s_a and rhs[b][t][a] = xty[t][p_a] / d over the ns rows
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
                               const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
-                              int branch, double meanyT, double h2, double* scal, double* u, double* rhs,
-                              hipStream_t s);
+                              int branch, double h2, double* scal, double* u, double* rhs, hipStream_t s);
 hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int64_t* off,
                          int64_t panel_stride, int64_t B, const int32_t* colsum_T,
                          const int32_t* colsum_all, const double* scal, const EvalDims& d,
@@ -103,13 +104,14 @@ struct CholLaunch {
   int64_t B;
   double* L;             // Lt tiles [B][NT][NT][128*128] (tile (I,J) holds L_IJ^T)
   double* Dinv;          // [B][NT][128][128]
-  double* z;             // [B][ns]
-  double* w;             // [B][ns] forward-substitution partial sums
-  const double* rhs;     // [B][ns] primal right-hand side (dual: y_T - mu on the fly)
+  double* z;             // [B][nt][ns]
+  double* w;             // [B][nt][ns] forward-substitution partial sums
+  const double* rhs;     // [B][nt][ns] primal right-hand sides (dual: y_T - mu on the fly)
   double* S;             // [B][2][36*256] diagonal-tile preparation, slot J&1
   double* Kd;            // [B][NT][36*256] GRM diagonal tiles
-  const double* yT;      // split phenotypes [nTp]
-  const double* yV;      // [nV]
+  const double* yT;      // split phenotypes [nt][nTp]
+  const double* yV;      // [nt][nV]
+  const double* ymu;     // [nt] mean(y_T) per trait
   const int8_t* panel;   // gathered genotypes
   int64_t pstride;       // panel bytes per individual
   const int64_t* off;    // [B+1] device offsets

@@ -62,9 +62,17 @@ class GpuBlupEngine:
     MAX_SPLITS = 16
 
     def __init__(self, data, labels, device=0, snp_major=False):
+        """labels: (n,) phenotypes, or (n, t) for multi-trait evaluation (t <= 4, BASELINE
+        config 5): one Cholesky per individual serves every trait, fitness = mean |r|."""
         self._lib = _native.load()
         geno = validate_genotypes(data)
-        pheno = np.ascontiguousarray(np.asarray(labels, dtype=np.float64).ravel())
+        labels = np.asarray(labels, dtype=np.float64)
+        if labels.ndim == 2 and labels.shape[1] == 1:
+            labels = labels[:, 0]
+        if labels.ndim not in (1, 2) or (labels.ndim == 2 and not 1 <= labels.shape[1] <= _native.MAX_TRAITS):
+            raise ValueError(f"phenotypes must be (n,) or (n, t) with t <= {_native.MAX_TRAITS}")
+        self.n_traits = 1 if labels.ndim == 1 else labels.shape[1]
+        pheno = np.ascontiguousarray(labels[:, 0] if labels.ndim == 2 else labels)
         if snp_major:
             n_snps, n = geno.shape
             layout = _native.LAYOUT_SNP_MAJOR
@@ -79,6 +87,10 @@ class GpuBlupEngine:
             geno.ctypes.data_as(ctypes.c_void_p), n, n_snps, layout, _ptr(pheno, ctypes.c_double), self.device,
             ctypes.byref(ctx)))
         self._ctx = ctx
+        if self.n_traits > 1:
+            mt = np.ascontiguousarray(labels)
+            _native.check("tblup_set_traits", self._lib.tblup_set_traits(
+                self._ctx, _ptr(mt, ctypes.c_double), self.n_traits))
         self._splits = OrderedDict()   # key -> (split_id, n_valid)
         self._next_split = 0
 
@@ -103,13 +115,15 @@ class GpuBlupEngine:
 
     # -------------------------------------------------------------- evaluation
     def evaluate(self, genomes, train, valid, h2, branch="auto", return_ebv=False):
-        """Fitness |pearson(EBV_V, y_V)| for each selected-index set (evaluator.py:244-314)."""
+        """Fitness |pearson(EBV_V, y_V)| for each selected-index set (evaluator.py:244-314);
+        multi-trait: the mean over traits, EBVs (B, t, n_valid)."""
         sid = self.split_id(train, valid)
         idx, offsets = concat_genomes(genomes)
         B = len(genomes)
         fit = np.empty(B, dtype=np.float64)
         n_valid = len(valid)
-        ebv = np.empty((B, n_valid), dtype=np.float64) if return_ebv else None
+        shape = (B, n_valid) if self.n_traits == 1 else (B, self.n_traits, n_valid)
+        ebv = np.empty(shape, dtype=np.float64) if return_ebv else None
         if B:
             _native.check("tblup_eval_batch", self._lib.tblup_eval_batch(
                 self._ctx, sid, _ptr(idx, ctypes.c_int64), _ptr(offsets, ctypes.c_int64), B, float(h2),

@@ -301,3 +301,53 @@ def test_config4_shape_sample_vs_oracle(gpu):
         f, e = O.blup_grm_form(g, T, V, geno, pheno, 0.4)
         assert abs(fit[i] - f) <= FIT_ATOL
         assert _relmax(ebv[i], e) <= EBV_RTOL
+
+
+# ---------------------------------------------------------------------------
+# Multi-trait (BASELINE config 5, build-defined): traits share K, one Cholesky, t RHS.
+# Each trait's EBVs must equal that phenotype's single-trait evaluation (the reference's
+# blup() per column); fitness = mean over traits of |r|.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("form", ["0", "1", "2"])
+def test_multitrait_equals_single_traits(golden_dir, gpu, monkeypatch, form):
+    from tblup_amd.engine import GpuBlupEngine
+    z = _load(golden_dir, "blup_200x1000.npz")
+    monkeypatch.setenv("TBLUP_FORM", form)
+    rng = np.random.default_rng(7)
+    Y = np.stack([z["pheno"], rng.standard_normal(200), 0.5 * z["pheno"] + rng.standard_normal(200)], axis=1)
+    genomes = [idx for _, idx in _cases(z)] if form != "2" else [c[2] for c in _snp_cases(z)]
+    with GpuBlupEngine(z["geno"], Y) as eng:
+        fit, ebv = eng.evaluate(genomes, z["T"], z["V"], 0.4, return_ebv=True)
+    assert ebv.shape == (len(genomes), 3, len(z["V"]))
+    singles = []
+    for tr in range(3):
+        with GpuBlupEngine(z["geno"], Y[:, tr]) as eng:
+            singles.append(eng.evaluate(genomes, z["T"], z["V"], 0.4, return_ebv=True))
+    for i, g in enumerate(genomes):
+        fs = []
+        for tr in range(3):
+            np.testing.assert_array_equal(ebv[i, tr], singles[tr][1][i])
+            fs.append(singles[tr][0][i])
+            f, e = O.blup_grm_form(g, z["T"], z["V"], z["geno"], Y[:, tr], 0.4)
+            assert _relmax(ebv[i, tr], e) <= EBV_RTOL
+        assert abs(fit[i] - np.mean(fs)) <= 1e-15
+
+
+def test_multitrait_config5_sample(config2):
+    """Config 5 shape: 2000 x 50k, k = 1000 (SNP-space form), 3 traits."""
+    from tblup_amd.engine import GpuBlupEngine
+    c = config2
+    rng = np.random.default_rng(55)
+    Y = np.stack([c["pheno"], rng.standard_normal(2000), rng.standard_normal(2000)], axis=1)
+    sel = [c["genomes"][i] for i in (0, 100, 255)]
+    with GpuBlupEngine(c["geno"], Y) as eng:
+        fit, ebv = eng.evaluate(sel, c["T"], c["V"], 0.4, return_ebv=True)
+    for j, g in enumerate(sel):
+        fs = []
+        for tr in range(3):
+            f, e = O.blup_grm_form(g, c["T"], c["V"], c["geno"], Y[:, tr], 0.4)
+            assert _relmax(ebv[j, tr], e) <= EBV_RTOL
+            fs.append(f)
+        assert abs(fit[j] - np.mean(fs)) <= FIT_ATOL
+    # trait 0 is the single-trait phenotype of the fixture
+    np.testing.assert_array_equal(ebv[:, 0], c["ebv"][[0, 100, 255]])
