@@ -124,6 +124,28 @@ int tblup_eval_batch_device(tblup_ctx* ctx, int split_id, const int64_t* d_idx,
                             double h2, int branch, double* d_fitness, double* d_ebv, void* stream);
 
 /*
+ * RandomKeyIndividual / CoevolutionIndividual genome decode
+ * (tblup/individual.py:154-156, `np.argsort(keys)[-int(length):]`): for each of
+ * `batch` key rows of length d, the indices of its k_b = offsets[b+1]-offsets[b]
+ * largest keys in ascending key order, written to idx_out[offsets[b] ...] — the
+ * (idx, offsets) pair tblup_eval_batch takes.  Equal keys are ordered by index (a
+ * stable argsort), so a tie straddling the k-th position selects its largest
+ * indices; with continuous keys this is the set numpy's default sort returns.
+ * 1 <= k_b <= min(d, 8192).  Host pointers, synchronous.
+ */
+int tblup_decode_topk(tblup_ctx* ctx, const double* keys, int64_t batch, int64_t d, const int64_t* offsets,
+                      int64_t* idx_out);
+
+/*
+ * Same on device-resident keys (row stride ld >= d doubles), offsets and output,
+ * enqueued on `stream` (NULL = the context's stream); h_offsets is the host copy
+ * (validation).  The output feeds tblup_eval_batch_device directly.
+ */
+int tblup_decode_topk_device(tblup_ctx* ctx, const double* d_keys, int64_t batch, int64_t d, int64_t ld,
+                             const int64_t* d_offsets, const int64_t* h_offsets, int64_t* d_idx_out,
+                             void* stream);
+
+/*
  * Per-kernel-class timing with HIP events on the launch stream.
  * tblup_set_profiling(ctx, 1) enables recording; tblup_get_profile returns
  * accumulated milliseconds, launch counts and algorithmic flops per class

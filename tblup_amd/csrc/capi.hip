@@ -69,6 +69,7 @@ struct tblup_ctx {
   int nt = 1;                  // traits (tblup_set_traits)
   std::map<int, std::unique_ptr<Split>> splits;
   DevBuf ws;
+  DevBuf dec_keys, dec_idx;   // host-pointer decode staging
   size_t budget = 0;
   // profiling
   bool profiling = false;
@@ -413,6 +414,8 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->colsum_all.release();
   c->scratch.release();
   c->ws.release();
+  c->dec_keys.release();
+  c->dec_idx.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -613,6 +616,52 @@ int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, co
   Carve cv{(char*)c->ws.p};
   return run_chunk(c, *sp, d, sd, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness, d_ebv, 0,
                    nullptr, nullptr);
+}
+
+static int validate_decode(int64_t batch, int64_t d, const int64_t* offsets) {
+  if (batch < 0 || d < 1 || d > 0x7fffffff) return fail(TBLUP_ERR_ARG, "decode needs batch >= 0, 1 <= d < 2^31");
+  if (batch > 0 && (!offsets || offsets[0] != 0)) return fail(TBLUP_ERR_ARG, "offsets must start at 0");
+  for (int64_t b = 0; b < batch; ++b) {
+    const int64_t k = offsets[b + 1] - offsets[b];
+    if (k < 1 || k > d || k > 8192) return fail(TBLUP_ERR_ARG, "every k must be in [1, min(d, 8192)]");
+  }
+  return 0;
+}
+
+int tblup_decode_topk_device(tblup_ctx* c, const double* d_keys, int64_t batch, int64_t d, int64_t ld,
+                             const int64_t* d_offsets, const int64_t* h_offsets, int64_t* d_idx_out, void* stream) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_decode(batch, d, h_offsets)) return rc;
+  if (ld < d) return fail(TBLUP_ERR_ARG, "ld < d");
+  if (batch == 0) return 0;
+  if (!d_keys || !d_offsets || !d_idx_out) return fail(TBLUP_ERR_ARG, "null device pointers");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  HIPCHK(launch_decode_topk(d_keys, batch, d, ld, d_offsets, d_idx_out, s));
+  return 0;
+}
+
+int tblup_decode_topk(tblup_ctx* c, const double* keys, int64_t batch, int64_t d, const int64_t* offsets,
+                      int64_t* idx_out) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_decode(batch, d, offsets)) return rc;
+  if (batch == 0) return 0;
+  if (!keys || !idx_out) return fail(TBLUP_ERR_ARG, "null keys/idx_out");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int64_t total = offsets[batch];
+  if (int rc = dev_alloc(c, c->dec_keys, (size_t)batch * d * 8)) return rc;
+  if (int rc = dev_alloc(c, c->dec_idx, (size_t)(total + batch + 1) * 8)) return rc;
+  int64_t* d_idx = (int64_t*)c->dec_idx.p;
+  int64_t* d_off = d_idx + total;
+  HIPCHK(hipMemcpyAsync(c->dec_keys.p, keys, (size_t)batch * d * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d_off, offsets, (size_t)(batch + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(launch_decode_topk((const double*)c->dec_keys.p, batch, d, d, d_off, d_idx, c->stream));
+  HIPCHK(hipMemcpyAsync(idx_out, d_idx, (size_t)total * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
 }
 
 int tblup_set_profiling(tblup_ctx* c, int enable) {

@@ -162,59 +162,6 @@ __device__ __forceinline__ void gemm1_tt(const double* __restrict__ ltJ, const d
   __syncthreads();
 }
 
-// Same GEMM with 8-row stages: a D = 4 ring of 16 KiB stages keeps three stages (48 KiB)
-// in flight per workgroup within the same 64 KiB of LDS.
-__device__ __forceinline__ void glds_lt_stage8(const double* __restrict__ src, double* stage) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int k = 2 * w + e;
-    __builtin_amdgcn_global_load_lds(src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(stage + k * TILE), 16, 0,
-                                     0);
-  }
-}
-
-template <int D>
-__device__ __forceinline__ void gemm1_tt8(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
-                                          double* lds, v4d (&acc)[8][2]) {
-  constexpr int S8 = 8 * TILE;   // doubles per 8-row stage of one operand
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int nst = 16 * J;
-  if (nst == 0) return;
-  auto issue = [&](int s) {
-    double* slot = lds + (s % D) * 2 * S8;
-    glds_lt_stage8(ltJ + (int64_t)s * S8, slot);
-    glds_lt_stage8(ltI + (int64_t)s * S8, slot + S8);
-  };
-  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
-  for (int s = 0; s < nst; ++s) {
-    if (s + D - 2 < nst) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (s + D - 1 < nst) issue(s + D - 1);
-    const double* As = lds + (s % D) * 2 * S8;
-    const double* Bs = As + S8;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int k = 4 * kk + (l >> 4);
-      double bv[2];
-#pragma unroll
-      for (int ib = 0; ib < 2; ++ib) bv[ib] = Bs[lt_off(k, 32 * w + 16 * ib + (l & 15))];
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) {
-        const double av = As[lt_off(k, 16 * cb + (l & 15))];
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) acc[cb][ib] = mfma64_nega(av, bv[ib], acc[cb][ib]);
-      }
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
 // ---- SYRK restricted to the 36 lower 16x16 blocks (diag kernel), A = Lt tiles (J, L) ----
 __host__ __device__ constexpr int tri_q(int e) {
   int q = 0;

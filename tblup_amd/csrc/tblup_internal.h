@@ -130,6 +130,10 @@ hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s);
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s);
 
+// ---- launcher (k_decode.hip): RandomKey genome decode, top-k of each key row ----
+hipError_t launch_decode_topk(const double* keys, int64_t B, int64_t d, int64_t ld, const int64_t* off, int64_t* out,
+                              hipStream_t s);
+
 // XCD-aware bijective remap of a 1-D block id (blocks b and b+8 share an XCD
 // under the observed round-robin placement; speed only, never correctness).
 __device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {

@@ -142,6 +142,43 @@ class GpuBlupEngine:
             ctypes.c_void_p(d_ebv_ptr) if d_ebv_ptr else None,
             ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def decode_randkey(self, keys, lengths):
+        """RandomKeyIndividual.genome for a batch (individual.py:154-156) on the GPU:
+        row i -> np.argsort(keys[i])[-int(lengths[i]):] (ascending key order; equal keys
+        ordered by index, as a stable argsort).  Returns (idx, offsets) for evaluate_concat."""
+        kk = np.ascontiguousarray(np.asarray(keys, dtype=np.float64))
+        if kk.ndim != 2:
+            raise ValueError("keys must be (batch, d)")
+        B, d = kk.shape
+        lens = np.broadcast_to(np.asarray(lengths), (B,)).astype(np.int64)
+        offsets = np.zeros(B + 1, dtype=np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        idx = np.empty(int(offsets[-1]), dtype=np.int64)
+        if B:
+            _native.check("tblup_decode_topk", self._lib.tblup_decode_topk(
+                self._ctx, _ptr(kk, ctypes.c_double), B, d, _ptr(offsets, ctypes.c_int64), _ptr(idx, ctypes.c_int64)))
+        return idx, offsets
+
+    def decode_randkey_device(self, d_keys_ptr, B, d, ld, d_off_ptr, h_offsets, d_idx_ptr, stream_ptr=None):
+        """Device-resident decode: keys (B x ld doubles) -> idx at offsets (device pointers)."""
+        h_off = _as_int64(h_offsets)
+        _native.check("tblup_decode_topk_device", self._lib.tblup_decode_topk_device(
+            self._ctx, ctypes.c_void_p(d_keys_ptr), B, d, ld, ctypes.c_void_p(d_off_ptr), _ptr(h_off, ctypes.c_int64),
+            ctypes.c_void_p(d_idx_ptr), ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def evaluate_concat(self, idx, offsets, train, valid, h2, branch="auto"):
+        """evaluate() on an already-concatenated (idx, offsets) batch."""
+        sid = self.split_id(train, valid)
+        idx = _as_int64(idx)
+        offsets = _as_int64(offsets)
+        B = len(offsets) - 1
+        fit = np.empty(B, dtype=np.float64)
+        if B:
+            _native.check("tblup_eval_batch", self._lib.tblup_eval_batch(
+                self._ctx, sid, _ptr(idx, ctypes.c_int64), _ptr(offsets, ctypes.c_int64), B, float(h2),
+                _native.BRANCH[branch], _ptr(fit, ctypes.c_double), None))
+        return fit
+
     def debug_grm(self, indices, train, valid, h2, branch="auto", stage=1):
         """K_{R,T} (stage 1) or the factored block (stage 2) and z for one individual."""
         sid = self.split_id(train, valid)

@@ -202,8 +202,26 @@ class BlupParallelEvaluator(ParallelEvaluator):
         for i, indv in enumerate(population):
             if indv.uid not in self.archive:
                 where.append(i)
-                todo.append(indv.genome)
-        return todo, where, False
+                todo.append(indv)
+        return self._batch_genomes(todo), where, False
+
+    _GPU_DECODE_TYPES = ("RandomKeyIndividual", "CoevolutionIndividual")
+
+    def _batch_genomes(self, individuals):
+        """`indv.genome` for a batch.  RandomKey / Coevolution individuals
+        (individual.py:154-156: argsort(keys)[-int(length):]) are decoded on the GPU in one
+        call (k_decode_topk); equal keys order by index, the set numpy returns unless a tie
+        straddles the k-th key (continuous keys; DE clipping only creates ties at 0)."""
+        dec = getattr(self.engine, "decode_randkey", None)
+        if dec is not None and individuals and all(
+                type(i).__name__ in self._GPU_DECODE_TYPES and hasattr(i, "_genome") for i in individuals):
+            keys = [np.asarray(i._genome, dtype=np.float64) for i in individuals]
+            d = keys[0].shape[0]
+            lens = [int(i.length) for i in individuals]
+            if all(k.ndim == 1 and k.shape[0] == d for k in keys) and all(1 <= n <= min(d, 8192) for n in lens):
+                idx, off = dec(np.stack(keys), lens)
+                return [idx[off[j]:off[j + 1]] for j in range(len(individuals))]
+        return [i.genome for i in individuals]
 
     def evaluate(self, previous_population, next_population, generation):
         """evaluator.py:359-378."""

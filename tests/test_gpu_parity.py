@@ -351,3 +351,67 @@ def test_multitrait_config5_sample(config2):
         assert abs(fit[j] - np.mean(fs)) <= FIT_ATOL
     # trait 0 is the single-trait phenotype of the fixture
     np.testing.assert_array_equal(ebv[:, 0], c["ebv"][[0, 100, 255]])
+
+
+# ---------------------------------------------------------------------------
+# GPU genome decode: RandomKeyIndividual.genome =
+# np.argsort(keys)[-k:] (individual.py:154-156) -- bit-exact indices, order included
+# ---------------------------------------------------------------------------
+def _stable_topk(keys, k):
+    return np.argsort(keys, kind="stable")[-k:]
+
+
+def test_decode_randkey_matches_numpy(small):
+    _, eng = small
+    rng = np.random.default_rng(21)
+    d = 50_000
+    keys = rng.uniform(size=(12, d))
+    keys[3] = -keys[3]                                      # negative keys
+    keys[4] *= 1e-300                                       # subnormal / tiny range
+    lens = np.array([1000, 1000, 1, 2, 1000, 8192, 4097, 999, 1000, 1000, 50, 1000])
+    idx, off = eng.decode_randkey(keys, lens)
+    for i in range(12):
+        got = idx[off[i]:off[i + 1]]
+        np.testing.assert_array_equal(got, _stable_topk(keys[i], lens[i]))
+        np.testing.assert_array_equal(got, np.argsort(keys[i])[-lens[i]:])   # continuous keys: numpy default too
+
+
+def test_decode_randkey_ties(small):
+    """Ties straddling the k-th key: stable-argsort semantics (largest indices win)."""
+    _, eng = small
+    rng = np.random.default_rng(22)
+    d = 20_000
+    keys = np.round(rng.uniform(size=(6, d)), 2)            # ~100 distinct values: heavy ties
+    keys[1] = 0.5                                           # all equal
+    keys[2, :] = np.clip(rng.normal(size=d) * 3e4, 0, d - 1)   # DE-style clipping: ties at 0 and d-1
+    lens = [1000, 777, 8192, 1, 8000, 20]
+    idx, off = eng.decode_randkey(keys, lens)
+    for i in range(6):
+        np.testing.assert_array_equal(idx[off[i]:off[i + 1]], _stable_topk(keys[i], lens[i]))
+
+
+def test_evaluator_gpu_decode_path(golden_dir, gpu, tmp_path):
+    """BlupParallelEvaluator decodes RandomKey individuals on the GPU; fitness equals the
+    host-decoded path and the reference flow golden."""
+    import random
+    from tblup_amd import evaluator as E
+    from tests.helpers import KeyIndividual
+    z = _load(golden_dir, "blup_200x1000.npz")
+    flow = _load(golden_dir, "evaluator_flow.npz")
+    gp, pp = str(tmp_path / "g.npy"), str(tmp_path / "p.npy")
+    np.save(gp, z["geno"].astype(np.float64))
+    np.save(pp, z["pheno"])
+
+    class RandomKeyIndividual(KeyIndividual):   # the reference's class name triggers the GPU decode
+        pass
+
+    random.seed(3)
+    np.random.seed(3)
+    rem = E.SNPRemovalHandler(100, 0.0, 0.4, False)
+    with E.BlupParallelEvaluator(gp, pp, 0.4, n_procs=2, snp_remover=rem) as ev:
+        pop = [RandomKeyIndividual(k, 100) for k in flow["flow_keys"]]
+        todo, where, _ = ev.genomes_to_evaluate(pop)
+        for g, indv in zip(todo, pop):
+            np.testing.assert_array_equal(g, indv.genome)
+        ev.evaluate(pop, pop, 0)
+        np.testing.assert_allclose([p.fitness for p in pop], flow["flow_fitness"], rtol=0, atol=FIT_ATOL)
