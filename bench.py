@@ -71,7 +71,7 @@ def make_workload(cfg, seed, rank, pop, traits=1):
     T, V = perm[:nT], perm[nT:nT + nV]
     keys = np.random.default_rng(seed + 100 + rank).uniform(size=(pop, P))
     genomes = np.argsort(keys, axis=1)[:, -k:]            # RandomKeyIndividual decode (individual.py:154-156)
-    return geno, pheno, T, V, genomes
+    return geno, pheno, T, V, genomes, keys
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -135,7 +135,9 @@ def main():
     pop = args.pop or pop_default
 
     traits = TRAITS.get(args.config, 1)
-    geno, pheno, T, V, genomes = make_workload(cfg, args.seed, rank, pop, traits)
+    geno, pheno, T, V, genomes, keys = make_workload(cfg, args.seed, rank, pop, traits)
+    if k > 8192:
+        keys = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(geno, pheno, T, V, genomes, args.h2, args.cpu_seconds)
@@ -179,6 +181,26 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
     prof = eng.profile()
+
+    # GPU genome decode of the same population (RandomKeyIndividual.genome, individual.py:154-156)
+    # from device-resident keys: reported beside the metric, not part of it
+    decode_ms = None
+    if keys is not None:
+        d_keys = torch.from_numpy(keys).cuda()
+        d_dec = torch.empty(int(off[-1]), dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            eng.decode_randkey_device(d_keys.data_ptr(), pop, P, P, d_off.data_ptr(), off, d_dec.data_ptr(),
+                                      stream.cuda_stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(5):
+            eng.decode_randkey_device(d_keys.data_ptr(), pop, P, P, d_off.data_ptr(), off, d_dec.data_ptr(),
+                                      stream.cuda_stream)
+        torch.cuda.synchronize()
+        decode_ms = (time.perf_counter() - t1) / 5 * 1e3
+        if not np.array_equal(d_dec.cpu().numpy(), idx):
+            raise RuntimeError("GPU decode differs from the host argsort decode")
+        del d_keys, d_dec
     fit = d_fit.cpu().numpy()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -230,6 +252,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": step_ms,
+            "gpu_decode_ms": None if decode_ms is None else round(decode_ms, 4),
             "fitness_checksum": float(np.nansum(fit)),
         }
         print(json.dumps(line), flush=True)
