@@ -415,3 +415,42 @@ def test_evaluator_gpu_decode_path(golden_dir, gpu, tmp_path):
             np.testing.assert_array_equal(g, indv.genome)
         ev.evaluate(pop, pop, 0)
         np.testing.assert_allclose([p.fitness for p in pop], flow["flow_fitness"], rtol=0, atol=FIT_ATOL)
+
+
+def test_knockout_local_search_gpu(golden_dir, gpu, tmp_path):
+    """KnockoutLocalSearch (local.py:50-76) with speculative GPU batches = the sequential
+    oracle walk."""
+    import random
+    from tblup_amd import evaluator as E
+    from tblup_amd.local import KnockoutLocalSearch
+    from tests.helpers import IdxIndividual
+    z = _load(golden_dir, "blup_200x1000.npz")
+    gp, pp = str(tmp_path / "g.npy"), str(tmp_path / "p.npy")
+    np.save(gp, z["geno"].astype(np.float64))
+    np.save(pp, z["pheno"])
+    random.seed(8)
+    np.random.seed(8)
+    rem = E.SNPRemovalHandler(100, 0.0, 0.4, False)
+    with E.BlupParallelEvaluator(gp, pp, 0.4, snp_remover=rem) as ev:
+        rng = np.random.default_rng(8)
+        pop = [IdxIndividual(np.sort(rng.choice(1000, 60, replace=False)), 60) for _ in range(4)]
+        ev.evaluate(pop, pop, 0)
+
+        class _Pop(list):
+            evaluator = ev
+
+        best = max(pop, key=lambda i: i.fitness)
+        genome, fit = KnockoutLocalSearch(_Pop(pop), window=16).search()
+    g, y, T, V = z["geno"].astype(np.float64), z["pheno"], ev.training_indices, ev.validation_indices
+    full = np.union1d(best.genome, np.array([])).astype(int)
+    mask = np.ones(len(full), dtype=bool)
+    bf = best.fitness
+    for i in range(len(full)):
+        mask[i] = False
+        f = O.blup(full[mask], T, V, g, y, 0.4)
+        if f > bf:
+            bf = f
+        else:
+            mask[i] = True
+    np.testing.assert_array_equal(genome, full[mask])
+    assert abs(fit - bf) <= FIT_ATOL
