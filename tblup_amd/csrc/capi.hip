@@ -48,7 +48,7 @@ struct DevBuf {
 struct Split {
   int64_t nT = 0, nV = 0, nTp = 0, nVp = 0, nRp = 0;
   std::vector<double> meanyT;   // [nt]
-  DevBuf geno, colsumT, xty, yT, yV, ymu;
+  DevBuf geno, gpk, colsumT, xty, yT, yV, ymu;
 };
 
 enum { KC_STATS = 0, KC_GATHER, KC_GRM, KC_DIAG, KC_OFFDIAG, KC_SOLVE };
@@ -283,7 +283,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   if (K_out) *K_out = L;
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
                 (const double*)sp.ymu.p, panel, pstride, d_off,
-                (const int8_t*)sp.geno.p, d_idx, d.nRp, u, scal,
+                (const int8_t*)sp.geno.p, d_idx, d.nRp, (const uint8_t*)sp.gpk.p, d.nRp / 4, u, scal,
                 c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0)};
   const double T3 = (double)TILE * TILE * TILE;
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
@@ -404,6 +404,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   for (auto& kv : c->splits) {
     kv.second->geno.release();
+    kv.second->gpk.release();
     kv.second->colsumT.release();
     kv.second->xty.release();
     kv.second->yT.release();
@@ -455,6 +456,7 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
     for (int64_t i = 0; i < nV; ++i) yV[t * nV + i] = c->pheno[valid[i] * nt + t];
   }
   if (int rc = dev_alloc(c, sp->geno, (size_t)(c->P + 1) * sp->nRp)) return rc;
+  if (int rc = dev_alloc(c, sp->gpk, (size_t)(c->P + 1) * (sp->nRp / 4))) return rc;
   if (int rc = dev_alloc(c, sp->colsumT, (size_t)c->P * 4)) return rc;
   if (int rc = dev_alloc(c, sp->xty, (size_t)nt * c->P * 8)) return rc;
   if (int rc = dev_alloc(c, sp->yT, yT.size() * 8)) return rc;
@@ -468,12 +470,13 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   HIPCHK(hipMemcpyAsync(sp->ymu.p, sp->meanyT.data(), (size_t)nt * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(launch_build_split((const int8_t*)c->geno_sm.p, c->n, c->P, (const int32_t*)rm.p, sp->nRp, nT,
                             (const double*)sp->yT.p, (const double*)sp->ymu.p, nt, (int8_t*)sp->geno.p,
-                            (int32_t*)sp->colsumT.p, (double*)sp->xty.p, c->stream));
+                            (uint8_t*)sp->gpk.p, (int32_t*)sp->colsumT.p, (double*)sp->xty.p, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   dev_free(c, rm);
   auto it = c->splits.find(split_id);
   if (it != c->splits.end()) {
     dev_free(c, it->second->geno);
+    dev_free(c, it->second->gpk);
     dev_free(c, it->second->colsumT);
     dev_free(c, it->second->xty);
     dev_free(c, it->second->yT);
@@ -492,6 +495,7 @@ int tblup_set_traits(tblup_ctx* c, const double* pheno, int64_t n_traits) {
   HIPCHK(hipStreamSynchronize(c->stream));
   for (auto& kv : c->splits) {   // splits hold per-trait phenotype vectors
     dev_free(c, kv.second->geno);
+    dev_free(c, kv.second->gpk);
     dev_free(c, kv.second->colsumT);
     dev_free(c, kv.second->xty);
     dev_free(c, kv.second->yT);
@@ -517,6 +521,7 @@ int tblup_drop_split(tblup_ctx* c, int split_id) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   dev_free(c, it->second->geno);
+    dev_free(c, it->second->gpk);
   dev_free(c, it->second->colsumT);
   dev_free(c, it->second->xty);
   dev_free(c, it->second->yT);

@@ -119,6 +119,47 @@ __device__ __forceinline__ void i8_tt(const int8_t* const (&sa)[2], const int8_t
   __syncthreads();
 }
 
+// Packed variant: stage kb = 64 animals = 16 B per row; rows of A (tile J) then B (tile I),
+// 4 KiB per stage, wave w loads rows 64(w&1)..+63 of operand w>>1.  src: this lane's row.
+template <int D>
+__device__ __forceinline__ void i8_tt_packed(const uint8_t* src, int64_t nblk, uint8_t* lds, v4i (&cnt)[8][2]) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = v4i{0, 0, 0, 0};
+  if (nblk <= 0) return;
+  constexpr int SB = 2 * TILE * 16;   // 4 KiB per stage
+  auto issue = [&](int64_t kb) {
+    __builtin_amdgcn_global_load_lds(src + kb * 16, (lds_ptr_t)(lds + (int)(kb % D) * SB + w * 1024), 16, 0, 0);
+  };
+  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    if (kb + D - 2 < nblk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 2) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kb + D - 1 < nblk) issue(kb + D - 1);
+    const uint8_t* As = lds + (int)(kb % D) * SB;
+    const uint8_t* Bs = As + TILE * 16;
+    v4i bv[2];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+      bv[ib] = unpack16(*reinterpret_cast<const uint32_t*>(Bs + (32 * w + 16 * ib + rho) * 16 + 4 * ch));
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const v4i av = unpack16(*reinterpret_cast<const uint32_t*>(As + (16 * cb + prow) * 16 + 4 * ch));
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[ib], cnt[cb][ib], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // ---- GEMM1 of the off-diagonal kernel: acc[cb][ib] -= sum_{k < 128J} L_J[c][k] L_I[i][k] ----
 // A = Lt tiles (J, L), B = Lt tiles (I, L), L < J; LDS-DMA ring of D slots x 32 KiB.
 template <int D>
@@ -316,8 +357,9 @@ struct CholArgs {
   const double* scal;       // [B][SCAL]
   int64_t ns, prow;         // padded system size, panel rows per contraction block
   int form;
-  // primal form: rows read in place from the split's SNP-major matrix (row P is zero)
-  const int8_t* gs;
+  // primal form: rows read in place from the split's 2-bit packed SNP-major matrix
+  // (row P is zero)
+  const uint8_t* gs;
   const int64_t* idx;
   const int64_t* off;
   int64_t gs_row, P;
@@ -329,21 +371,20 @@ struct CholArgs {
 };
 
 // Address of system row r's contraction block 0 for individual b: the gathered panel
-// (dual) or the selected SNP row of the split matrix itself (primal; padding rows -> the
-// zero row P).  Stage kb is at + kb * row_kstep(a).
+// (dual; stage kb at + kb * prow * 64).
 __device__ __forceinline__ const int8_t* row_base(const CholArgs& a, int64_t b, int64_t r) {
-  if (a.form == FORM_PRIMAL) {
-    const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
-    int64_t p = a.P;
-    if (r < k) {
-      p = a.idx[o0 + r];
-      p = p < 0 ? 0 : (p >= a.P ? a.P - 1 : p);
-    }
-    return a.gs + p * a.gs_row;
-  }
   return a.panel + b * a.pstride + r * KBLK;
 }
-__device__ __forceinline__ int64_t row_kstep(const CholArgs& a) { return a.form == FORM_PRIMAL ? KBLK : a.prow * KBLK; }
+// Packed split row of system row r (primal; padding rows -> the zero row P; stage kb at + 16 kb).
+__device__ __forceinline__ const uint8_t* row_packed(const CholArgs& a, int64_t b, int64_t r) {
+  const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
+  int64_t p = a.P;
+  if (r < k) {
+    p = a.idx[o0 + r];
+    p = p < 0 ? 0 : (p >= a.P ? a.P - 1 : p);
+  }
+  return a.gs + p * a.gs_row;
+}
 
 // ---------------------------------------------------------------------------
 // Diagonal tile T_J = K_JJ - sum_{L<J} L_JL L_JL^T is assembled from pieces that are
@@ -391,13 +432,19 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
   double* Kd = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
   v16i ci[2][2];
   if (!(a.skip & 1)) {
-    const int8_t* src[2];
+    if (a.form == FORM_PRIMAL) {
+      const int t = threadIdx.x;
+      i8_tile_syrk_packed<16>(row_packed(a, b, j0 + ((t >> 6) & 1) * 64 + (t & 63)), nblk,
+                              reinterpret_cast<uint8_t*>(lds), ci);
+    } else {
+      const int8_t* src[2];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int row = i8_ring_row(e);
-      src[e] = row_base(a, b, j0 + row) + i8_ring_chunk(row);
+      for (int e = 0; e < 2; ++e) {
+        const int row = i8_ring_row(e);
+        src[e] = row_base(a, b, j0 + row) + i8_ring_chunk(row);
+      }
+      i8_tile_syrk_ring<8>(src, nblk, a.prow * KBLK, lds, ci);
     }
-    i8_tile_syrk_ring<8>(src, nblk, row_kstep(a), lds, ci);
   } else {
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -641,7 +688,11 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   {
     v4i cnt[8][2];
     const int64_t nblk = (int64_t)sc[SC_CBLK];
-    if (!(a.skip & 32)) {
+    if (!(a.skip & 32) && a.form == FORM_PRIMAL) {
+      // wave w loads rows 64(w&1) + l of tile J (w < 2) or tile I (w >= 2)
+      i8_tt_packed<16>(row_packed(a, b, ((w >> 1) ? i0 : j0) + 64 * (w & 1) + l), nblk,
+                       reinterpret_cast<uint8_t*>(lds), cnt);
+    } else if (!(a.skip & 32)) {
       const int8_t *sa[2], *sb[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -649,7 +700,7 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
         sa[e] = row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3));
         sb[e] = row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2));
       }
-      i8_tt<4>(sa, sb, nblk, row_kstep(a), reinterpret_cast<int8_t*>(lds),
+      i8_tt<4>(sa, sb, nblk, a.prow * KBLK, reinterpret_cast<int8_t*>(lds),
                cnt);
     } else {
 #pragma unroll
@@ -758,21 +809,21 @@ __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int I0, int
 
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip};
   hipLaunchKernelGGL(k_diag_grm, dim3((unsigned)(c.B * c.sd.NT)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gs, c.idx, c.off, c.gs_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
   const int I0 = J + 1, nI = c.sd.NT - I0;
   if (nI <= 0) return hipSuccess;
   a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;

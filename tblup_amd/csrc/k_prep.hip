@@ -82,17 +82,28 @@ hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, 
 __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ g, int64_t n, int64_t P,
                                                      const int32_t* __restrict__ rowmap, int64_t nRp, int64_t nT,
                                                      const double* __restrict__ yT, const double* __restrict__ ymu,
-                                                     int nt, int8_t* __restrict__ out, int32_t* __restrict__ csT,
-                                                     double* __restrict__ xty) {
+                                                     int nt, int8_t* __restrict__ out, uint8_t* __restrict__ opk,
+                                                     int32_t* __restrict__ csT, double* __restrict__ xty) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * 4 + w;
   if (p > P) return;
   int8_t* orow = out + p * nRp;
+  uint8_t* prow = opk + p * (nRp / 4);
   if (p == P) {   // the zero row
     for (int64_t r = l; r < nRp; r += 64) orow[r] = 0;
+    for (int64_t q = l; q < nRp / 4; q += 64) prow[q] = 0;
     return;
   }
   const int8_t* row = g + p * n;
+  for (int64_t q = l; q < nRp / 4; q += 64) {   // 2-bit packed copy: animal 4q+i at bits 2i
+    uint32_t pk = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t src = rowmap[4 * q + i];
+      pk |= (uint32_t)(src >= 0 ? (uint8_t)row[src] : 0u) << (2 * i);
+    }
+    prow[q] = (uint8_t)pk;
+  }
   const int64_t nTp = (nT + TILE - 1) / TILE * TILE;
   int s = 0;
   double dot[MAXT] = {0.0, 0.0, 0.0, 0.0};
@@ -123,9 +134,9 @@ __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ 
 
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap, int64_t nRp,
                               int64_t nT, const double* yT, const double* ymu, int nt, int8_t* geno_split,
-                              int32_t* colsum_T, double* xty, hipStream_t s) {
+                              uint8_t* geno_packed, int32_t* colsum_T, double* xty, hipStream_t s) {
   hipLaunchKernelGGL(k_build_split, dim3((unsigned)((P + 1 + 3) / 4)), dim3(256), 0, s, geno_sm, n, P, rowmap, nRp,
-                     nT, yT, ymu, nt, geno_split, colsum_T, xty);
+                     nT, yT, ymu, nt, geno_split, geno_packed, colsum_T, xty);
   return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 //   per split s (train T, valid V; nTp/nVp = sizes rounded up to 128):
 //     geno      int8 [P+1][nRp]   SNP-major rows permuted to [T | 0-pad | V | 0-pad], nRp = nTp+nVp;
 //                                 row P is all zero (padding rows of the primal form)
+//     gpk       uint8 [P+1][nRp/4] the same, 2-bit packed (animal 4j+i at bits 2i of byte j)
 //     colsum_T  int32 [P]         allele counts over T (snp p)
 //     xty       f64  [nt][P]      sum_t x_tp (y_t - mean y_T): the primal right-hand side, per SNP and trait
 //     yT        f64 [nTp]         phenotypes of T (0 in padding), yV f64 [nV]
@@ -83,7 +84,8 @@ hipError_t launch_transpose_geno(const int8_t* src, int8_t* dst, int64_t n, int6
 hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap,
                               int64_t nRp, int64_t nT, const double* yT, const double* ymu, int nt,
-                              int8_t* geno_split, int32_t* colsum_T, double* xty, hipStream_t s);
+                              int8_t* geno_split, uint8_t* geno_packed, int32_t* colsum_T, double* xty,
+                              hipStream_t s);
 // primal form (sd.form): also u[b][a] = s_a and rhs[b][t][a] = xty[t][p_a] / d over the ns rows
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
                               const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
@@ -118,6 +120,8 @@ struct CholLaunch {
   const int8_t* gs;      // split SNP-major matrix [P+1][gs_row] (row P zero): primal rows in place
   const int64_t* idx;    // device SNP indices of the chunk
   int64_t gs_row;        // bytes per split row (nRp)
+  const uint8_t* gpk;    // the same matrix 2-bit packed [P+1][gpk_row] (4 animals per byte)
+  int64_t gpk_row;       // nRp / 4
   const double* u;       // [B][prow]
   const double* scal;    // [B][SCAL]
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
