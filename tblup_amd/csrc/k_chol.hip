@@ -210,6 +210,13 @@ __host__ __device__ constexpr int tri_q(int e) {
   return q;
 }
 __host__ __device__ constexpr int tri_s(int e) { return e - tri_q(e) * (tri_q(e) + 1) / 2; }
+// runtime row of packed lower block e (e < 36)
+__device__ __forceinline__ int tri_q_rt(int e) {
+  int q = (int)((__builtin_sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+  if ((q + 1) * (q + 2) / 2 <= e) ++q;
+  if (q * (q + 1) / 2 > e) --q;
+  return q;
+}
 
 template <int W>
 __device__ __forceinline__ void syrk_stage(const double* As, v4d (&acc)[9], int l) {
@@ -499,7 +506,11 @@ __device__ __forceinline__ void syrk_rows_global(const double* __restrict__ lt, 
 // ---------------------------------------------------------------------------
 // Diagonal tile J of individual b.  T = S - sum_{L0 <= L < J} L_JL L_JL^T where S is
 // K_JJ - sum_{L < L0} (the buffer slot J&1 left by an earlier off-diagonal launch) when
-// L0 > 0, else k_diag_grm's K_JJ.  lds >= (NPACK + NBLK) * BLKD doubles.
+// L0 > 0, else k_diag_grm's K_JJ.
+// LDS (lds >= 2 * NPACK * BLKD doubles = 144 KiB): Tp = T -> L (packed lower 16x16 blocks),
+// Xp = X = L^{-1} in the same packed layout; before the factorisation Xp's space is the
+// 64 KiB SYRK stage ring.  X never round-trips through global memory: Dinv receives X^T
+// once, at the end.
 __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, int L0, double* lds,
                                           double (*rsh)[TILE]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -511,16 +522,15 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   const int64_t nrow = (int64_t)sc[SC_NROW];
   const int nt = a.nt;
   double* Tp = lds;
-  double* Xd = lds + NPACK * BLKD;   // X_pp, p = 0..7
+  double* Xp = lds + NPACK * BLKD;
   double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;   // X^T, row-major: XT[c][i] = X[i][c]
 
-  // T = S - sum_{L0 <= L < J} L_JL L_JL^T, wave w taking the packed blocks {w + 4i} over
-  // the 128 k rows of each Lt tile (J, L), straight from global.
+  // T = S - sum_{L0 <= L < J} L_JL L_JL^T: S by LDS-DMA, the SYRK through the stage ring
   {
     const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
                                   : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
 #pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread, LDS-DMA
+    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread
       const int chunk = (e * 4 + w) * 64;
       __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
     }
@@ -528,15 +538,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       v4d acc[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-      const double* lt = a.L + ((b * NT + J) * (int64_t)NT + L0) * TT;
-      for (int k0 = 0; k0 < TILE * (J - L0); k0 += 32) {
-        if (w == 0) syrk_rows_global<0>(lt, k0, acc, l);
-        else if (w == 1) syrk_rows_global<1>(lt, k0, acc, l);
-        else if (w == 2) syrk_rows_global<2>(lt, k0, acc, l);
-        else syrk_rows_global<3>(lt, k0, acc, l);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      // waits for all its stages (and the older S loads) and ends in a barrier
+      syrk_lower<4>(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
         const int e = w + 4 * i;
@@ -565,11 +568,11 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 
   // C. blocked right-looking factorisation over 16-column panels
   for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
-    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xd + p * BLKD, l);
+    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xp + pk(p, p), l);
     __syncthreads();
     for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += 4) {
       v4d x = {0.0, 0.0, 0.0, 0.0};
-      x = mma_abt(Tp + pk(q, p), Xd + p * BLKD, x, l);
+      x = mma_abt(Tp + pk(q, p), Xp + pk(p, p), x, l);
 #pragma unroll
       for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
     }
@@ -589,16 +592,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   }
   if (a.skip & 16) return;
 
-  // E1. X^T tile: diagonal blocks from Xd.  Blocks below the diagonal of X^T (X = 0 there)
-  //     are never written and never read (k_solve and the off-diagonal GEMM2 skip them).
-  for (int e = t; e < NBLK * BLKD; e += 256) {
-    const int pb = e >> 8, rr = (e >> 4) & 15, cc = e & 15;
-    XT[(16 * pb + rr) * TILE + 16 * pb + cc] = Xd[pb * BLKD + bo(cc, rr)];
-  }
-  __threadfence_block();
-  __syncthreads();
-
-  // D. blocked inverse, one block diagonal per round, off-diagonal blocks through Dinv:
+  // D. blocked inverse in LDS, one block diagonal per round:
   //    X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
   for (int dd = 1; dd < ((a.skip & 8) ? 0 : NBLK); ++dd) {
     for (int jb = w; jb + dd < NBLK; jb += 4) {
@@ -606,29 +600,31 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       v4d sacc = {0.0, 0.0, 0.0, 0.0};
       for (int lb = jb; lb < q; ++lb) {
         const double* A = Tp + pk(q, lb);
+        const double* B = Xp + pk(lb, jb);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int k = 4 * kk + (l >> 4);
-          // B[k][c] = X_{lb,jb}[k][c] = XT[16jb + c][16lb + k]
-          const double xb = (lb == jb) ? Xd[jb * BLKD + bo(k, l & 15)] : XT[(16 * jb + (l & 15)) * TILE + 16 * lb + k];
-          sacc = mfma64(A[bo(l & 15, k)], xb, sacc);
+          sacc = mfma64(A[bo(l & 15, k)], B[bo(k, l & 15)], sacc);
         }
       }
       v4d xo = {0.0, 0.0, 0.0, 0.0};
-      const double* Xqq = Xd + q * BLKD;
+      const double* Xqq = Xp + pk(q, q);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) xo = mfma64(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
+      for (int kk = 0; kk < 4; ++kk) xo = mfma64_nega(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
+      double* dst = Xp + pk(q, jb);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)   // X_{q,jb}[i][c] -> XT[16jb + c][16q + i]
-        XT[(16 * jb + (l & 15)) * TILE + 16 * q + (l >> 4) + 4 * r] = -xo[r];
+      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] = xo[r];
     }
-    __threadfence_block();
     __syncthreads();
   }
 
-  // E2. L_JJ^T into the Lt tile (J, J); z_J = X_J r  (z_i = sum_c XT[c][i] r_c)
-  //     (L_JJ itself is read by nothing downstream -- only X is -- so it is written only
-  //     for the debug readback)
+  // E. X^T into Dinv (blocks (q >= jb) of X; blocks of X^T below its diagonal are never
+  //    written and never read), z_J = X r, and L_JJ^T only for the debug readback.
+  for (int e = t; e < NPACK * BLKD; e += 256) {
+    const int blk = e >> 8, c = (e >> 4) & 15, i = e & 15;
+    const int q = tri_q_rt(blk), jb = blk - q * (q + 1) / 2;
+    XT[(16 * jb + c) * TILE + 16 * q + i] = Xp[blk * BLKD + bo(i, c)];
+  }
   if (a.skip & FLAG_WRITE_LJJ) {
     double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
     for (int e = t; e < TT; e += 256) {
@@ -638,8 +634,9 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   }
   if (t < TILE) {
     double acc_z[MAXT] = {0.0, 0.0, 0.0, 0.0};
+    const int qi = t >> 4, ii = t & 15;
     for (int c = 0; c <= t; ++c) {
-      const double xc = XT[c * TILE + t];
+      const double xc = Xp[pk(qi, c >> 4) + bo(ii, c & 15)];
 #pragma unroll
       for (int tr = 0; tr < MAXT; ++tr) acc_z[tr] += xc * rsh[tr][c];
     }
@@ -652,7 +649,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 // Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
 // K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
 __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) double lds[(NPACK + NBLK) * BLKD];
+  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
   __shared__ double rsh[MAXT][TILE];
   diag_tile(a, blockIdx.x, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
 }
