@@ -566,10 +566,14 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   }
   __syncthreads();
 
-  // C. blocked right-looking factorisation over 16-column panels
-  for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
-    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(p, p), Xp + pk(p, p), l);
+  // C. blocked right-looking factorisation over 16-column panels, with a one-block
+  //    look-ahead: wave 0 updates diagonal block p+1 first and factors it while waves 1-3
+  //    finish the rest of step p's trailing update.
+  if (!(a.skip & 4)) {
+    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(0, 0), Xp + pk(0, 0), l);
     __syncthreads();
+  }
+  for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
     for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += 4) {
       v4d x = {0.0, 0.0, 0.0, 0.0};
       x = mma_abt(Tp + pk(q, p), Xp + pk(p, p), x, l);
@@ -577,16 +581,29 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
     }
     __syncthreads();
+    if (p + 1 == NBLK) break;
     const int nb = NBLK - 1 - p;
-    for (int e = w; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += 4) {
-      int qq = 0;
-      while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
-      const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
-      v4d x = {0.0, 0.0, 0.0, 0.0};
-      x = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), x, l);
-      double* dst = Tp + pk(q, sb);
+    if (w == 0) {
+      if (!(a.skip & 512)) {
+        v4d x = {0.0, 0.0, 0.0, 0.0};
+        x = mma_abt(Tp + pk(p + 1, p), Tp + pk(p + 1, p), x, l);
+        double* dst = Tp + pk(p + 1, p + 1);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
+        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
+      }
+      if (!(a.skip & 256)) factor16(Tp + pk(p + 1, p + 1), Xp + pk(p + 1, p + 1), l);
+    } else {
+      // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over waves 1-3
+      for (int e = w; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += 3) {
+        int qq = 0;
+        while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
+        const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
+        v4d x = {0.0, 0.0, 0.0, 0.0};
+        x = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), x, l);
+        double* dst = Tp + pk(q, sb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
+      }
     }
     __syncthreads();
   }
