@@ -171,7 +171,7 @@ size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_
   add((size_t)B * sd.prow * 8);                                 // u
   add((size_t)B * SCAL * 8);                                    // scal
   add((size_t)B * sd.ns * sd.ns * 8);                           // L (Lt tiles)
-  add((size_t)B * sd.NT * TILE * TILE * 8);                     // Dinv
+  add((size_t)B * sd.NT * NPACK * BLKD * 8);                    // Dinv (packed X)
   add((size_t)B * d.nt * sd.ns * 8);                            // z
   add((size_t)B * d.nt * sd.ns * 8);                            // w
   add((size_t)B * d.nt * sd.ns * 8);                            // rhs
@@ -249,7 +249,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* u = cv.take<double>((size_t)B * sd.prow);
   double* scal = cv.take<double>((size_t)B * SCAL);
   double* L = cv.take<double>((size_t)B * sd.ns * sd.ns);
-  double* Dinv = cv.take<double>((size_t)B * sd.NT * TILE * TILE);
+  double* Dinv = cv.take<double>((size_t)B * sd.NT * NPACK * BLKD);
   double* z = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* wv = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* rhs = cv.take<double>((size_t)B * d.nt * sd.ns);

@@ -257,15 +257,6 @@ __device__ __forceinline__ void syrk_lower(const double* __restrict__ src, int n
   __syncthreads();
 }
 
-// ---- packed lower-triangular 16x16 block storage of a 128x128 tile in LDS ----
-constexpr int NB = 16;                       // base block edge
-constexpr int NBLK = TILE / NB;              // 8 block rows
-constexpr int NPACK = NBLK * (NBLK + 1) / 2; // 36 lower blocks
-constexpr int BLKD = NB * NB;                // doubles per block
-
-__device__ __forceinline__ int pk(int q, int s) { return (q * (q + 1) / 2 + s) * BLKD; }
-// element (r, c) of a 16x16 block; 16-B chunk swizzle makes the fragment reads conflict-free
-__device__ __forceinline__ int bo(int r, int c) { return r * NB + 2 * ((c >> 1) ^ ((r >> 1) & 7)) + (c & 1); }
 
 // acc (16x16, f64 MFMA C layout) += A(16x16) * B(16x16)^T, both blocks in LDS
 __device__ __forceinline__ v4d mma_abt(const double* A, const double* Bt, v4d acc, int l) {
@@ -350,7 +341,7 @@ __device__ __forceinline__ void factor16(double* D, double* X, int l) {
 // Per-launch arguments shared by the two Cholesky kernels.
 struct CholArgs {
   double* L;                // Lt tiles [B][NT][NT][128*128]
-  double* Dinv;             // [B][NT][128][128]
+  double* Dinv;             // [B][NT][36 packed 16x16 blocks] X = L_JJ^{-1}
   double* z;                // [B][nt][ns]
   double* w;                // [B][nt][ns] forward-substitution partial sums
   double* S;                // [B][2][36*256] K_JJ - sum_{L<J-1} L_JL L_JL^T, slot J&1
@@ -523,7 +514,6 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   const int nt = a.nt;
   double* Tp = lds;
   double* Xp = lds + NPACK * BLKD;
-  double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;   // X^T, row-major: XT[c][i] = X[i][c]
 
   // T = S - sum_{L0 <= L < J} L_JL L_JL^T: S by LDS-DMA, the SYRK through the stage ring
   {
@@ -635,12 +625,15 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     __syncthreads();
   }
 
-  // E. X^T into Dinv (blocks (q >= jb) of X; blocks of X^T below its diagonal are never
-  //    written and never read), z_J = X r, and L_JJ^T only for the debug readback.
-  for (int e = t; e < NPACK * BLKD; e += 256) {
-    const int blk = e >> 8, c = (e >> 4) & 15, i = e & 15;
-    const int q = tri_q_rt(blk), jb = blk - q * (q + 1) / 2;
-    XT[(16 * jb + c) * TILE + 16 * q + i] = Xp[blk * BLKD + bo(i, c)];
+  // E. X into Dinv as packed lower blocks, each block transposed (block (q, jb) holds
+  //    X_{q,jb}^T in the bo() layout), z_J = X r, and L_JJ^T only for the debug readback.
+  {
+    double* Xg = a.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
+    for (int e = t; e < NPACK * BLKD; e += 256) {   // linear (conflict-free) LDS reads
+      const int blk = e >> 8, o = e & 255, i = o >> 4;
+      const int cpos = o & 15, c = 2 * ((cpos >> 1) ^ ((i >> 1) & 7)) + (cpos & 1);   // o = bo(i, c)
+      Xg[blk * BLKD + bo(c, i)] = Xp[e];
+    }
   }
   if (a.skip & FLAG_WRITE_LJJ) {
     double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
@@ -740,37 +733,34 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   // 1. T^T = K_JI - sum_L L_JL L_IL^T
   if (J > 0 && !(a.skip & 64)) gemm1_tt<2>(Lb + (int64_t)J * NT * TT, Lb + (int64_t)I * NT * TT, J, lds, acc);
 
-  // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X^T, so
-  //    the stage for block jb (X^T[c][16jb..16jb+15], 128 rows x 128 B) lands in LDS as the
-  //    [c][j] image the A fragments want, by LDS-DMA (8 rows per wave instruction).
-  const double* XT = a.Dinv + (b * NT + J) * (int64_t)TT;
+  // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X in the
+  //    packed block layout (blocks transposed): all 36 blocks (72 KiB) land in LDS in one
+  //    LDS-DMA burst, then
+  //    the 8 block rows run without further waits.
   double* Lout = const_cast<double*>(Lb) + ((int64_t)I * NT + J) * TT;
-  double* xs = lds;   // [2][128 c][16 j]
-  auto xissue = [&](int jb) {
-    double* slot = xs + (jb & 1) * TILE * 16;
+  double* xl = lds;
+  {
+    const double* Xg = a.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = 32 * w + 8 * e + (l >> 3);
-      __builtin_amdgcn_global_load_lds(XT + c * TILE + 16 * jb + 2 * (l & 7),
-                                       (lds_ptr_t)(slot + (32 * w + 8 * e) * 16), 16, 0, 0);
+    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread
+      const int chunk = (e * 4 + w) * 64;
+      __builtin_amdgcn_global_load_lds(Xg + 2 * (chunk + l), (lds_ptr_t)(xl + 2 * chunk), 16, 0, 0);
     }
-  };
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   double wacc[MAXT][2] = {};
-  xissue(0);
 #pragma unroll 1
   for (int jb = 0; jb < NBLK; ++jb) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (jb + 1 < NBLK) xissue(jb + 1);
     v4d o[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
     if (!(a.skip & 128)) {
-      const double* xb = xs + (jb & 1) * TILE * 16;
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) {
         if (cb <= jb) {
+          const double* xb = xl + pk(jb, cb);
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
-            const double av = xb[(16 * cb + 4 * kk + (l >> 4)) * 16 + (l & 15)];
+            const double av = xb[bo(4 * kk + (l >> 4), l & 15)];   // X_{jb,cb}[l&15][k], stored transposed
 #pragma unroll
             for (int ib = 0; ib < 2; ++ib) o[ib] = mfma64(av, acc[cb][ib][kk], o[ib]);
           }
@@ -810,7 +800,7 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
 // L = J term: S[(J+1)&1] = K - sum_{L<J} (those tiles are final already).
 // LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
 __global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
-  __shared__ __attribute__((aligned(16))) double lds[4 * LTS];   // 64 KiB
+  __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
   __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
   const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
   if ((int64_t)blockIdx.x < n_extra) {

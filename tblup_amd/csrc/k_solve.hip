@@ -98,7 +98,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
-  const double* Db = c.Dinv + b * (int64_t)NT * TILE * TILE;
+  const double* Db = c.Dinv + b * (int64_t)NT * NPACK * BLKD;
   const double* sc = c.scal + b * SCAL;
   const double invN = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], muf = sc[SC_MUF];
 
@@ -129,16 +129,19 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       if (seg == 0) vsh[tr][rc] = c.z[(b * nt + tr) * ns + (int64_t)I * TILE + rc] - s[tr];
     }
     __syncthreads();
-    // alpha_I = X_I^T v: Dinv holds X^T, so again row c dotted with v
-    // (blocks with seg < rc/16 are zero in X^T and are never stored)
-    const double* xrow = Db + (int64_t)I * TILE * TILE + rc * TILE + 16 * seg;
+    // alpha_I[c] = (X_I^T v)[c] = sum_i X[i][c] v[i].  Dinv holds the lower blocks of X
+    // transposed (block (q, jb) stores X_{q,jb}^T), so thread (c, seg) reads row c%16 of
+    // block (seg, c/16) -- 16 contiguous i -- which exists iff seg >= c/16.
     double s2[NTR] = {};
     if (seg >= (rc >> 4)) {
+      const double* xb = Db + (int64_t)I * NPACK * BLKD + pk(seg, rc >> 4) + (rc & 15) * NB;
+      const int sw = (rc >> 1) & 7;   // bo(): 16-B chunk m of the row holds columns 2(m ^ sw), +1
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const v2d x = *reinterpret_cast<const v2d*>(xrow + 2 * e);
+      for (int m = 0; m < 8; ++m) {
+        const v2d x = *reinterpret_cast<const v2d*>(xb + 2 * m);
+        const int i0 = 16 * seg + 2 * (m ^ sw);
 #pragma unroll
-        for (int tr = 0; tr < NTR; ++tr) s2[tr] += x[0] * vsh[tr][16 * seg + 2 * e] + x[1] * vsh[tr][16 * seg + 2 * e + 1];
+        for (int tr = 0; tr < NTR; ++tr) s2[tr] += x[0] * vsh[tr][i0] + x[1] * vsh[tr][i0 + 1];
       }
     }
 #pragma unroll

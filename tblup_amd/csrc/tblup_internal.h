@@ -21,7 +21,7 @@
 //     u      f64  [B][prow]            centring sums (dual: u_i = sum_s m_s a_is; primal: s_a)
 //     scal   f64  [B][16]              see SC_* below
 //     L      f64  [B][NT][NT][128^2]   Lt tiles (tile (I,J) holds L_IJ^T)
-//     Dinv   f64  [B][NT][128][128]    X^T of each diagonal tile, X = L_JJ^{-1}
+//     Dinv   f64  [B][NT][36][16x16]   X = L_JJ^{-1} of each diagonal tile, packed lower blocks
 //     z      f64  [B][ns]              L^{-1} rhs
 //     fit    f64  [B]
 #pragma once
@@ -79,6 +79,16 @@ struct EvalDims {
   int nt;           // traits
 };
 
+// ---- packed lower-triangular 16x16 block storage of a 128x128 tile (LDS and Dinv) ----
+constexpr int NB = 16;                       // base block edge
+constexpr int NBLK = TILE / NB;              // 8 block rows
+constexpr int NPACK = NBLK * (NBLK + 1) / 2; // 36 lower blocks
+constexpr int BLKD = NB * NB;                // doubles per block
+
+__host__ __device__ __forceinline__ int pk(int q, int s) { return (q * (q + 1) / 2 + s) * BLKD; }
+// element (r, c) of a 16x16 block; 16-B chunk swizzle makes the fragment reads conflict-free
+__host__ __device__ __forceinline__ int bo(int r, int c) { return r * NB + 2 * ((c >> 1) ^ ((r >> 1) & 7)) + (c & 1); }
+
 // ---- launchers (k_prep.hip) ----
 hipError_t launch_transpose_geno(const int8_t* src, int8_t* dst, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, int64_t P, hipStream_t s);
@@ -105,7 +115,7 @@ struct CholLaunch {
   SysDims sd;
   int64_t B;
   double* L;             // Lt tiles [B][NT][NT][128*128] (tile (I,J) holds L_IJ^T)
-  double* Dinv;          // [B][NT][128][128]
+  double* Dinv;          // [B][NT][NPACK*BLKD] X = L_JJ^{-1}, packed lower 16x16 blocks
   double* z;             // [B][nt][ns]
   double* w;             // [B][nt][ns] forward-substitution partial sums
   const double* rhs;     // [B][nt][ns] primal right-hand sides (dual: y_T - mu on the fly)
