@@ -71,95 +71,6 @@ __device__ __forceinline__ void glds_lt_stage(const double* __restrict__ src, do
 __device__ __forceinline__ int i8off_a(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
 __device__ __forceinline__ int i8off_b(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 2)); }
 
-// Sources are per lane (rows 16(2w+e) + (l>>2), chunk l&3, swizzle applied), stage kb at + kb*kstep.
-__device__ __forceinline__ int i8_tt_row(int e) { return (2 * (threadIdx.x >> 6) + e) * 16 + ((threadIdx.x & 63) >> 2); }
-
-template <int D>
-__device__ __forceinline__ void i8_tt(const int8_t* const (&sa)[2], const int8_t* const (&sb)[2], int64_t nblk,
-                                      int64_t kstep, int8_t* lds, v4i (&cnt)[8][2]) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-#pragma unroll
-  for (int cb = 0; cb < 8; ++cb)
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = v4i{0, 0, 0, 0};
-  if (nblk <= 0) return;
-  constexpr int TB = TILE * KBLK;
-  auto issue = [&](int64_t kb) {
-    int8_t* slot = lds + (int)(kb % D) * 2 * TB;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int cblk = 2 * w + e;
-      __builtin_amdgcn_global_load_lds(sa[e] + kb * kstep, (lds_ptr_t)(slot + cblk * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(sb[e] + kb * kstep, (lds_ptr_t)(slot + TB + cblk * 1024), 16, 0, 0);
-    }
-  };
-  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
-  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    if (kb + D - 2 < nblk) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kb + D - 1 < nblk) issue(kb + D - 1);
-    const int8_t* As = lds + (int)(kb % D) * 2 * TB;
-    const int8_t* Bs = As + TB;
-    v4i bv[2];
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) bv[ib] = *reinterpret_cast<const v4i*>(Bs + i8off_b(32 * w + 16 * ib + rho, ch));
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
-      const v4i av = *reinterpret_cast<const v4i*>(As + i8off_a(16 * cb + prow, ch));
-#pragma unroll
-      for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[ib], cnt[cb][ib], 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-// Packed variant: stage kb = 64 animals = 16 B per row; rows of A (tile J) then B (tile I),
-// 4 KiB per stage, wave w loads rows 64(w&1)..+63 of operand w>>1.  src: this lane's row.
-template <int D>
-__device__ __forceinline__ void i8_tt_packed(const uint8_t* src, int64_t nblk, uint8_t* lds, v4i (&cnt)[8][2]) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-#pragma unroll
-  for (int cb = 0; cb < 8; ++cb)
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = v4i{0, 0, 0, 0};
-  if (nblk <= 0) return;
-  constexpr int SB = 2 * TILE * 16;   // 4 KiB per stage
-  auto issue = [&](int64_t kb) {
-    __builtin_amdgcn_global_load_lds(src + kb * 16, (lds_ptr_t)(lds + (int)(kb % D) * SB + w * 1024), 16, 0, 0);
-  };
-  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
-  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    if (kb + D - 2 < nblk) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 2) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kb + D - 1 < nblk) issue(kb + D - 1);
-    const uint8_t* As = lds + (int)(kb % D) * SB;
-    const uint8_t* Bs = As + TILE * 16;
-    v4i bv[2];
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib)
-      bv[ib] = unpack16(*reinterpret_cast<const uint32_t*>(Bs + (32 * w + 16 * ib + rho) * 16 + 4 * ch));
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
-      const v4i av = unpack16(*reinterpret_cast<const uint32_t*>(As + (16 * cb + prow) * 16 + 4 * ch));
-#pragma unroll
-      for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[ib], cnt[cb][ib], 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
 // ---- GEMM1 of the off-diagonal kernel: acc[cb][ib] -= sum_{k < 128J} L_J[c][k] L_I[i][k] ----
 // A = Lt tiles (J, L), B = Lt tiles (I, L), L < J; LDS-DMA ring of D slots x 32 KiB.
 template <int D>
@@ -393,27 +304,6 @@ __device__ __forceinline__ const uint8_t* row_packed(const CholArgs& a, int64_t 
 // Each piece is written in the packed block layout the diagonal kernel factorises in,
 // so the diagonal kernel sums them with a linear sweep.
 // ---------------------------------------------------------------------------
-// S[b][Jt&1] = K_{Jt,Jt} - sum_{L < nterm} L_{Jt,L} L_{Jt,L}^T (packed blocks), by one
-// workgroup through the LDS-DMA stage ring.
-__device__ __forceinline__ void syrk_partial(const CholArgs& a, int64_t b, int Jt, int nterm, double* lds) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  v4d acc[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-  if (!(a.skip & 2)) syrk_lower<4>(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc);
-  const double* Kb = a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD;
-  double* Pd = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int e = w + 4 * i, q = tri_q(e), sb = tri_s(e);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o = pk(q, sb) + bo((l >> 4) + 4 * r, l & 15);
-      Pd[o] = Kb[o] - acc[i][r];
-    }
-  }
-}
-
 // K_JJ for every (individual, J): int8 MFMA tile, exact counts + fp64 centring, + lambda I,
 // identity on padded rows; packed lower 16x16 blocks into Kd[b][J].
 __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
@@ -471,20 +361,6 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
     }
 }
 
-// SYRK of 32 k rows of an Lt tile for the 9 packed blocks {W + 4i}, straight from global
-// (16 lanes read one 128-B row segment).
-template <int W>
-__device__ __forceinline__ void syrk_rows_global(const double* __restrict__ lt, int k0, v4d (&acc)[9], int l) {
-#pragma unroll 2
-  for (int kk = 0; kk < 8; ++kk) {
-    const int k = k0 + 4 * kk + (l >> 4);
-    double a8[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a8[q] = lt[k * TILE + 16 * q + (l & 15)];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) acc[i] = mfma64(a8[tri_q(W + 4 * i)], a8[tri_s(W + 4 * i)], acc[i]);
-  }
-}
 
 // ---------------------------------------------------------------------------
 // diagonal tile
@@ -671,6 +547,205 @@ __global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
 //   2. out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb]   (X = inv(L_JJ); acc is the B operand)
 //      -> Lt tile (I, J); w_I += L_IJ z_J
 // LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
+// ===========================================================================
+// Off-diagonal launch, 8 waves (512 threads) per workgroup, two workgroups per CU:
+// wave w owns the 16 columns i in [16w, 16w+16) of its tile; 16 waves per CU hide the
+// operand latency better than 8 (GEMM1 microbenchmark: 62 vs 58 TFLOP/s).
+// ===========================================================================
+constexpr int OW = 8;            // waves per off-diagonal workgroup
+constexpr int OTH = 64 * OW;     // threads
+
+// int8 tile, kernel form (gathered int8 panel): A = panel rows of tile J, B = tile I.
+// Stage kb = 8 KiB per operand; wave w loads 1 KiB chunk w of each (rows 16w..16w+15).
+template <int D>
+__device__ __forceinline__ void i8_tt8(const int8_t* sa, const int8_t* sb, int64_t nblk, int64_t kstep, int8_t* lds,
+                                       v4i (&cnt)[8]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
+  if (nblk <= 0) return;
+  constexpr int TB = TILE * KBLK;
+  auto issue = [&](int64_t kb) {
+    int8_t* slot = lds + (int)(kb % D) * 2 * TB;
+    __builtin_amdgcn_global_load_lds(sa + kb * kstep, (lds_ptr_t)(slot + w * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(sb + kb * kstep, (lds_ptr_t)(slot + TB + w * 1024), 16, 0, 0);
+  };
+  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    if (kb + D - 2 < nblk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kb + D - 1 < nblk) issue(kb + D - 1);
+    const int8_t* As = lds + (int)(kb % D) * 2 * TB;
+    const int8_t* Bs = As + TB;
+    const v4i bv = *reinterpret_cast<const v4i*>(Bs + i8off_b(16 * w + rho, ch));
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const v4i av = *reinterpret_cast<const v4i*>(As + i8off_a(16 * cb + prow, ch));
+      cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cnt[cb], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// int8 tile, SNP form (2-bit packed rows in place): 4 KiB stages (A rows then B rows);
+// waves 0-3 load (row 64(w&1) + l of operand w>>1), waves 4-7 only compute.
+template <int D>
+__device__ __forceinline__ void i8_tt8_packed(const uint8_t* src, int64_t nblk, uint8_t* lds, v4i (&cnt)[8]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
+  if (nblk <= 0) return;
+  constexpr int SB = 2 * TILE * 16;
+  auto issue = [&](int64_t kb) {
+    if (w < 4) __builtin_amdgcn_global_load_lds(src + kb * 16, (lds_ptr_t)(lds + (int)(kb % D) * SB + w * 1024), 16, 0, 0);
+  };
+  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    if (w < 4) {
+      if (kb + D - 2 < nblk) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 2) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kb + D - 1 < nblk) issue(kb + D - 1);
+    const uint8_t* As = lds + (int)(kb % D) * SB;
+    const uint8_t* Bs = As + TILE * 16;
+    const v4i bv = unpack16(*reinterpret_cast<const uint32_t*>(Bs + (16 * w + rho) * 16 + 4 * ch));
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const v4i av = unpack16(*reinterpret_cast<const uint32_t*>(As + (16 * cb + prow) * 16 + 4 * ch));
+      cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cnt[cb], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Lt stage (16 k rows x 1 KiB) loaded by 8 waves: rows 2w, 2w+1.
+__device__ __forceinline__ void glds_lt_stage8w(const double* __restrict__ src, double* stage) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int k = 2 * w + e;
+    __builtin_amdgcn_global_load_lds(src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(stage + k * TILE), 16, 0,
+                                     0);
+  }
+}
+
+// GEMM1: acc[cb] -= sum_{k < 128J} L_J[c][k] L_I[i][k] for the wave's 16 columns i.
+template <int D>
+__device__ __forceinline__ void gemm1_tt8(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
+                                          double* lds, v4d (&acc)[8]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nst = 8 * J;
+  if (nst == 0) return;
+  auto issue = [&](int s) {
+    double* slot = lds + (s % D) * 2 * LTS;
+    const int64_t src = (int64_t)(s >> 3) * TT + (s & 7) * LTS;
+    glds_lt_stage8w(ltJ + src, slot);
+    glds_lt_stage8w(ltI + src, slot + LTS);
+  };
+  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    if (s + D - 2 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + D - 1 < nst) issue(s + D - 1);
+    const double* As = lds + (s % D) * 2 * LTS;
+    const double* Bs = As + LTS;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * kk + (l >> 4);
+      const double bv = Bs[lt_off(k, 16 * w + (l & 15))];
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) acc[cb] = mfma64_nega(As[lt_off(k, 16 * cb + (l & 15))], bv, acc[cb]);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// SYRK of Lt stages restricted to the 36 lower blocks, 8 waves: wave W takes blocks
+// W + 8i (5 blocks for W < 4, 4 for W >= 4).
+template <int W>
+__device__ __forceinline__ void syrk_stage8(const double* As, v4d (&acc)[5], int l) {
+  constexpr int NBW = (W < 4) ? 5 : 4;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 4 * kk + (l >> 4);
+    double a8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a8[q] = As[lt_off(k, 16 * q + (l & 15))];
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) acc[i] = mfma64(a8[tri_q(W + 8 * i)], a8[tri_s(W + 8 * i)], acc[i]);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void syrk_lower8(const double* __restrict__ src, int nst, double* lds, v4d (&acc)[5]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (nst <= 0) return;
+  auto issue = [&](int s) { glds_lt_stage8w(src + (int64_t)s * LTS, lds + (s % D) * LTS); };
+  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    if (s + D - 2 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + D - 1 < nst) issue(s + D - 1);
+    const double* As = lds + (s % D) * LTS;
+    switch (w) {
+      case 0: syrk_stage8<0>(As, acc, l); break;
+      case 1: syrk_stage8<1>(As, acc, l); break;
+      case 2: syrk_stage8<2>(As, acc, l); break;
+      case 3: syrk_stage8<3>(As, acc, l); break;
+      case 4: syrk_stage8<4>(As, acc, l); break;
+      case 5: syrk_stage8<5>(As, acc, l); break;
+      case 6: syrk_stage8<6>(As, acc, l); break;
+      default: syrk_stage8<7>(As, acc, l); break;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// S[b][Jt&1] = K_{Jt,Jt} - sum_{L < nterm} L_{Jt,L} L_{Jt,L}^T (packed blocks), 8 waves.
+__device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int Jt, int nterm, double* lds) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v4d acc[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
+  if (!(a.skip & 2)) syrk_lower8<4>(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc);
+  const double* Kb = a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD;
+  double* Pd = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int e = w + 8 * i;
+    if (e < NPACK) {
+      const int q = tri_q_rt(e), sb = e - q * (q + 1) / 2;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = pk(q, sb) + bo((l >> 4) + 4 * r, l & 15);
+        Pd[o] = Kb[o] - acc[i][r];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I, double* lds, double* uj_sh,
                                              double* ui_sh, double (*zj_sh)[TILE]) {
@@ -691,105 +766,86 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   }
   __syncthreads();
 
-  v4d acc[8][2];
+  // 0. K_JI on int8 MFMA (16x16x64, rows permuted so the counts land in the f64 layout)
+  v4d acc[8];
   {
-    v4i cnt[8][2];
+    v4i cnt[8];
     const int64_t nblk = (int64_t)sc[SC_CBLK];
     if (!(a.skip & 32) && a.form == FORM_PRIMAL) {
-      // wave w loads rows 64(w&1) + l of tile J (w < 2) or tile I (w >= 2)
-      i8_tt_packed<16>(row_packed(a, b, ((w >> 1) ? i0 : j0) + 64 * (w & 1) + l), nblk,
-                       reinterpret_cast<uint8_t*>(lds), cnt);
+      i8_tt8_packed<16>(row_packed(a, b, ((w >> 1) & 1 ? i0 : j0) + 64 * (w & 1) + l), nblk,
+                        reinterpret_cast<uint8_t*>(lds), cnt);
     } else if (!(a.skip & 32)) {
-      const int8_t *sa[2], *sb[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int row = i8_tt_row(e), pos = l & 3;
-        sa[e] = row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3));
-        sb[e] = row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2));
-      }
-      i8_tt<4>(sa, sb, nblk, a.prow * KBLK, reinterpret_cast<int8_t*>(lds),
-               cnt);
+      const int row = 16 * w + (l >> 2), pos = l & 3;
+      i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
+                row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, a.prow * KBLK,
+                reinterpret_cast<int8_t*>(lds), cnt);
     } else {
 #pragma unroll
-      for (int cb = 0; cb < 8; ++cb)
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) cnt[cb][ib] = v4i{0, 0, 0, 0};
+      for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
     }
+    const int il = 16 * w + (l & 15);
+    const bool ireal = i0 + il < nrow;
 #pragma unroll
-    for (int cb = 0; cb < 8; ++cb)
+    for (int cb = 0; cb < 8; ++cb) {
 #pragma unroll
-      for (int ib = 0; ib < 2; ++ib) {
-        const int il = 32 * w + 16 * ib + (l & 15);
-        const bool ireal = i0 + il < nrow;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cl = 16 * cb + (l >> 4) + 4 * r;
-          const double v = grm_value(cnt[cb][ib][r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
-          acc[cb][ib][r] = (ireal && j0 + cl < nrow) ? v : 0.0;
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int cl = 16 * cb + (l >> 4) + 4 * r;
+        const double v = grm_value(cnt[cb][r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
+        acc[cb][r] = (ireal && j0 + cl < nrow) ? v : 0.0;
       }
+    }
   }
 
   // 1. T^T = K_JI - sum_L L_JL L_IL^T
-  if (J > 0 && !(a.skip & 64)) gemm1_tt<2>(Lb + (int64_t)J * NT * TT, Lb + (int64_t)I * NT * TT, J, lds, acc);
+  if (J > 0 && !(a.skip & 64)) gemm1_tt8<2>(Lb + (int64_t)J * NT * TT, Lb + (int64_t)I * NT * TT, J, lds, acc);
 
   // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X in the
   //    packed block layout (blocks transposed): all 36 blocks (72 KiB) land in LDS in one
-  //    LDS-DMA burst, then
-  //    the 8 block rows run without further waits.
+  //    LDS-DMA burst, then the 8 block rows run without further waits.
   double* Lout = const_cast<double*>(Lb) + ((int64_t)I * NT + J) * TT;
   double* xl = lds;
   {
     const double* Xg = a.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
 #pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread
-      const int chunk = (e * 4 + w) * 64;
+    for (int e = 0; e < NPACK * BLKD / 2 / OTH; ++e) {   // 9 x 16 B per thread
+      const int chunk = (e * OW + w) * 64;
       __builtin_amdgcn_global_load_lds(Xg + 2 * (chunk + l), (lds_ptr_t)(xl + 2 * chunk), 16, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  double wacc[MAXT][2] = {};
+  double wacc[MAXT] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
   for (int jb = 0; jb < NBLK; ++jb) {
-    v4d o[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+    v4d o = {0.0, 0.0, 0.0, 0.0};
     if (!(a.skip & 128)) {
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) {
         if (cb <= jb) {
           const double* xb = xl + pk(jb, cb);
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk) {
-            const double av = xb[bo(4 * kk + (l >> 4), l & 15)];   // X_{jb,cb}[l&15][k], stored transposed
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib) o[ib] = mfma64(av, acc[cb][ib][kk], o[ib]);
-          }
+          for (int kk = 0; kk < 4; ++kk) o = mfma64(xb[bo(4 * kk + (l >> 4), l & 15)], acc[cb][kk], o);
         }
       }
     }
 #pragma unroll
-    for (int ib = 0; ib < 2; ++ib)
+    for (int r = 0; r < 4; ++r) {
+      const int jl = 16 * jb + (l >> 4) + 4 * r, il = 16 * w + (l & 15);
+      Lout[jl * TILE + il] = o[r];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int jl = 16 * jb + (l >> 4) + 4 * r, il = 32 * w + 16 * ib + (l & 15);
-        Lout[jl * TILE + il] = o[ib][r];
-#pragma unroll
-        for (int tr = 0; tr < MAXT; ++tr) wacc[tr][ib] += o[ib][r] * zj_sh[tr][jl];
-      }
+      for (int tr = 0; tr < MAXT; ++tr) wacc[tr] += o[r] * zj_sh[tr][jl];
+    }
   }
   // w_I[i] += sum_j L_IJ[i][j] z_J[j]: reduce the 4 lane groups that share a column i
 #pragma unroll
   for (int tr = 0; tr < MAXT; ++tr) {
     if (tr < a.nt) {
-#pragma unroll
-      for (int ib = 0; ib < 2; ++ib) {
-        double v = wacc[tr][ib];
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if ((l >> 4) == 0) {
-          const int64_t gi = (b * a.nt + tr) * ns + i0 + 32 * w + 16 * ib + l;
-          a.w[gi] = (J == 0) ? v : a.w[gi] + v;
-        }
+      double v = wacc[tr];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if ((l >> 4) == 0) {
+        const int64_t gi = (b * a.nt + tr) * ns + i0 + 16 * w + l;
+        a.w[gi] = (J == 0) ? v : a.w[gi] + v;
       }
     }
   }
@@ -799,12 +855,12 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
 // overlap the tiles) one workgroup per individual preparing diagonal tile J+1 except its
 // L = J term: S[(J+1)&1] = K - sum_{L<J} (those tiles are final already).
 // LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
-__global__ __launch_bounds__(256, 2) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
+__global__ __launch_bounds__(OTH, 2) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
   __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
   __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
   const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
   if ((int64_t)blockIdx.x < n_extra) {
-    syrk_partial(a, blockIdx.x, a.J + 1, a.J, lds);
+    syrk_partial8(a, blockIdx.x, a.J + 1, a.J, lds);
     return;
   }
   const int64_t logical = xcd_remap(blockIdx.x - n_extra, n_tiles);
@@ -832,7 +888,7 @@ hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
   if (nI <= 0) return hipSuccess;
   a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;
   const int64_t n_tiles = c.B * nI;
-  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX)), dim3(256), 0, s, a, I0, nI, n_tiles);
+  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX)), dim3(OTH), 0, s, a, I0, nI, n_tiles);
   return hipGetLastError();
 }
 
