@@ -362,191 +362,9 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------
-// diagonal tile
-//   A. T = K_JJ - sum_{L<J} L_JL L_JL^T = Kd + partials; r = y_J - mu - w_J
-//   C. for panel p: one wave factors T_pp (-> L_pp, X_pp = L_pp^{-1});
-//      all waves: L_qp = T_qp X_pp^T (q > p); T_qs -= L_qp L_sp^T (q >= s > p)   [MFMA]
-//   D. blocked inverse X = L^{-1}: X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
-//      (off-diagonal X blocks written to / re-read from Dinv, diagonal ones stay in LDS)
-//   E. write L_JJ^T (Lt tile), X_J^T (Dinv, zeros below its diagonal), z_J = X_J r
-// ---------------------------------------------------------------------------
-// Diagonal tile J of individual b.  T = S - sum_{L0 <= L < J} L_JL L_JL^T where S is
-// K_JJ - sum_{L < L0} (the buffer slot J&1 left by an earlier off-diagonal launch) when
-// L0 > 0, else k_diag_grm's K_JJ.
-// LDS (lds >= 2 * NPACK * BLKD doubles = 144 KiB): Tp = T -> L (packed lower 16x16 blocks),
-// Xp = X = L^{-1} in the same packed layout; before the factorisation Xp's space is the
-// 64 KiB SYRK stage ring.  X never round-trips through global memory: Dinv receives X^T
-// once, at the end.
-__device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, int L0, double* lds,
-                                          double (*rsh)[TILE]) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int64_t ns = a.ns;
-  const int NT = a.NT;
-  const int64_t j0 = (int64_t)J * TILE;
-  const double* sc = a.scal + b * SCAL;
-  const double muf = sc[SC_MUF];
-  const int64_t nrow = (int64_t)sc[SC_NROW];
-  const int nt = a.nt;
-  double* Tp = lds;
-  double* Xp = lds + NPACK * BLKD;
+constexpr int DW = 8;            // waves per diagonal workgroup
+constexpr int DTHR = 64 * DW;
 
-  // T = S - sum_{L0 <= L < J} L_JL L_JL^T: S by LDS-DMA, the SYRK through the stage ring
-  {
-    const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
-                                  : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
-#pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / 256; ++e) {   // 18 x 16 B per thread
-      const int chunk = (e * 4 + w) * 64;
-      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
-    }
-    if (J > L0 && !(a.skip & 2)) {
-      v4d acc[9];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-      // waits for all its stages (and the older S loads) and ends in a barrier
-      syrk_lower<4>(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const int e = w + 4 * i;
-        double* blk = Tp + pk(tri_q(e), tri_s(e));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) blk[bo((l >> 4) + 4 * r, l & 15)] -= acc[i][r];
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  if (t < TILE) {
-    const int64_t gi = j0 + t;
-#pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr) {
-      if (tr < nt) {
-        const int64_t o = (b * nt + tr) * ns + gi;
-        const double wv = (J > 0) ? a.w[o] : 0.0;
-        const double rv = (a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ymu[tr];
-        rsh[tr][t] = (gi < nrow) ? (rv - wv) : 0.0;
-      } else {
-        rsh[tr][t] = 0.0;
-      }
-    }
-  }
-  __syncthreads();
-
-  // C. blocked right-looking factorisation over 16-column panels, with a one-block
-  //    look-ahead: wave 0 updates diagonal block p+1 first and factors it while waves 1-3
-  //    finish the rest of step p's trailing update.
-  if (!(a.skip & 4)) {
-    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(0, 0), Xp + pk(0, 0), l);
-    __syncthreads();
-  }
-  for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
-    for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += 4) {
-      v4d x = {0.0, 0.0, 0.0, 0.0};
-      x = mma_abt(Tp + pk(q, p), Xp + pk(p, p), x, l);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
-    }
-    __syncthreads();
-    if (p + 1 == NBLK) break;
-    const int nb = NBLK - 1 - p;
-    if (w == 0) {
-      if (!(a.skip & 512)) {
-        v4d x = {0.0, 0.0, 0.0, 0.0};
-        x = mma_abt(Tp + pk(p + 1, p), Tp + pk(p + 1, p), x, l);
-        double* dst = Tp + pk(p + 1, p + 1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
-      }
-      if (!(a.skip & 256)) factor16(Tp + pk(p + 1, p + 1), Xp + pk(p + 1, p + 1), l);
-    } else {
-      // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over waves 1-3
-      for (int e = w; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += 3) {
-        int qq = 0;
-        while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
-        const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
-        v4d x = {0.0, 0.0, 0.0, 0.0};
-        x = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), x, l);
-        double* dst = Tp + pk(q, sb);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
-      }
-    }
-    __syncthreads();
-  }
-  if (a.skip & 16) return;
-
-  // D. blocked inverse in LDS, one block diagonal per round:
-  //    X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
-  for (int dd = 1; dd < ((a.skip & 8) ? 0 : NBLK); ++dd) {
-    for (int jb = w; jb + dd < NBLK; jb += 4) {
-      const int q = jb + dd;
-      v4d sacc = {0.0, 0.0, 0.0, 0.0};
-      for (int lb = jb; lb < q; ++lb) {
-        const double* A = Tp + pk(q, lb);
-        const double* B = Xp + pk(lb, jb);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int k = 4 * kk + (l >> 4);
-          sacc = mfma64(A[bo(l & 15, k)], B[bo(k, l & 15)], sacc);
-        }
-      }
-      v4d xo = {0.0, 0.0, 0.0, 0.0};
-      const double* Xqq = Xp + pk(q, q);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) xo = mfma64_nega(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
-      double* dst = Xp + pk(q, jb);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] = xo[r];
-    }
-    __syncthreads();
-  }
-
-  // E. X into Dinv as packed lower blocks, each block transposed (block (q, jb) holds
-  //    X_{q,jb}^T in the bo() layout), z_J = X r, and L_JJ^T only for the debug readback.
-  {
-    double* Xg = a.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
-    for (int e = t; e < NPACK * BLKD; e += 256) {   // linear (conflict-free) LDS reads
-      const int blk = e >> 8, o = e & 255, i = o >> 4;
-      const int cpos = o & 15, c = 2 * ((cpos >> 1) ^ ((i >> 1) & 7)) + (cpos & 1);   // o = bo(i, c)
-      Xg[blk * BLKD + bo(c, i)] = Xp[e];
-    }
-  }
-  if (a.skip & FLAG_WRITE_LJJ) {
-    double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
-    for (int e = t; e < TT; e += 256) {
-      const int rr = e >> 7, cc = e & 127;
-      Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
-    }
-  }
-  if (t < TILE) {
-    double acc_z[MAXT] = {0.0, 0.0, 0.0, 0.0};
-    const int qi = t >> 4, ii = t & 15;
-    for (int c = 0; c <= t; ++c) {
-      const double xc = Xp[pk(qi, c >> 4) + bo(ii, c & 15)];
-#pragma unroll
-      for (int tr = 0; tr < MAXT; ++tr) acc_z[tr] += xc * rsh[tr][c];
-    }
-#pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr)
-      if (tr < nt) a.z[(b * nt + tr) * ns + j0 + t] = acc_z[tr];
-  }
-}
-
-// Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
-// K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
-__global__ __launch_bounds__(256) void k_chol_diag(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
-  __shared__ double rsh[MAXT][TILE];
-  diag_tile(a, blockIdx.x, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
-}
-
-// ---------------------------------------------------------------------------
-// off-diagonal tiles of column J (one WG per individual x tile row I > J)
-//   0. cnt = A_J A_I^T on int8 MFMA, landing in the f64 layout; acc = K_JI = K_IJ^T
-//   1. acc -= sum_{L<J} L_JL L_IL^T          (acc = T^T, wave w holds all c x its 32 i)
-//   2. out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb]   (X = inv(L_JJ); acc is the B operand)
-//      -> Lt tile (I, J); w_I += L_IJ z_J
-// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
 // ===========================================================================
 // Off-diagonal launch, 8 waves (512 threads) per workgroup, two workgroups per CU:
 // wave w owns the 16 columns i in [16w, 16w+16) of its tile; 16 waves per CU hide the
@@ -747,6 +565,195 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
 }
 
 // ---------------------------------------------------------------------------
+// diagonal tile
+//   A. T = K_JJ - sum_{L<J} L_JL L_JL^T = Kd + partials; r = y_J - mu - w_J
+//   C. for panel p: one wave factors T_pp (-> L_pp, X_pp = L_pp^{-1});
+//      all waves: L_qp = T_qp X_pp^T (q > p); T_qs -= L_qp L_sp^T (q >= s > p)   [MFMA]
+//   D. blocked inverse X = L^{-1}: X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
+//      (off-diagonal X blocks written to / re-read from Dinv, diagonal ones stay in LDS)
+//   E. write L_JJ^T (Lt tile), X_J^T (Dinv, zeros below its diagonal), z_J = X_J r
+// ---------------------------------------------------------------------------
+// Diagonal tile J of individual b.  T = S - sum_{L0 <= L < J} L_JL L_JL^T where S is
+// K_JJ - sum_{L < L0} (the buffer slot J&1 left by an earlier off-diagonal launch) when
+// L0 > 0, else k_diag_grm's K_JJ.
+// LDS (lds >= 2 * NPACK * BLKD doubles = 144 KiB): Tp = T -> L (packed lower 16x16 blocks),
+// Xp = X = L^{-1} in the same packed layout; before the factorisation Xp's space is the
+// 64 KiB SYRK stage ring.  X never round-trips through global memory: Dinv receives X^T
+// once, at the end.
+__device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, int L0, double* lds,
+                                          double (*rsh)[TILE]) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int64_t ns = a.ns;
+  const int NT = a.NT;
+  const int64_t j0 = (int64_t)J * TILE;
+  const double* sc = a.scal + b * SCAL;
+  const double muf = sc[SC_MUF];
+  const int64_t nrow = (int64_t)sc[SC_NROW];
+  const int nt = a.nt;
+  double* Tp = lds;
+  double* Xp = lds + NPACK * BLKD;
+
+  // T = S - sum_{L0 <= L < J} L_JL L_JL^T: S by LDS-DMA, the SYRK through the stage ring
+  {
+    const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
+                                  : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
+#pragma unroll
+    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
+      const int chunk = (e * DW + w) * 64;
+      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
+    }
+    if (J > L0 && !(a.skip & 2)) {
+      v4d acc[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
+      // waits for all its stages (and the older S loads) and ends in a barrier
+      syrk_lower8<4>(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int e = w + DW * i;
+        if (e < NPACK) {
+          const int q = tri_q_rt(e);
+          double* blk = Tp + pk(q, e - q * (q + 1) / 2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) blk[bo((l >> 4) + 4 * r, l & 15)] -= acc[i][r];
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (t < TILE) {
+    const int64_t gi = j0 + t;
+#pragma unroll
+    for (int tr = 0; tr < MAXT; ++tr) {
+      if (tr < nt) {
+        const int64_t o = (b * nt + tr) * ns + gi;
+        const double wv = (J > 0) ? a.w[o] : 0.0;
+        const double rv = (a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ymu[tr];
+        rsh[tr][t] = (gi < nrow) ? (rv - wv) : 0.0;
+      } else {
+        rsh[tr][t] = 0.0;
+      }
+    }
+  }
+  __syncthreads();
+
+  // C. blocked right-looking factorisation over 16-column panels, with a one-block
+  //    look-ahead: wave 0 updates diagonal block p+1 first and factors it while waves 1-3
+  //    finish the rest of step p's trailing update.
+  if (!(a.skip & 4)) {
+    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(0, 0), Xp + pk(0, 0), l);
+    __syncthreads();
+  }
+  for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
+    for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += DW) {
+      v4d x = {0.0, 0.0, 0.0, 0.0};
+      x = mma_abt(Tp + pk(q, p), Xp + pk(p, p), x, l);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
+    }
+    __syncthreads();
+    if (p + 1 == NBLK) break;
+    const int nb = NBLK - 1 - p;
+    if (w == 0) {
+      if (!(a.skip & 512)) {
+        v4d x = {0.0, 0.0, 0.0, 0.0};
+        x = mma_abt(Tp + pk(p + 1, p), Tp + pk(p + 1, p), x, l);
+        double* dst = Tp + pk(p + 1, p + 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
+      }
+      if (!(a.skip & 256)) factor16(Tp + pk(p + 1, p + 1), Xp + pk(p + 1, p + 1), l);
+    } else {
+      // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over waves 1-3
+      for (int e = w; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += DW - 1) {
+        int qq = 0;
+        while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
+        const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
+        v4d x = {0.0, 0.0, 0.0, 0.0};
+        x = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), x, l);
+        double* dst = Tp + pk(q, sb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
+      }
+    }
+    __syncthreads();
+  }
+  if (a.skip & 16) return;
+
+  // D. blocked inverse in LDS, one block diagonal per round:
+  //    X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
+  for (int dd = 1; dd < ((a.skip & 8) ? 0 : NBLK); ++dd) {
+    for (int jb = w; jb + dd < NBLK; jb += DW) {
+      const int q = jb + dd;
+      v4d sacc = {0.0, 0.0, 0.0, 0.0};
+      for (int lb = jb; lb < q; ++lb) {
+        const double* A = Tp + pk(q, lb);
+        const double* B = Xp + pk(lb, jb);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * kk + (l >> 4);
+          sacc = mfma64(A[bo(l & 15, k)], B[bo(k, l & 15)], sacc);
+        }
+      }
+      v4d xo = {0.0, 0.0, 0.0, 0.0};
+      const double* Xqq = Xp + pk(q, q);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) xo = mfma64_nega(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
+      double* dst = Xp + pk(q, jb);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] = xo[r];
+    }
+    __syncthreads();
+  }
+
+  // E. X into Dinv as packed lower blocks, each block transposed (block (q, jb) holds
+  //    X_{q,jb}^T in the bo() layout), z_J = X r, and L_JJ^T only for the debug readback.
+  {
+    double* Xg = a.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
+    for (int e = t; e < NPACK * BLKD; e += DTHR) {   // linear (conflict-free) LDS reads
+      const int blk = e >> 8, o = e & 255, i = o >> 4;
+      const int cpos = o & 15, c = 2 * ((cpos >> 1) ^ ((i >> 1) & 7)) + (cpos & 1);   // o = bo(i, c)
+      Xg[blk * BLKD + bo(c, i)] = Xp[e];
+    }
+  }
+  if (a.skip & FLAG_WRITE_LJJ) {
+    double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
+    for (int e = t; e < TT; e += DTHR) {
+      const int rr = e >> 7, cc = e & 127;
+      Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
+    }
+  }
+  if (t < TILE) {
+    double acc_z[MAXT] = {0.0, 0.0, 0.0, 0.0};
+    const int qi = t >> 4, ii = t & 15;
+    for (int c = 0; c <= t; ++c) {
+      const double xc = Xp[pk(qi, c >> 4) + bo(ii, c & 15)];
+#pragma unroll
+      for (int tr = 0; tr < MAXT; ++tr) acc_z[tr] += xc * rsh[tr][c];
+    }
+#pragma unroll
+    for (int tr = 0; tr < MAXT; ++tr)
+      if (tr < nt) a.z[(b * nt + tr) * ns + j0 + t] = acc_z[tr];
+  }
+}
+
+// Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
+// K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
+__global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
+  __shared__ double rsh[MAXT][TILE];
+  diag_tile(a, blockIdx.x, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
+}
+
+// ---------------------------------------------------------------------------
+// off-diagonal tiles of column J (one WG per individual x tile row I > J)
+//   0. cnt = A_J A_I^T on int8 MFMA, landing in the f64 layout; acc = K_JI = K_IJ^T
+//   1. acc -= sum_{L<J} L_JL L_IL^T          (acc = T^T, wave w holds all c x its 32 i)
+//   2. out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb]   (X = inv(L_JJ); acc is the B operand)
+//      -> Lt tile (I, J); w_I += L_IJ z_J
+// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
+
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I, double* lds, double* uj_sh,
                                              double* ui_sh, double (*zj_sh)[TILE]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -877,7 +884,7 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
-  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
   return hipGetLastError();
 }
 
