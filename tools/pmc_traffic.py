@@ -22,7 +22,7 @@ def per_class(path, counter):
                 continue
             name = row["Kernel_Name"]
             for key, cls in CLASSES.items():
-                if "::" + key + "(" in name:
+                if "::" + key + "(" in name or "::" + key + "<" in name:
                     acc[cls].append(float(row["Counter_Value"]) * 1024.0)
     return acc
 
