@@ -456,7 +456,7 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
     for (int64_t i = 0; i < nV; ++i) yV[t * nV + i] = c->pheno[valid[i] * nt + t];
   }
   if (int rc = dev_alloc(c, sp->geno, (size_t)(c->P + 1) * sp->nRp)) return rc;
-  if (int rc = dev_alloc(c, sp->gpk, (size_t)(c->P + 1) * (sp->nRp / 4))) return rc;
+  if (int rc = dev_alloc(c, sp->gpk, (size_t)(c->P + 1) * (sp->nRp / 4) + 64)) return rc;
   if (int rc = dev_alloc(c, sp->colsumT, (size_t)c->P * 4)) return rc;
   if (int rc = dev_alloc(c, sp->xty, (size_t)nt * c->P * 8)) return rc;
   if (int rc = dev_alloc(c, sp->yT, yT.size() * 8)) return rc;

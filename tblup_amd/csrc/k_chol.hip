@@ -448,6 +448,60 @@ __device__ __forceinline__ void i8_tt8_packed(const uint8_t* src, int64_t nblk, 
   __syncthreads();
 }
 
+// SNP form, 64-B stages: stage st = 256 animals = 64 B of each packed row, loaded and laid
+// out exactly like the int8 panel stages of i8_tt8 (rows of 4 swizzled 16-B chunks; every
+// 128-B line of a row is consumed by two consecutive stages instead of eight 16-B pieces).
+// Lane (rho, ch) reads one 16-B chunk = 4 packed dwords and feeds dword s to k-step s, so
+// the four lane groups x four k-steps cover the 16 dwords once (animal order inside a
+// stage is immaterial to the counts; A and B use the same order).  A stage past the
+// training block (nblk = 64-animal blocks, nblk % 4 != 0) zeroes chunks ch >= nblk % 4.
+template <int D>
+__device__ __forceinline__ void i8_tt8_pk64(const uint8_t* sa, const uint8_t* sb, int64_t nblk, uint8_t* lds,
+                                            v4i (&cnt)[8]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
+  if (nblk <= 0) return;
+  const int64_t nst = (nblk + 3) >> 2;
+  constexpr int TB = TILE * 64;
+  auto issue = [&](int64_t st) {
+    uint8_t* slot = lds + (int)(st % D) * 2 * TB;
+    __builtin_amdgcn_global_load_lds(sa + st * 64, (lds_ptr_t)(slot + w * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(sb + st * 64, (lds_ptr_t)(slot + TB + w * 1024), 16, 0, 0);
+  };
+  for (int64_t st = 0; st < D - 1 && st < nst; ++st) issue(st);
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  const int tail_ch = (int)(nblk & 3);
+  for (int64_t st = 0; st < nst; ++st) {
+    if (st + D - 2 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (st + D - 1 < nst) issue(st + D - 1);
+    const uint8_t* As = lds + (int)(st % D) * 2 * TB;
+    const uint8_t* Bs = As + TB;
+    uint4 bq = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * w + rho, ch));
+    if (st == nst - 1 && tail_ch != 0 && ch >= tail_ch) bq = uint4{0u, 0u, 0u, 0u};
+    uint4 aq[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) aq[cb] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * cb + prow, ch));
+    const uint32_t bw[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const v4i bv = unpack16(bw[s4]);
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        const uint32_t aw = s4 == 0 ? aq[cb].x : s4 == 1 ? aq[cb].y : s4 == 2 ? aq[cb].z : aq[cb].w;
+        cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(unpack16(aw), bv, cnt[cb], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // Lt stage (16 k rows x 1 KiB) loaded by 8 waves: rows 2w, 2w+1.
 __device__ __forceinline__ void glds_lt_stage8w(const double* __restrict__ src, double* stage) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -779,8 +833,10 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
     v4i cnt[8];
     const int64_t nblk = (int64_t)sc[SC_CBLK];
     if (!(a.skip & 32) && a.form == FORM_PRIMAL) {
-      i8_tt8_packed<16>(row_packed(a, b, ((w >> 1) & 1 ? i0 : j0) + 64 * (w & 1) + l), nblk,
-                        reinterpret_cast<uint8_t*>(lds), cnt);
+      const int row = 16 * w + (l >> 2), pos = l & 3;
+      i8_tt8_pk64<4>(row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
+                     row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk,
+                     reinterpret_cast<uint8_t*>(lds), cnt);
     } else if (!(a.skip & 32)) {
       const int row = 16 * w + (l >> 2), pos = l & 3;
       i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
