@@ -310,8 +310,9 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
   __shared__ __attribute__((aligned(16))) int8_t lds[8 * TILE * KBLK];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
   const int NT = a.NT;
-  const int64_t b = blockIdx.x / NT;
-  const int J = (int)(blockIdx.x % NT);
+  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
+  const int64_t b = lg / NT;
+  const int J = (int)(lg % NT);
   const int64_t j0 = (int64_t)J * TILE;
   const double* sc = a.scal + b * SCAL;
   const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
@@ -364,6 +365,7 @@ __global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
 
 constexpr int DW = 8;            // waves per diagonal workgroup
 constexpr int DTHR = 64 * DW;
+static_assert(DTHR == 4 * TILE, "diag z: four lanes per row");
 
 // ===========================================================================
 // Off-diagonal launch, 8 waves (512 threads) per workgroup, two workgroups per CU:
@@ -777,17 +779,23 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
     }
   }
-  if (t < TILE) {
+  // z_J[i] = sum_{c <= i} X[i][c] r[c]: four lanes per row (c = q mod 4), shuffle-reduced
+  {
+    const int i = t >> 2, q = t & 3;
     double acc_z[MAXT] = {0.0, 0.0, 0.0, 0.0};
-    const int qi = t >> 4, ii = t & 15;
-    for (int c = 0; c <= t; ++c) {
+    const int qi = i >> 4, ii = i & 15;
+    for (int c = q; c <= i; c += 4) {
       const double xc = Xp[pk(qi, c >> 4) + bo(ii, c & 15)];
 #pragma unroll
       for (int tr = 0; tr < MAXT; ++tr) acc_z[tr] += xc * rsh[tr][c];
     }
 #pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr)
-      if (tr < nt) a.z[(b * nt + tr) * ns + j0 + t] = acc_z[tr];
+    for (int tr = 0; tr < MAXT; ++tr) {
+      double v = acc_z[tr];
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      if (q == 0 && tr < nt) a.z[(b * nt + tr) * ns + j0 + i] = v;
+    }
   }
 }
 
@@ -796,7 +804,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
   __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
   __shared__ double rsh[MAXT][TILE];
-  diag_tile(a, blockIdx.x, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
+  // individual b on the XCD that runs its off-diagonal tiles (same L2 for L, S, X, w)
+  diag_tile(a, xcd_remap(blockIdx.x, gridDim.x), a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
 }
 
 // ---------------------------------------------------------------------------
@@ -923,7 +932,7 @@ __global__ __launch_bounds__(OTH, 2) void k_chol_offdiag(CholArgs a, int I0, int
   __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
   const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
   if ((int64_t)blockIdx.x < n_extra) {
-    syrk_partial8(a, blockIdx.x, a.J + 1, a.J, lds);
+    syrk_partial8(a, xcd_remap(blockIdx.x, n_extra), a.J + 1, a.J, lds);
     return;
   }
   const int64_t logical = xcd_remap(blockIdx.x - n_extra, n_tiles);

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   double* alpha = dyn;
   double* eall = dyn + nt * ns;
   const int t = threadIdx.x;
-  const int64_t b = blockIdx.x;
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);   // the XCD that factorised it
   const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
   const double* Db = c.Dinv + b * (int64_t)NT * NPACK * BLKD;
   const double* sc = c.scal + b * SCAL;
