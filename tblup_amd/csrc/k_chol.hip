@@ -629,6 +629,28 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
 //      (off-diagonal X blocks written to / re-read from Dinv, diagonal ones stay in LDS)
 //   E. write L_JJ^T (Lt tile), X_J^T (Dinv, zeros below its diagonal), z_J = X_J r
 // ---------------------------------------------------------------------------
+// X block (q, jb), q > jb, of X = L^{-1}: X_{q,jb} = -X_qq sum_{lb=jb}^{q-1} L_{q,lb} X_{lb,jb}
+// (needs L row q and X rows jb..q-1, X_qq); one wave.
+__device__ __forceinline__ void xinv_block(const double* Tp, double* Xp, int q, int jb, int l) {
+  v4d sacc = {0.0, 0.0, 0.0, 0.0};
+  for (int lb = jb; lb < q; ++lb) {
+    const double* A = Tp + pk(q, lb);
+    const double* B = Xp + pk(lb, jb);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * kk + (l >> 4);
+      sacc = mfma64(A[bo(l & 15, k)], B[bo(k, l & 15)], sacc);
+    }
+  }
+  v4d xo = {0.0, 0.0, 0.0, 0.0};
+  const double* Xqq = Xp + pk(q, q);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) xo = mfma64_nega(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
+  double* dst = Xp + pk(q, jb);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] = xo[r];
+}
+
 // Diagonal tile J of individual b.  T = S - sum_{L0 <= L < J} L_JL L_JL^T where S is
 // K_JJ - sum_{L < L0} (the buffer slot J&1 left by an earlier off-diagonal launch) when
 // L0 > 0, else k_diag_grm's K_JJ.
@@ -731,34 +753,17 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 #pragma unroll
         for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
       }
+      // D (overlapped). block row p of X = L^{-1}: L row p and X rows < p are final and
+      // X_pp came out of the previous window's factor16
+      if (!(a.skip & 8) && w - 1 < p) xinv_block(Tp, Xp, p, w - 1, l);
     }
     __syncthreads();
   }
   if (a.skip & 16) return;
 
-  // D. blocked inverse in LDS, one block diagonal per round:
-  //    X_{j+d,j} = -X_{j+d,j+d} sum_{l=j}^{j+d-1} L_{j+d,l} X_{l,j}
-  for (int dd = 1; dd < ((a.skip & 8) ? 0 : NBLK); ++dd) {
-    for (int jb = w; jb + dd < NBLK; jb += DW) {
-      const int q = jb + dd;
-      v4d sacc = {0.0, 0.0, 0.0, 0.0};
-      for (int lb = jb; lb < q; ++lb) {
-        const double* A = Tp + pk(q, lb);
-        const double* B = Xp + pk(lb, jb);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int k = 4 * kk + (l >> 4);
-          sacc = mfma64(A[bo(l & 15, k)], B[bo(k, l & 15)], sacc);
-        }
-      }
-      v4d xo = {0.0, 0.0, 0.0, 0.0};
-      const double* Xqq = Xp + pk(q, q);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) xo = mfma64_nega(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
-      double* dst = Xp + pk(q, jb);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] = xo[r];
-    }
+  // D. last block row of X (rows < NBLK-1 were built inside the factorisation windows)
+  if (!(a.skip & 4) && !(a.skip & 8)) {
+    if (w < NBLK - 1) xinv_block(Tp, Xp, NBLK - 1, w, l);
     __syncthreads();
   }
 
