@@ -741,9 +741,11 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
         for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
       }
       if (!(a.skip & 256)) factor16(Tp + pk(p + 1, p + 1), Xp + pk(p + 1, p + 1), l);
-    } else {
-      // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over waves 1-3
-      for (int e = w; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += DW - 1) {
+    } else if (w != DW / 2) {
+      // wave DW/2 shares wave 0's SIMD and stays idle so that factor16 issues alone there;
+      // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over the others
+      const int wi = (w < DW / 2) ? w - 1 : w - 2;   // 0 .. DW-3
+      for (int e = wi + 1; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += DW - 2) {
         int qq = 0;
         while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
         const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
@@ -755,7 +757,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       }
       // D (overlapped). block row p of X = L^{-1}: L row p and X rows < p are final and
       // X_pp came out of the previous window's factor16
-      if (!(a.skip & 8) && w - 1 < p) xinv_block(Tp, Xp, p, w - 1, l);
+      if (!(a.skip & 8) && wi < p) xinv_block(Tp, Xp, p, wi, l);
     }
     __syncthreads();
   }
