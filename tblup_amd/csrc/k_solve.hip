@@ -85,7 +85,7 @@ __device__ __forceinline__ double pearson_abs(const double* e, const double* yV,
 
 template <int NTR>
 __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict__ fit, double* __restrict__ ebv) {
-  extern __shared__ double dyn[];  // alpha[nt][ns] then e[nt][nV]
+  extern __shared__ double dyn[];  // alpha[nt][ns], e[nt][nV], then (primal) int32 rowp[ns]
   __shared__ double part[NTH / 64][2 * TILE];   // reused as [64][64]
   __shared__ double vsh[MAXT][TILE];
   __shared__ double wblk[KBLK];
@@ -95,6 +95,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   constexpr int nt = NTR;
   double* alpha = dyn;
   double* eall = dyn + nt * ns;
+  int32_t* rowp = reinterpret_cast<int32_t*>(eall + nt * nV);   // [ns] primal: split row per SNP
   const int t = threadIdx.x;
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);   // the XCD that factorised it
   const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
@@ -108,16 +109,32 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   const int rc = t >> 3, seg = t & 7;
   for (int I = NT - 1; I >= 0; --I) {
     double s[NTR] = {};
-    for (int J = I + 1; J < NT; ++J) {
-      const double* row = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 16 * seg;
-      constexpr int EU = NTR > 1 ? 2 : 8;
-#pragma unroll EU
+    // two tiles per step: 256 B per thread (256 KiB per workgroup) in flight
+    for (int J = I + 1; J < ((c.skip & 1024) ? 0 : NT); J += 2) {
+      const bool two = J + 1 < NT;
+      const double* row0 = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 16 * seg;
+      const double* row1 = two ? row0 + (int64_t)NT * TILE * TILE : row0;
+      v2d x0[8], x1[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x0[e] = *reinterpret_cast<const v2d*>(row0 + 2 * e);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x1[e] = *reinterpret_cast<const v2d*>(row1 + 2 * e);
+#pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const v2d x = *reinterpret_cast<const v2d*>(row + 2 * e);
 #pragma unroll
         for (int tr = 0; tr < NTR; ++tr) {
           const double* al = alpha + tr * ns + J * TILE + 16 * seg;
-          s[tr] += x[0] * al[2 * e] + x[1] * al[2 * e + 1];
+          s[tr] += x0[e][0] * al[2 * e] + x0[e][1] * al[2 * e + 1];
+        }
+      }
+      if (two) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+#pragma unroll
+          for (int tr = 0; tr < NTR; ++tr) {
+            const double* al = alpha + tr * ns + (J + 1) * TILE + 16 * seg;
+            s[tr] += x1[e][0] * al[2 * e] + x1[e][1] * al[2 * e + 1];
+          }
         }
       }
     }
@@ -156,6 +173,14 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 
   const double* ub = c.u + b * prow;
   const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
+  if (c.sd.form == FORM_PRIMAL) {
+    const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b];
+    for (int64_t r = t; r < kk; r += NTH) {
+      int64_t p = c.idx[o0 + r];
+      rowp[r] = (int32_t)(p < 0 ? 0 : (p >= c.d.P ? c.d.P - 1 : p));
+    }
+    __syncthreads();
+  }
   const int dq = t & 15, rg = t >> 4;   // dword (4 bytes) within a 64-wide block row, row group (64)
   double* pw = &part[0][0];             // [64 row groups][64]
   double fsum = 0.0;
@@ -170,31 +195,44 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       double s_ub = 0.0;
       for (int64_t r = t; r < kk; r += NTH) s_ub += ub[r] * al[r];
       const double MB = block_sum(s_ub, red) * sc[SC_SM];
-      // X_V read in place from the split's SNP-major rows (V animals start at byte nTp)
-      const int64_t o0 = c.off[b];
-      const int64_t nvb = (nV + KBLK - 1) / KBLK;
-      for (int64_t vb = 0; vb < nvb; ++vb) {
-        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-        for (int64_t r = rg; r < kk; r += NTH / 16) {
-          int64_t p = c.idx[o0 + r];
-          p = p < 0 ? 0 : (p >= c.d.P ? c.d.P - 1 : p);
-          const uint32_t x = reinterpret_cast<const uint32_t*>(c.gs + p * c.gs_row + nTp + vb * KBLK)[dq];
+      // X_V read in place from the split's SNP-major rows (V animals start at byte nTp), in
+      // 256-animal chunks: thread (row group rg, lane lq) reads 16 animals of each of its rows
+      // with one 16-B load; the four row groups of a wave reduce by lane shuffles, the 16
+      // waves through LDS.
+      const int lq = t & 15, rg = t >> 4, l = t & 63, w = t >> 6;
+      double* pv = &part[0][0];   // [16 waves][256]
+      const int64_t nch = (nV + 255) / 256;
+      for (int64_t ch = 0; ch < nch; ++ch) {
+        double acc[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+        const int64_t vo = nTp + ch * 256 + 16 * lq;
+#pragma unroll 4
+        for (int64_t r = rg; r < ((c.skip & 2048) ? 0 : kk); r += NTH / 16) {
+          const uint4 x = *reinterpret_cast<const uint4*>(c.gs + (int64_t)rowp[r] * c.gs_row + vo);
           const double ar = al[r];
-          p0 += (double)(x & 0xff) * ar;
-          p1 += (double)((x >> 8) & 0xff) * ar;
-          p2 += (double)((x >> 16) & 0xff) * ar;
-          p3 += (double)(x >> 24) * ar;
+          const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[4 * d + j] += (double)((xw[d] >> (8 * j)) & 0xff) * ar;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          acc[j] += __shfl_xor(acc[j], 16);
+          acc[j] += __shfl_xor(acc[j], 32);
         }
         __syncthreads();
-        pw[rg * KBLK + 4 * dq + 0] = p0;
-        pw[rg * KBLK + 4 * dq + 1] = p1;
-        pw[rg * KBLK + 4 * dq + 2] = p2;
-        pw[rg * KBLK + 4 * dq + 3] = p3;
+        if (l < 16) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) pv[w * 256 + 16 * lq + j] = acc[j];
+        }
         __syncthreads();
-        if (t < KBLK && vb * KBLK + t < nV) {
-          double acc = 0.0;
-          for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
-          e[vb * KBLK + t] = acc - MB + mu;
+        if (t < 256 && ch * 256 + t < nV) {
+          double sacc = 0.0;
+#pragma unroll
+          for (int q = 0; q < NTH / 64; ++q) sacc += pv[q * 256 + t];
+          e[ch * 256 + t] = sacc - MB + mu;
         }
       }
       __syncthreads();
@@ -260,7 +298,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 }
 
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s) {
-  const size_t shm = (size_t)c.d.nt * (size_t)(c.sd.ns + c.d.nV) * sizeof(double);
+  const size_t shm = (size_t)c.d.nt * (size_t)(c.sd.ns + c.d.nV) * sizeof(double) + (size_t)((c.sd.ns + 1) / 2) * sizeof(double);
   auto launch = [&](const void* fn, auto kernel) -> hipError_t {
     if (shm > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);

@@ -10,7 +10,7 @@ m = sys.argv[1]
 rows = list(csv.DictReader(open(f"gpurun_out/abl_{m}/t_kernel_stats.csv")))
 out = []
 for r in rows:
-    name = r["Name"].split("(")[0].replace("tblup::", "")
+    name = r["Name"].split("(")[0].replace("tblup::", "").replace("void ", "").split("<")[0]
     if name.startswith("k_"):
         out.append(f"{name}={float(r['AverageNs'])/1e3:.1f}us")
 print("mask", m, " ".join(sorted(out)))
