@@ -107,6 +107,11 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   // the stored diagonal inverses.  (L_JI^T alpha_J)[c] = sum_r Lt_(J,I)[c][r] alpha_J[r]:
   // row c of the transposed tile, 8 threads per row (16 contiguous r each), lane shuffles.
   const int rc = t >> 3, seg = t & 7;
+  // z into alpha's slots up front (alpha_I replaces z_I once computed): no global load on
+  // the block-row chain except the tiles and X_I
+  if (c.skip & 8192) return;
+  for (int64_t i = t; i < nt * ns; i += NTH) alpha[i] = c.z[b * nt * ns + i];
+  __syncthreads();
   for (int I = NT - 1; I >= 0; --I) {
     double s[NTR] = {};
     // two tiles per step: 256 B per thread (256 KiB per workgroup) in flight
@@ -138,24 +143,31 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
         }
       }
     }
+    // alpha_I[c] = (X_I^T v)[c] = sum_i X[i][c] v[i].  Dinv holds the lower blocks of X
+    // transposed (block (q, jb) stores X_{q,jb}^T), so thread (c, seg) reads row c%16 of
+    // block (seg, c/16) -- 16 contiguous i -- which exists iff seg >= c/16.  Loaded before
+    // the reduction and barrier so that their latency overlaps them.
+    const bool xrow = seg >= (rc >> 4);
+    v2d xr[8];
+    {
+      const double* xb = Db + (int64_t)I * NPACK * BLKD + (xrow ? pk(seg, rc >> 4) + (rc & 15) * NB : 0);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) xr[m] = *reinterpret_cast<const v2d*>(xb + 2 * m);
+    }
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr) {
       s[tr] += __shfl_xor(s[tr], 1);
       s[tr] += __shfl_xor(s[tr], 2);
       s[tr] += __shfl_xor(s[tr], 4);
-      if (seg == 0) vsh[tr][rc] = c.z[(b * nt + tr) * ns + (int64_t)I * TILE + rc] - s[tr];
+      if (seg == 0) vsh[tr][rc] = alpha[tr * ns + (int64_t)I * TILE + rc] - s[tr];
     }
     __syncthreads();
-    // alpha_I[c] = (X_I^T v)[c] = sum_i X[i][c] v[i].  Dinv holds the lower blocks of X
-    // transposed (block (q, jb) stores X_{q,jb}^T), so thread (c, seg) reads row c%16 of
-    // block (seg, c/16) -- 16 contiguous i -- which exists iff seg >= c/16.
     double s2[NTR] = {};
-    if (seg >= (rc >> 4)) {
-      const double* xb = Db + (int64_t)I * NPACK * BLKD + pk(seg, rc >> 4) + (rc & 15) * NB;
+    if (xrow) {
       const int sw = (rc >> 1) & 7;   // bo(): 16-B chunk m of the row holds columns 2(m ^ sw), +1
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const v2d x = *reinterpret_cast<const v2d*>(xb + 2 * m);
+        const v2d x = xr[m];
         const int i0 = 16 * seg + 2 * (m ^ sw);
 #pragma unroll
         for (int tr = 0; tr < NTR; ++tr) s2[tr] += x[0] * vsh[tr][i0] + x[1] * vsh[tr][i0 + 1];
@@ -171,6 +183,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     __syncthreads();
   }
 
+  if (c.skip & 4096) return;
   const double* ub = c.u + b * prow;
   const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
   if (c.sd.form == FORM_PRIMAL) {
