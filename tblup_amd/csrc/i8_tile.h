@@ -72,65 +72,6 @@ __device__ __forceinline__ void i8_tile_gemm(const int8_t* __restrict__ a_base, 
   }
 }
 
-// Same product (A = B, the symmetric diagonal tile) with an LDS-DMA ring
-// (global_load_lds_dwordx4): D stage slots, D-1 stages in flight while one is consumed,
-// one barrier per stage.  The LDS image is lane-linear per wave instruction; the chunk
-// swizzle of lds_off_i8 is applied to the SOURCE address (an involution), so fragment
-// reads use lds_off_i8 unchanged.
-// Sources are per lane: this lane's 16-B chunks of the two rows it loads (see
-// i8_ring_row), already swizzled; stage kb adds kb * kstep.  That covers both the
-// materialised panel (kstep = panel block stride) and rows read in place from the
-// SNP-major split matrix (kstep = 64).  lds must hold D * 8 KiB.
-__device__ __forceinline__ int i8_ring_row(int e) { return (2 * (threadIdx.x >> 6) + e) * 16 + ((threadIdx.x & 63) >> 2); }
-__device__ __forceinline__ int i8_ring_chunk(int row) { return 16 * ((threadIdx.x & 3) ^ ((row >> 2) & 3)); }
-
-template <int D>
-__device__ __forceinline__ void i8_tile_syrk_ring(const int8_t* const (&src)[2], int64_t nblk, int64_t kstep,
-                                                  int8_t* lds, v16i (&acc)[2][2]) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
-  if (nblk <= 0) return;
-  constexpr int TB = TILE * KBLK;             // 8 KiB per stage
-  auto issue = [&](int64_t kb) {
-    int8_t* slot = lds + (int)(kb % D) * TB;
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-      __builtin_amdgcn_global_load_lds(src[e] + kb * kstep, (__attribute__((address_space(3))) void*)(slot + (2 * w + e) * 1024),
-                                       16, 0, 0);
-  };
-  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    if (kb + D - 2 < nblk) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kb + D - 1 < nblk) issue(kb + D - 1);   // into the slot consumed at kb-1
-    const int8_t* As = lds + (int)(kb % D) * TB;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = (l >> 5) + 2 * kk;
-      v4i a[2], bb[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) a[m] = *reinterpret_cast<const v4i*>(As + lds_off_i8(64 * wr + 32 * m + (l & 31), chunk));
-#pragma unroll
-      for (int n = 0; n < 2; ++n) bb[n] = *reinterpret_cast<const v4i*>(As + lds_off_i8(64 * wc + 32 * n + (l & 31), chunk));
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bb[n], acc[m][n], 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
 // ---- 2-bit packed genotypes ----
 // A packed row holds 4 genotypes per byte, animal 4j+i at bits 2i of byte j.  One 32-bit
 // word (16 animals) unpacks to the 16 int8 MFMA operand bytes with two ops per dword:
@@ -140,58 +81,6 @@ __device__ __forceinline__ void i8_tile_syrk_ring(const int8_t* const (&src)[2],
 __device__ __forceinline__ v4i unpack16(uint32_t x) {
   return v4i{(int)(x & 0x03030303u), (int)((x >> 2) & 0x03030303u), (int)((x >> 4) & 0x03030303u),
              (int)((x >> 6) & 0x03030303u)};
-}
-
-// Packed variant of i8_tile_syrk_ring: stage kb = 64 animals = 16 B per row, a 2 KB stage
-// of 128 rows; D stages in flight (D = 16 fits 32 KiB).  src: this lane's row (row
-// 64 (w&1) + l of the tile for waves 0-1; waves 2-3 load nothing), stage kb at + 16 kb.
-template <int D>
-__device__ __forceinline__ void i8_tile_syrk_packed(const uint8_t* src, int64_t nblk, uint8_t* lds,
-                                                    v16i (&acc)[2][2]) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0;
-  if (nblk <= 0) return;
-  constexpr int SB = TILE * 16;   // 2 KiB per stage
-  auto issue = [&](int64_t kb) {
-    if (w < 2)
-      __builtin_amdgcn_global_load_lds(src + kb * 16, (__attribute__((address_space(3))) void*)(lds + (int)(kb % D) * SB + w * 1024),
-                                       16, 0, 0);
-  };
-  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    if (w < 2) {
-      if (kb + D - 2 < nblk) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 2) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kb + D - 1 < nblk) issue(kb + D - 1);
-    const uint8_t* As = lds + (int)(kb % D) * SB;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = (l >> 5) + 2 * kk;   // 16 animals
-      v4i a[2], bb[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-        a[m] = unpack16(*reinterpret_cast<const uint32_t*>(As + (64 * wr + 32 * m + (l & 31)) * 16 + 4 * chunk));
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-        bb[n] = unpack16(*reinterpret_cast<const uint32_t*>(As + (64 * wc + 32 * n + (l & 31)) * 16 + 4 * chunk));
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bb[n], acc[m][n], 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
 }
 
 // Row / column (within the 128x128 tile) of accumulator element r of block (m, n) for lane l.

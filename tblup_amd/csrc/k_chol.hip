@@ -304,65 +304,6 @@ __device__ __forceinline__ const uint8_t* row_packed(const CholArgs& a, int64_t 
 // Each piece is written in the packed block layout the diagonal kernel factorises in,
 // so the diagonal kernel sums them with a linear sweep.
 // ---------------------------------------------------------------------------
-// K_JJ for every (individual, J): int8 MFMA tile, exact counts + fp64 centring, + lambda I,
-// identity on padded rows; packed lower 16x16 blocks into Kd[b][J].
-__global__ __launch_bounds__(256, 2) void k_diag_grm(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[8 * TILE * KBLK];
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
-  const int NT = a.NT;
-  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
-  const int64_t b = lg / NT;
-  const int J = (int)(lg % NT);
-  const int64_t j0 = (int64_t)J * TILE;
-  const double* sc = a.scal + b * SCAL;
-  const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
-  const int64_t nrow = (int64_t)sc[SC_NROW], nblk = (int64_t)sc[SC_CBLK];
-  const double* ub = a.u + b * a.prow;
-  double* Kd = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
-  v16i ci[2][2];
-  if (!(a.skip & 1)) {
-    if (a.form == FORM_PRIMAL) {
-      const int t = threadIdx.x;
-      i8_tile_syrk_packed<16>(row_packed(a, b, j0 + ((t >> 6) & 1) * 64 + (t & 63)), nblk,
-                              reinterpret_cast<uint8_t*>(lds), ci);
-    } else {
-      const int8_t* src[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int row = i8_ring_row(e);
-        src[e] = row_base(a, b, j0 + row) + i8_ring_chunk(row);
-      }
-      i8_tile_syrk_ring<8>(src, nblk, a.prow * KBLK, lds, ci);
-    }
-  } else {
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) ci[m][n][r] = 0;
-  }
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int col = i8_col(wc, n, l);
-      const int64_t gj = j0 + col;
-      const double uj = ub[gj];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = i8_row(wr, m, r, l);
-        if ((row >> 4) >= (col >> 4)) {
-          const int64_t gi = j0 + row;
-          const double kv = grm_value(ci[m][n][r], ub[gi], uj, sa, cN, invd, sm);
-          const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
-          Kd[pk(row >> 4, col >> 4) + bo(row & 15, col & 15)] = v;
-        }
-      }
-    }
-}
-
-
 constexpr int DW = 8;            // waves per diagonal workgroup
 constexpr int DTHR = 64 * DW;
 static_assert(DTHR == 4 * TILE, "diag z: four lanes per row");
@@ -946,10 +887,61 @@ __global__ __launch_bounds__(OTH, 2) void k_chol_offdiag(CholArgs a, int I0, int
   offdiag_tile(a, logical / nI, I0 + (int)(logical % nI), lds, uj_sh, ui_sh, zj_sh);
 }
 
+// K_JJ for every (individual, J) with the off-diagonal kernel's 8-wave int8 tile (A = B =
+// the rows of tile J, output in the f64 accumulator layout: wave w holds columns
+// 16w..16w+15 of every row block), exact counts + fp64 centring, + lambda I, identity on
+// padded rows; packed lower 16x16 blocks into Kd[b][J].
+__global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * TILE * 64];
+  __shared__ double u_sh[TILE];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int NT = a.NT;
+  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
+  const int64_t b = lg / NT;
+  const int J = (int)(lg % NT);
+  const int64_t j0 = (int64_t)J * TILE;
+  const double* sc = a.scal + b * SCAL;
+  const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
+  const int64_t nrow = (int64_t)sc[SC_NROW], nblk = (int64_t)sc[SC_CBLK];
+  if (t < TILE) u_sh[t] = a.u[b * a.prow + j0 + t];
+  double* Kd = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
+  v4i cnt[8];
+  const int row = 16 * w + (l >> 2), pos = l & 3;
+  if (a.skip & 1) {
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
+  } else if (a.form == FORM_PRIMAL) {
+    const uint8_t* rp = row_packed(a, b, j0 + row);
+    i8_tt8_pk64<4>(rp + 16 * (pos ^ ((row >> 2) & 3)), rp + 16 * (pos ^ ((row >> 2) & 2)), nblk,
+                   lds, cnt);
+  } else {
+    const int8_t* rb = row_base(a, b, j0 + row);
+    i8_tt8<4>(rb + 16 * (pos ^ ((row >> 2) & 3)), rb + 16 * (pos ^ ((row >> 2) & 2)), nblk, a.prow * KBLK,
+              reinterpret_cast<int8_t*>(lds), cnt);
+  }
+  __syncthreads();
+  const int il = 16 * w + (l & 15);
+  const int64_t gj = j0 + il;
+  const double uj = u_sh[il];
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) {
+    if (cb >= w) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cl = 16 * cb + (l >> 4) + 4 * r;
+        const int64_t gi = j0 + cl;
+        const double kv = grm_value(cnt[cb][r], u_sh[cl], uj, sa, cN, invd, sm);
+        const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
+        Kd[pk(cb, w) + bo(cl & 15, il & 15)] = v;
+      }
+    }
+  }
+}
+
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip};
-  hipLaunchKernelGGL(k_diag_grm, dim3((unsigned)(c.B * c.sd.NT)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * c.sd.NT)), dim3(OTH), 0, s, a);
   return hipGetLastError();
 }
 
