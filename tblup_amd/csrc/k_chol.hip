@@ -318,10 +318,13 @@ constexpr int OTH = 64 * OW;     // threads
 
 // int8 tile, kernel form (gathered int8 panel): A = panel rows of tile J, B = tile I.
 // Stage kb = 8 KiB per operand; wave w loads 1 KiB chunk w of each (rows 16w..16w+15).
-template <int D>
+// WCL >= 0: this wave computes column block WCL and only the row blocks cb >= WCL (the
+// lower blocks of a symmetric diagonal tile); WCL < 0: column block w, all row blocks.
+template <int D, int WCL = -1>
 __device__ __forceinline__ void i8_tt8(const int8_t* sa, const int8_t* sb, int64_t nblk, int64_t kstep, int8_t* lds,
                                        v4i (&cnt)[8]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wc = (WCL < 0) ? w : WCL;
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
   if (nblk <= 0) return;
@@ -343,48 +346,13 @@ __device__ __forceinline__ void i8_tt8(const int8_t* sa, const int8_t* sb, int64
     if (kb + D - 1 < nblk) issue(kb + D - 1);
     const int8_t* As = lds + (int)(kb % D) * 2 * TB;
     const int8_t* Bs = As + TB;
-    const v4i bv = *reinterpret_cast<const v4i*>(Bs + i8off_b(16 * w + rho, ch));
+    const v4i bv = *reinterpret_cast<const v4i*>(Bs + i8off_b(16 * wc + rho, ch));
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb) {
-      const v4i av = *reinterpret_cast<const v4i*>(As + i8off_a(16 * cb + prow, ch));
-      cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cnt[cb], 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-// int8 tile, SNP form (2-bit packed rows in place): 4 KiB stages (A rows then B rows);
-// waves 0-3 load (row 64(w&1) + l of operand w>>1), waves 4-7 only compute.
-template <int D>
-__device__ __forceinline__ void i8_tt8_packed(const uint8_t* src, int64_t nblk, uint8_t* lds, v4i (&cnt)[8]) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
-  if (nblk <= 0) return;
-  constexpr int SB = 2 * TILE * 16;
-  auto issue = [&](int64_t kb) {
-    if (w < 4) __builtin_amdgcn_global_load_lds(src + kb * 16, (lds_ptr_t)(lds + (int)(kb % D) * SB + w * 1024), 16, 0, 0);
-  };
-  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
-  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    if (w < 4) {
-      if (kb + D - 2 < nblk) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 2) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (cb >= WCL) {
+        const v4i av = *reinterpret_cast<const v4i*>(As + i8off_a(16 * cb + prow, ch));
+        cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cnt[cb], 0, 0, 0);
       }
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kb + D - 1 < nblk) issue(kb + D - 1);
-    const uint8_t* As = lds + (int)(kb % D) * SB;
-    const uint8_t* Bs = As + TILE * 16;
-    const v4i bv = unpack16(*reinterpret_cast<const uint32_t*>(Bs + (16 * w + rho) * 16 + 4 * ch));
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
-      const v4i av = unpack16(*reinterpret_cast<const uint32_t*>(As + (16 * cb + prow) * 16 + 4 * ch));
-      cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cnt[cb], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -398,10 +366,11 @@ __device__ __forceinline__ void i8_tt8_packed(const uint8_t* src, int64_t nblk, 
 // the four lane groups x four k-steps cover the 16 dwords once (animal order inside a
 // stage is immaterial to the counts; A and B use the same order).  A stage past the
 // training block (nblk = 64-animal blocks, nblk % 4 != 0) zeroes chunks ch >= nblk % 4.
-template <int D>
+template <int D, int WCL = -1>
 __device__ __forceinline__ void i8_tt8_pk64(const uint8_t* sa, const uint8_t* sb, int64_t nblk, uint8_t* lds,
                                             v4i (&cnt)[8]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wc = (WCL < 0) ? w : WCL;
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
   if (nblk <= 0) return;
@@ -425,19 +394,22 @@ __device__ __forceinline__ void i8_tt8_pk64(const uint8_t* sa, const uint8_t* sb
     if (st + D - 1 < nst) issue(st + D - 1);
     const uint8_t* As = lds + (int)(st % D) * 2 * TB;
     const uint8_t* Bs = As + TB;
-    uint4 bq = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * w + rho, ch));
+    uint4 bq = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * wc + rho, ch));
     if (st == nst - 1 && tail_ch != 0 && ch >= tail_ch) bq = uint4{0u, 0u, 0u, 0u};
     uint4 aq[8];
 #pragma unroll
-    for (int cb = 0; cb < 8; ++cb) aq[cb] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * cb + prow, ch));
+    for (int cb = 0; cb < 8; ++cb)
+      if (cb >= WCL) aq[cb] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * cb + prow, ch));
     const uint32_t bw[4] = {bq.x, bq.y, bq.z, bq.w};
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const v4i bv = unpack16(bw[s4]);
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) {
-        const uint32_t aw = s4 == 0 ? aq[cb].x : s4 == 1 ? aq[cb].y : s4 == 2 ? aq[cb].z : aq[cb].w;
-        cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(unpack16(aw), bv, cnt[cb], 0, 0, 0);
+        if (cb >= WCL) {
+          const uint32_t aw = s4 == 0 ? aq[cb].x : s4 == 1 ? aq[cb].y : s4 == 2 ? aq[cb].z : aq[cb].w;
+          cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(unpack16(aw), bv, cnt[cb], 0, 0, 0);
+        }
       }
     }
   }
@@ -888,9 +860,9 @@ __global__ __launch_bounds__(OTH, 2) void k_chol_offdiag(CholArgs a, int I0, int
 }
 
 // K_JJ for every (individual, J) with the off-diagonal kernel's 8-wave int8 tile (A = B =
-// the rows of tile J, output in the f64 accumulator layout: wave w holds columns
-// 16w..16w+15 of every row block), exact counts + fp64 centring, + lambda I, identity on
-// padded rows; packed lower 16x16 blocks into Kd[b][J].
+// the rows of tile J, output in the f64 accumulator layout: a wave holds the 16 columns of
+// one column block, MFMAs only for the lower row blocks), exact counts + fp64 centring,
+// + lambda I, identity on padded rows; packed lower 16x16 blocks into Kd[b][J].
 __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * TILE * 64];
   __shared__ double u_sh[TILE];
@@ -907,32 +879,58 @@ __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a) {
   double* Kd = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
   v4i cnt[8];
   const int row = 16 * w + (l >> 2), pos = l & 3;
-  if (a.skip & 1) {
+  // lower blocks only; waves w and w+4 share a SIMD, so they take column blocks w and 7-w
+  // (8-w and w+1 row blocks: 9 per SIMD)
+  const int wc = (w < 4) ? w : 11 - w;
 #pragma unroll
-    for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
+  for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
+  if (a.skip & 1) {
+    __syncthreads();
   } else if (a.form == FORM_PRIMAL) {
     const uint8_t* rp = row_packed(a, b, j0 + row);
-    i8_tt8_pk64<4>(rp + 16 * (pos ^ ((row >> 2) & 3)), rp + 16 * (pos ^ ((row >> 2) & 2)), nblk,
-                   lds, cnt);
+    const uint8_t* sa = rp + 16 * (pos ^ ((row >> 2) & 3));
+    const uint8_t* sb = rp + 16 * (pos ^ ((row >> 2) & 2));
+    switch (wc) {   // wave-uniform: one instantiation per column block
+      case 0: i8_tt8_pk64<4, 0>(sa, sb, nblk, lds, cnt); break;
+      case 1: i8_tt8_pk64<4, 1>(sa, sb, nblk, lds, cnt); break;
+      case 2: i8_tt8_pk64<4, 2>(sa, sb, nblk, lds, cnt); break;
+      case 3: i8_tt8_pk64<4, 3>(sa, sb, nblk, lds, cnt); break;
+      case 4: i8_tt8_pk64<4, 4>(sa, sb, nblk, lds, cnt); break;
+      case 5: i8_tt8_pk64<4, 5>(sa, sb, nblk, lds, cnt); break;
+      case 6: i8_tt8_pk64<4, 6>(sa, sb, nblk, lds, cnt); break;
+      default: i8_tt8_pk64<4, 7>(sa, sb, nblk, lds, cnt); break;
+    }
   } else {
     const int8_t* rb = row_base(a, b, j0 + row);
-    i8_tt8<4>(rb + 16 * (pos ^ ((row >> 2) & 3)), rb + 16 * (pos ^ ((row >> 2) & 2)), nblk, a.prow * KBLK,
-              reinterpret_cast<int8_t*>(lds), cnt);
+    const int8_t* sa = rb + 16 * (pos ^ ((row >> 2) & 3));
+    const int8_t* sb = rb + 16 * (pos ^ ((row >> 2) & 2));
+    int8_t* ld8 = reinterpret_cast<int8_t*>(lds);
+    const int64_t ks = a.prow * KBLK;
+    switch (wc) {
+      case 0: i8_tt8<4, 0>(sa, sb, nblk, ks, ld8, cnt); break;
+      case 1: i8_tt8<4, 1>(sa, sb, nblk, ks, ld8, cnt); break;
+      case 2: i8_tt8<4, 2>(sa, sb, nblk, ks, ld8, cnt); break;
+      case 3: i8_tt8<4, 3>(sa, sb, nblk, ks, ld8, cnt); break;
+      case 4: i8_tt8<4, 4>(sa, sb, nblk, ks, ld8, cnt); break;
+      case 5: i8_tt8<4, 5>(sa, sb, nblk, ks, ld8, cnt); break;
+      case 6: i8_tt8<4, 6>(sa, sb, nblk, ks, ld8, cnt); break;
+      default: i8_tt8<4, 7>(sa, sb, nblk, ks, ld8, cnt); break;
+    }
   }
   __syncthreads();
-  const int il = 16 * w + (l & 15);
+  const int il = 16 * wc + (l & 15);
   const int64_t gj = j0 + il;
   const double uj = u_sh[il];
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) {
-    if (cb >= w) {
+    if (cb >= wc) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * cb + (l >> 4) + 4 * r;
         const int64_t gi = j0 + cl;
         const double kv = grm_value(cnt[cb][r], u_sh[cl], uj, sa, cN, invd, sm);
         const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
-        Kd[pk(cb, w) + bo(cl & 15, il & 15)] = v;
+        Kd[pk(cb, wc) + bo(cl & 15, il & 15)] = v;
       }
     }
   }
