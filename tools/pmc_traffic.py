@@ -10,7 +10,7 @@ import csv
 import json
 from collections import defaultdict
 
-CLASSES = {"k_indiv_stats": "stats", "k_gather": "gather", "k_grm": "grm", "k_diag_grm": "grm",
+CLASSES = {"k_indiv_stats": "stats", "k_gather": "gather", "k_grm": "grm", "k_diag_grm": "grm", "k_diag_grm8": "grm",
            "k_chol_diag": "chol_diag", "k_chol_offdiag": "chol_offdiag", "k_solve": "solve"}
 
 
