@@ -63,6 +63,8 @@ int tblup_device_count(int* out_count);
  * Create a context on HIP device `device`: uploads the {0,1,2} genotype
  * matrix (int8) and the phenotype vector (float64, length n_animals).
  * Replaces the per-worker np.load of evaluator.py:215-216.
+ * tblup_ctx_create(NULL, 0, 0, layout, NULL, device, &ctx) creates a context
+ * without a panel, for the DE step and genome decode only (no split can be set).
  */
 int tblup_ctx_create(const int8_t* geno, int64_t n_animals, int64_t n_snps, int layout,
                      const double* pheno, int device, tblup_ctx** out_ctx);
@@ -166,6 +168,38 @@ int tblup_reset_profile(tblup_ctx* ctx);
  */
 int tblup_debug_grm(tblup_ctx* ctx, int split_id, const int64_t* idx, int64_t k, double h2,
                     int branch, int stage, double* out, double* z_out);
+
+/*
+ * One differential-evolution generation (mutation + binary crossover + clip) for a
+ * population of `pop` internal genomes of length L, bit-exact to the reference:
+ *   TBLUP_DE_RAND_1            DERandOneEvolver.de_rand_one   tblup/evolver.py:103-138
+ *                              donors[i] = (a, b, c):   mutant = a + F (b - c)
+ *   TBLUP_DE_CURRENT_TO_BEST_1 DECurrentToBestOneEvolver.de_currenttobest_one  evolver.py:179-221
+ *                              donors[i] = (best, a, b): mutant = x + F (best - x) + F (a - b)
+ *   crossover (evolver.py:63-82): child_j = mutant_j where u_j < cr or j == fixed[i], else x_j,
+ *   u = numpy's legacy np.random.rand(L) for individual i; clip (np.clip(., 0, clip_hi)) when clip.
+ * The donors and `fixed` are the caller's python-`random` draws (exclusive_randrange,
+ * random.randrange: utils.py:21-36, evolver.py:76).  mt_key / mt_pos hold numpy's global
+ * MT19937 state (np.random.get_state()[1:3]) before the generation's first
+ * np.random.rand call; on return they hold the state after all pop x 2L outputs, in
+ * numpy's own representation (np.random.set_state continues the stream exactly).
+ * Host pointers (parents/children: pop x L doubles), synchronous.
+ */
+enum { TBLUP_DE_RAND_1 = 0, TBLUP_DE_CURRENT_TO_BEST_1 = 1 };
+int tblup_de_step(tblup_ctx* ctx, int strategy, const double* parents, int64_t pop, int64_t L,
+                  const int32_t* donors, const int64_t* fixed, double F, double cr, int clip, double clip_hi,
+                  uint32_t* mt_key, int32_t* mt_pos, double* children);
+
+/* Same with device-resident parents / children (row strides ld, ldc >= L doubles) enqueued on
+ * `stream` (NULL = the context's stream); donors, fixed and the MT state are host arrays.
+ * Synchronises `stream` before returning (the new MT state is read back). */
+int tblup_de_step_device(tblup_ctx* ctx, int strategy, const double* d_parents, int64_t pop, int64_t L, int64_t ld,
+                         const int32_t* donors, const int64_t* fixed, double F, double cr, int clip, double clip_hi,
+                         uint32_t* mt_key, int32_t* mt_pos, double* d_children, int64_t ldc, void* stream);
+
+/* Host-only: advance numpy's MT19937 (key[624], pos) state by n_words 32-bit outputs
+ * (GF(2) jump-ahead; used to check the DE step's stream arithmetic without a GPU). */
+int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint32_t* key_out, int32_t* pos_out);
 
 /* Device memory currently held by the context (bytes). */
 int tblup_mem_info(tblup_ctx* ctx, int64_t* bytes_in_use);

@@ -22,6 +22,8 @@ _c = ctypes
 _P = _c.c_void_p
 _I64P = _c.POINTER(_c.c_int64)
 _DP = _c.POINTER(_c.c_double)
+_I32P = _c.POINTER(_c.c_int32)
+_U32P = _c.POINTER(_c.c_uint32)
 SIGNATURES = {
     "tblup_last_error": (_c.c_char_p, []),
     "tblup_version": (_c.c_char_p, []),
@@ -42,7 +44,14 @@ SIGNATURES = {
     "tblup_mem_info": (_c.c_int, [_P, _I64P]),
     "tblup_decode_topk": (_c.c_int, [_P, _DP, _c.c_int64, _c.c_int64, _I64P, _I64P]),
     "tblup_decode_topk_device": (_c.c_int, [_P, _P, _c.c_int64, _c.c_int64, _c.c_int64, _P, _I64P, _P, _P]),
+    "tblup_de_step": (_c.c_int, [_P, _c.c_int, _DP, _c.c_int64, _c.c_int64, _I32P, _I64P, _c.c_double, _c.c_double,
+                                 _c.c_int, _c.c_double, _U32P, _I32P, _DP]),
+    "tblup_de_step_device": (_c.c_int, [_P, _c.c_int, _P, _c.c_int64, _c.c_int64, _c.c_int64, _I32P, _I64P,
+                                        _c.c_double, _c.c_double, _c.c_int, _c.c_double, _U32P, _I32P, _P,
+                                        _c.c_int64, _P]),
+    "tblup_mt19937_jump": (_c.c_int, [_U32P, _c.c_int32, _c.c_uint64, _U32P, _I32P]),
 }
+DE_STRATEGY = {"de_rand_1": 0, "de_currenttobest_1": 1}
 
 
 class TblupError(RuntimeError):

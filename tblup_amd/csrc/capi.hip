@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/tblup_gpu.h"
+#include "mt_jump.h"
 #include "tblup_internal.h"
 
 using namespace tblup;
@@ -70,6 +71,9 @@ struct tblup_ctx {
   std::map<int, std::unique_ptr<Split>> splits;
   DevBuf ws;
   DevBuf dec_keys, dec_idx;   // host-pointer decode staging
+  DevBuf de_polys, de_small, de_par, de_chi;   // DE step: jump polynomials, per-call args, host-path staging
+  int64_t de_L = -1, de_pop = -1;              // (L, pop) of the uploaded polynomials
+  bool de_end_jump = false;
   size_t budget = 0;
   // profiling
   bool profiling = false;
@@ -356,7 +360,8 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   g_err.clear();
   if (!out) return fail(TBLUP_ERR_ARG, "null out_ctx");
   *out = nullptr;
-  if (!geno || !pheno || n < 2 || P < 1) return fail(TBLUP_ERR_ARG, "bad genotype/phenotype arguments");
+  const bool panel = geno || pheno || n || P;   // (NULL, 0, 0, NULL): DE / decode-only context
+  if (panel && (!geno || !pheno || n < 2 || P < 1)) return fail(TBLUP_ERR_ARG, "bad genotype/phenotype arguments");
   if (layout != TBLUP_LAYOUT_ANIMAL_MAJOR && layout != TBLUP_LAYOUT_SNP_MAJOR) return fail(TBLUP_ERR_ARG, "bad layout");
   if (n > (int64_t)1 << 30) return fail(TBLUP_ERR_ARG, "too many animals");
   int ndev = 0;
@@ -367,7 +372,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->device = device;
   c->n = n;
   c->P = P;
-  c->pheno.assign(pheno, pheno + n);
+  if (panel) c->pheno.assign(pheno, pheno + n);
   c->nt = 1;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   const char* env = getenv("TBLUP_WORKSPACE_MB");
@@ -376,6 +381,10 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->dbg_skip = dbg ? atoi(dbg) : 0;
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
+  if (!panel) {
+    *out = c.release();
+    return 0;
+  }
   const size_t gbytes = (size_t)n * (size_t)P;
   if (int rc = dev_alloc(c.get(), c->geno_sm, gbytes)) return rc;
   if (int rc = dev_alloc(c.get(), c->colsum_all, (size_t)P * 4)) return rc;
@@ -417,6 +426,10 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->ws.release();
   c->dec_keys.release();
   c->dec_idx.release();
+  c->de_polys.release();
+  c->de_small.release();
+  c->de_par.release();
+  c->de_chi.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -426,6 +439,7 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
                     int64_t nV) {
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;
+  if (c->n == 0) return fail(TBLUP_ERR_STATE, "context has no genotype panel (DE / decode-only context)");
   if (!train || !valid || nT < 1 || nV < 2) return fail(TBLUP_ERR_ARG, "split needs >= 1 train and >= 2 valid rows");
   for (int64_t i = 0; i < nT; ++i)
     if (train[i] < 0 || train[i] >= c->n) return fail(TBLUP_ERR_ARG, "train index out of range");
@@ -490,6 +504,7 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
 int tblup_set_traits(tblup_ctx* c, const double* pheno, int64_t n_traits) {
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;
+  if (c->n == 0) return fail(TBLUP_ERR_STATE, "context has no genotype panel (DE / decode-only context)");
   if (!pheno || n_traits < 1 || n_traits > MAXT) return fail(TBLUP_ERR_ARG, "need 1 <= n_traits <= 4 and phenotypes");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -753,6 +768,98 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
     std::memcpy(z_out, zz.data(), (size_t)d.nT * 8);
   }
   if (c->profiling) return drain_events(c);
+  return 0;
+}
+
+// ---- differential-evolution step (k_de.hip; jump polynomials from mt_jump.cpp) ----
+
+int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint32_t* key_out, int32_t* pos_out) {
+  g_err.clear();
+  if (!key || !key_out || !pos_out) return fail(TBLUP_ERR_ARG, "null key/key_out/pos_out");
+  if (pos < 0 || pos > 624) return fail(TBLUP_ERR_ARG, "pos must be in [0, 624]");
+  int po = 0;
+  tblup_mt::jump_state(key, pos, n_words, key_out, &po);
+  *pos_out = po;
+  return 0;
+}
+
+static int validate_de(int strategy, int64_t pop, int64_t L, const int32_t* donors, const int64_t* fixed, double cr,
+                       const uint32_t* mt_key, const int32_t* mt_pos) {
+  if (strategy != TBLUP_DE_RAND_1 && strategy != TBLUP_DE_CURRENT_TO_BEST_1)
+    return fail(TBLUP_ERR_ARG, "unknown DE strategy");
+  if (pop < 1 || pop > 65535 || L < 1 || L > ((int64_t)1 << 31)) return fail(TBLUP_ERR_ARG, "need 1 <= pop <= 65535, 1 <= L <= 2^31");
+  if (!donors || !fixed || !mt_key || !mt_pos) return fail(TBLUP_ERR_ARG, "null donors/fixed/mt_key/mt_pos");
+  if (*mt_pos < 0 || *mt_pos > 624) return fail(TBLUP_ERR_ARG, "mt_pos must be in [0, 624]");
+  if (!(cr == cr)) return fail(TBLUP_ERR_ARG, "crossover rate is NaN");
+  for (int64_t i = 0; i < 3 * pop; ++i)
+    if (donors[i] < 0 || donors[i] >= pop) return fail(TBLUP_ERR_ARG, "donor index out of range");
+  for (int64_t i = 0; i < pop; ++i)
+    if (fixed[i] < 0 || fixed[i] >= L) return fail(TBLUP_ERR_ARG, "fixed crossover position out of range");
+  return 0;
+}
+
+int tblup_de_step_device(tblup_ctx* c, int strategy, const double* d_parents, int64_t pop, int64_t L, int64_t ld,
+                         const int32_t* donors, const int64_t* fixed, double F, double cr, int clip, double clip_hi,
+                         uint32_t* mt_key, int32_t* mt_pos, double* d_children, int64_t ldc, void* stream) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_de(strategy, pop, L, donors, fixed, cr, mt_key, mt_pos)) return rc;
+  if (ld < L || ldc < L) return fail(TBLUP_ERR_ARG, "ld/ldc < L");
+  if (!d_parents || !d_children) return fail(TBLUP_ERR_ARG, "null device pointers");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (c->de_L != L || c->de_pop != pop) {
+    const tblup_mt::DePolys dp = tblup_mt::de_polys(L, pop);
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (int rc = dev_alloc(c, c->de_polys, dp.words.size() * 4)) return rc;
+    HIPCHK(hipMemcpy(c->de_polys.p, dp.words.data(), dp.words.size() * 4, hipMemcpyHostToDevice));
+    c->de_L = L;
+    c->de_pop = pop;
+    c->de_end_jump = dp.end_jump;
+  }
+  // per-call arguments: key in, key out, pos out, donors, fixed
+  const size_t o_keyo = 624 * 4, o_pos = 2 * 624 * 4, o_don = o_pos + 16, o_fix = o_don + (size_t)round_up(12 * pop, 16);
+  const size_t small = o_fix + 8 * (size_t)pop;
+  if (small > c->de_small.bytes) {
+    HIPCHK(hipStreamSynchronize(s));
+    if (int rc = dev_alloc(c, c->de_small, small)) return rc;
+  }
+  char* base = (char*)c->de_small.p;
+  std::vector<char> stage(small);
+  std::memcpy(stage.data(), mt_key, 624 * 4);
+  std::memcpy(stage.data() + o_don, donors, 12 * pop);
+  std::memcpy(stage.data() + o_fix, fixed, 8 * pop);
+  HIPCHK(hipMemcpyAsync(base, stage.data(), small, hipMemcpyHostToDevice, s));
+  const tblup_mt::EndState e = tblup_mt::end_state(*mt_pos, 2 * (uint64_t)L * (uint64_t)pop);
+  HIPCHK(launch_de_step((const uint32_t*)base, *mt_pos, (const uint32_t*)c->de_polys.p, c->de_end_jump ? 1 : 0, e.s,
+                        e.pos, d_parents, ld, (const int32_t*)(base + o_don), (const int64_t*)(base + o_fix), strategy,
+                        F, cr, clip ? 1 : 0, clip_hi, L, (int)pop, d_children, ldc, (uint32_t*)(base + o_keyo),
+                        (int32_t*)(base + o_pos), s));
+  HIPCHK(hipMemcpyAsync(stage.data(), base + o_keyo, 624 * 4 + 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(mt_key, stage.data(), 624 * 4);
+  std::memcpy(mt_pos, stage.data() + 624 * 4, 4);
+  return 0;
+}
+
+int tblup_de_step(tblup_ctx* c, int strategy, const double* parents, int64_t pop, int64_t L, const int32_t* donors,
+                  const int64_t* fixed, double F, double cr, int clip, double clip_hi, uint32_t* mt_key,
+                  int32_t* mt_pos, double* children) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_de(strategy, pop, L, donors, fixed, cr, mt_key, mt_pos)) return rc;
+  if (!parents || !children) return fail(TBLUP_ERR_ARG, "null parents/children");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const size_t bytes = (size_t)pop * L * 8;
+  if (int rc = dev_alloc(c, c->de_par, bytes)) return rc;
+  if (int rc = dev_alloc(c, c->de_chi, bytes)) return rc;
+  HIPCHK(hipMemcpyAsync(c->de_par.p, parents, bytes, hipMemcpyHostToDevice, c->stream));
+  if (int rc = tblup_de_step_device(c, strategy, (const double*)c->de_par.p, pop, L, L, donors, fixed, F, cr, clip,
+                                    clip_hi, mt_key, mt_pos, (double*)c->de_chi.p, L, nullptr))
+    return rc;
+  HIPCHK(hipMemcpy(children, c->de_chi.p, bytes, hipMemcpyDeviceToHost));
   return 0;
 }
 

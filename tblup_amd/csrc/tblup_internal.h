@@ -148,6 +148,12 @@ hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipSt
 hipError_t launch_decode_topk(const double* keys, int64_t B, int64_t d, int64_t ld, const int64_t* off, int64_t* out,
                               hipStream_t s);
 
+// ---- launcher (k_de.hip): one DE generation (mutation + binary crossover + clip) per individual ----
+hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, int end_jump, int end_s, int end_pos,
+                          const double* parent, int64_t ldp, const int32_t* donors, const int64_t* fixed, int strategy,
+                          double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
+                          uint32_t* key_out, int32_t* pos_out, hipStream_t s);
+
 // XCD-aware bijective remap of a 1-D block id (blocks b and b+8 share an XCD
 // under the observed round-robin placement; speed only, never correctness).
 __device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {

@@ -1,0 +1,208 @@
+"""Drop-in DE evolvers whose generation step runs on the GPU.
+
+Mirrors `tblup/evolver.py` for the two classic strategies:
+
+* `DERandOneEvolver` (evolver.py:86-157): mutant = a + F (b - c)
+* `DECurrentToBestOneEvolver` (evolver.py:160-244): mutant = x + F (best - x) + F (a - b),
+  always clipped (the reference's `evolve` never passes `self.clip`, evolver.py:239-244)
+
+with the reference's binary crossover (evolver.py:63-82) and F = 5 on every 5th
+generation.  The per-individual python-`random` draws (the donors through
+`exclusive_randrange`, utils.py:21-36, and the forced crossover position,
+evolver.py:76) stay on the host in the reference's order; numpy's global MT19937
+stream, which the reference consumes with one `np.random.rand(L)` per individual,
+is jumped ahead on the GPU (k_de.hip, mt_jump.cpp) so every individual's
+uniforms, mutant, crossover and clip are computed in parallel.  The children's
+genomes and the numpy / python RNG states afterwards are bit-identical to the
+reference's sequential loop (tests/test_evolver.py, tests/test_gpu_evolver.py).
+
+SaDE and MDE_pBX (evolver.py:423-720) draw per-individual F/CR from normal and
+Cauchy distributions and are not accelerated: `get_evolver` raises for them.
+There is no CPU fallback: without the HIP library, `evolve` raises ImportError.
+"""
+import abc
+import ctypes
+import os
+import random
+from copy import deepcopy
+
+import numpy as np
+
+from . import _native
+
+
+def get_evolver(args):
+    """evolver.py:13-32 for the strategies this package runs on the GPU."""
+    if args.de_strategy == "de_rand_1":
+        return DERandOneEvolver(args.dimensionality, args.crossover_rate, args.mutation_intensity, args.clip)
+    if args.de_strategy == "de_currenttobest_1":
+        return DECurrentToBestOneEvolver(args.dimensionality, args.crossover_rate, args.mutation_intensity, args.clip)
+    if args.de_strategy in ("sade", "mde_pbx"):
+        raise NotImplementedError(
+            "Evolver {} has no GPU step in tblup_amd (adaptive F/CR draws); use tblup.evolver.get_evolver for it"
+            .format(args.de_strategy))
+    raise NotImplementedError("Evolver with config option {} is not implemented.".format(args.de_strategy))
+
+
+def exclusive_randrange(begin, end, exclude):
+    """utils.py:21-36, same python-`random` consumption (first draw before the assert)."""
+    r = random.randrange(begin, end)
+    exclude = set(exclude)
+    assert len(exclude) < (end - begin), "Exclusion range larger than random range."
+    while r in exclude:
+        r = random.randrange(begin, end)
+    return r
+
+
+class GpuDEStep:
+    """A panel-less GPU context running tblup_de_step (one per process and device)."""
+
+    _instances = {}
+
+    @classmethod
+    def get(cls, device=None):
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        inst = cls._instances.get(device)
+        if inst is None:
+            inst = cls._instances[device] = cls(device)
+        return inst
+
+    def __init__(self, device=0):
+        self._lib = _native.load()
+        ctx = ctypes.c_void_p()
+        _native.check("tblup_ctx_create", self._lib.tblup_ctx_create(None, 0, 0, 0, None, int(device),
+                                                                     ctypes.byref(ctx)))
+        self._ctx = ctx
+        self.device = int(device)
+
+    def step(self, strategy, parents, donors, fixed, F, cr, clip, clip_hi):
+        """children (pop x L) for the current numpy global state, which is advanced
+        past the generation's pop x L uniforms exactly as the reference's loop does."""
+        parents = np.ascontiguousarray(parents, dtype=np.float64)
+        pop, L = parents.shape
+        donors = np.ascontiguousarray(donors, dtype=np.int32)
+        fixed = np.ascontiguousarray(fixed, dtype=np.int64)
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise RuntimeError("numpy's global RandomState is not MT19937")
+        key = np.array(st[1], dtype=np.uint32)
+        pos = ctypes.c_int32(int(st[2]))
+        children = np.empty_like(parents)
+        _native.check("tblup_de_step", self._lib.tblup_de_step(
+            self._ctx, int(strategy), parents.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), pop, L,
+            donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+            float(F), float(cr), 1 if clip else 0, float(clip_hi),
+            key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
+            children.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
+        return children
+
+    def close(self):
+        if self._ctx:
+            self._lib.tblup_ctx_destroy(self._ctx)
+            self._ctx = None
+            GpuDEStep._instances.pop(self.device, None)
+
+
+def _child_dtypes(genomes, donors, strategy, mi, clip):
+    """Per-child dtype numpy gives the reference: np.where(mask, mutant, target) (+ np.clip);
+    None when every child is float64 (the usual RandomKey case)."""
+    dts = [np.asarray(g).dtype for g in genomes]
+    if all(dt == np.float64 for dt in dts):
+        return None
+    out = []
+    e = np.zeros(0, dtype=bool)
+    for i, (x, y, z) in enumerate(donors):
+        t, a, b, c = (np.zeros(0, dtype=dts[j]) for j in (i, x, y, z))
+        mutant = a + mi * (b - c) if strategy == 0 else t + mi * (a - t) + mi * (b - c)
+        r = np.where(e, mutant, t)
+        out.append((np.clip(r, 0, 1) if clip else r).dtype)
+    return out
+
+
+class Evolver(abc.ABC):
+    """evolver.py:35-44."""
+
+    @abc.abstractmethod
+    def evolve(self, population):
+        raise NotImplementedError()
+
+
+class _GpuDEEvolver(Evolver):
+    strategy = None
+    device = None
+
+    def __init__(self, dimensionality, crossover_rate, mutation_intensity, clip=True):
+        self.dimensionality = dimensionality
+        self.crossover_rate = crossover_rate
+        self.mutation_intensity = mutation_intensity
+        self.clip = clip
+
+    def _donors(self, population, L):
+        raise NotImplementedError()
+
+    def _clip(self):
+        return self.clip
+
+    def evolve(self, population):
+        mi = 5 if population.generation % 5 == 0 else self.mutation_intensity
+        n = len(population)
+        genomes = [population[i].get_internal_genome() for i in range(n)]
+        L = len(genomes[0])
+        if any(len(g) != L for g in genomes):
+            raise ValueError("DE needs internal genomes of one length (numpy broadcasting in evolver.py:132)")
+        donors, fixed = self._donors(population, L)
+        clip = self._clip()
+        dtypes = _child_dtypes(genomes, donors, self.strategy, mi, clip)
+        children = GpuDEStep.get(self.device).step(self.strategy, np.stack(genomes), donors, fixed, mi,
+                                                   self.crossover_rate, clip, self.dimensionality - 1)
+        next_pop = []
+        for i in range(n):
+            candidate = deepcopy(population[i])
+            # an own array per child (a row view would pin the whole generation's block)
+            candidate.set_internal_genome(np.array(children[i], dtype=None if dtypes is None else dtypes[i]))
+            next_pop.append(candidate)
+        return next_pop
+
+
+class DERandOneEvolver(_GpuDEEvolver):
+    """DE/rand/1 (evolver.py:86-157)."""
+
+    strategy = _native.DE_STRATEGY["de_rand_1"]
+
+    def _donors(self, population, L):
+        n = len(population)
+        donors = np.empty((n, 3), dtype=np.int32)
+        fixed = np.empty(n, dtype=np.int64)
+        for i in range(n):   # de_rand_one (evolver.py:118-121) then crossover (evolver.py:76)
+            a = exclusive_randrange(0, n, [i])
+            b = exclusive_randrange(0, n, [i, a])
+            c = exclusive_randrange(0, n, [i, a, b])
+            donors[i] = (a, b, c)
+            fixed[i] = random.randrange(0, L)
+        return donors, fixed
+
+
+class DECurrentToBestOneEvolver(_GpuDEEvolver):
+    """DE/current-to-best/1 (evolver.py:160-244)."""
+
+    strategy = _native.DE_STRATEGY["de_currenttobest_1"]
+
+    def _clip(self):
+        return True   # evolve() calls de_currenttobest_one without clip (default True)
+
+    def _donors(self, population, L):
+        n = len(population)
+        best = max(population, key=lambda individual: individual.fitness)   # evolver.py:235
+        best_index = population.population.index(best)                      # evolver.py:194
+        donors = np.empty((n, 3), dtype=np.int32)
+        fixed = np.empty(n, dtype=np.int64)
+        for i in range(n):   # evolver.py:199-203, then crossover (evolver.py:76)
+            exclusion_list = [i, best_index]
+            a = exclusive_randrange(0, n, exclusion_list)
+            exclusion_list.append(a)
+            b = exclusive_randrange(0, n, exclusion_list)
+            donors[i] = (best_index, a, b)
+            fixed[i] = random.randrange(0, L)
+        return donors, fixed

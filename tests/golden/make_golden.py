@@ -325,6 +325,97 @@ def gen_blup_config2():
                         fitness=np.array(fits), ebv=np.stack(ebvs[:3]), ebv_gblup=ebvs[3])
 
 
+class _Pop:
+    """The slice of tblup.Population the evolvers read: .population, .generation, [], len."""
+
+    def __init__(self, individuals, generation):
+        self.population = individuals
+        self.generation = generation
+
+    def __getitem__(self, i):
+        return self.population[i]
+
+    def __len__(self):
+        return len(self.population)
+
+
+DE_CASES = [
+    # name, individual kind, strategy, d, length, pop, generation, cr, F, clip, pre_draws
+    ("rk_rand1", "rk", "de_rand_1", 1000, 50, 8, 1, 0.8, 0.5, False, 0),
+    ("rk_rand1_f5", "rk", "de_rand_1", 700, 40, 6, 5, 0.8, 0.5, False, 3),
+    ("rk_rand1_clip", "rk", "de_rand_1", 333, 20, 5, 10, 0.9, 0.5, True, 1),
+    ("rk_ctb", "rk", "de_currenttobest_1", 300, 30, 6, 3, 0.8, 0.5, False, 7),
+    ("coev_rand1", "coev", "de_rand_1", 200, 20, 5, 2, 0.7, 0.6, False, 2),
+    ("index_rand1_int", "index", "de_rand_1", 500, 25, 6, 5, 0.8, 0.5, True, 5),
+    ("index_ctb", "index", "de_currenttobest_1", 500, 25, 5, 4, 0.5, 0.5, True, 0),
+]
+
+
+def gen_de():
+    """One generation of the reference's DE evolvers (evolver.py:86-244) from seeded RNG states:
+    parents, fitness, the children's internal genomes and the RNG states afterwards."""
+    from tblup.evolver import DERandOneEvolver, DECurrentToBestOneEvolver
+    from tblup.individual import RandomKeyIndividual, CoevolutionIndividual, IndexIndividual
+    out = {}
+    for ci, (name, kind, strat, d, length, pop, gen, cr, F, clip, pre) in enumerate(DE_CASES):
+        rng = np.random.default_rng(100 + ci)
+        if kind == "index":
+            parents = [rng.integers(0, d, size=length) for _ in range(pop)]
+            inds = [IndexIndividual(length, d, genome=g.copy()) for g in parents]
+        elif kind == "coev":
+            keys = rng.uniform(size=(pop, d))
+            lens = rng.integers(int(length * 0.9), int(length * 1.1) + 1, size=pop)
+            inds = []
+            for i in range(pop):
+                ind = CoevolutionIndividual(length, d, genome=keys[i].copy())
+                ind.length = int(lens[i])
+                inds.append(ind)
+            parents = [ind.get_internal_genome() for ind in inds]
+        else:
+            parents = [rng.uniform(size=d) for _ in range(pop)]
+            inds = [RandomKeyIndividual(length, d, genome=g.copy()) for g in parents]
+        fit = rng.uniform(size=pop)
+        for ind, f in zip(inds, fit):
+            ind.fitness = float(f)
+        random.seed(1000 + ci)
+        np.random.seed(2000 + ci)
+        np.random.rand(pre)   # move numpy's pos off the block boundary
+        ev = (DERandOneEvolver if strat == "de_rand_1" else DECurrentToBestOneEvolver)(d, cr, F, clip)
+        kids = ev.evolve(_Pop(inds, gen))
+        st = np.random.get_state()
+        p = "de_%s_" % name
+        out[p + "parents"] = np.stack([np.asarray(g) for g in parents])
+        out[p + "fitness"] = fit
+        out[p + "children"] = np.stack([np.asarray(k.get_internal_genome()) for k in kids])
+        out[p + "children_dtype"] = np.array(str(np.asarray(kids[0].get_internal_genome()).dtype))
+        out[p + "mt_key"] = np.asarray(st[1], dtype=np.uint32)
+        out[p + "mt_pos"] = np.int64(st[2])
+        out[p + "py_next"] = np.float64(random.random())
+    # a config-2-sized generation by checksum: pop 32 of d = 50000 RandomKey genomes
+    rng = np.random.default_rng(7)
+    d, pop = 50000, 32
+    keys = rng.uniform(size=(pop, d))
+    fit = rng.uniform(size=pop)
+    for strat in ("de_rand_1", "de_currenttobest_1"):
+        inds = [RandomKeyIndividual(1000, d, genome=keys[i].copy()) for i in range(pop)]
+        for ind, f in zip(inds, fit):
+            ind.fitness = float(f)
+        random.seed(31)
+        np.random.seed(32)
+        np.random.rand(11)
+        ev = (DERandOneEvolver if strat == "de_rand_1" else DECurrentToBestOneEvolver)(d, 0.8, 0.5, False)
+        kids = ev.evolve(_Pop(inds, 1))
+        st = np.random.get_state()
+        p = "big_%s_" % strat
+        out[p + "children_sha256"] = np.array(sha(np.stack([k.get_internal_genome() for k in kids])))
+        out[p + "children_row0"] = kids[0].get_internal_genome()[:64]
+        out[p + "mt_key"] = np.asarray(st[1], dtype=np.uint32)
+        out[p + "mt_pos"] = np.int64(st[2])
+        out[p + "py_next"] = np.float64(random.random())
+    out["big_d"], out["big_pop"] = d, pop
+    np.savez_compressed(os.path.join(HERE, "de.npz"), **out)
+
+
 if __name__ == "__main__":
     gen_grm()
     gen_blup_small()
@@ -332,4 +423,5 @@ if __name__ == "__main__":
     gen_decode()
     gen_evaluator_flow()
     gen_blup_config2()
+    gen_de()
     print("golden fixtures written to", HERE)

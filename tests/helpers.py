@@ -33,6 +33,60 @@ class KeyIndividual:
         self.fitness = f
 
 
+    def get_internal_genome(self):
+        return self._genome
+
+    def set_internal_genome(self, genome):
+        self._genome = genome
+
+    def __deepcopy__(self, memo):
+        """individual.py:43-59 / 110-118: same class and attributes, a new uid."""
+        cp = self.__class__.__new__(self.__class__)
+        cp.__dict__.update(self.__dict__)
+        cp.uid = next(_uid)
+        return cp
+
+
+class CoevoIndividual(KeyIndividual):
+    """CoevolutionIndividual stand-in (tblup/individual.py:170-222): the length rides along
+    as the last element of the internal genome."""
+
+    def __init__(self, keys, length, dimensionality):
+        super().__init__(keys, length)
+        self.dimensionality = dimensionality
+
+    def get_internal_genome(self):
+        return np.append(self._genome, self.length)
+
+    def set_internal_genome(self, genome):
+        if len(genome) == self.dimensionality + 1:
+            if genome[-1] < 1:
+                self.length = 1
+            elif genome[-1] > self.dimensionality:
+                self.length = self.dimensionality
+            else:
+                self.length = genome[-1]
+            self._genome = np.delete(genome, -1)
+        elif len(genome) == self.dimensionality:
+            self._genome = genome
+        else:
+            raise RuntimeError("Genome of invalid length, must be dimensionality d or d + 1.")
+
+
+class Pop:
+    """The slice of tblup.Population the evolvers read (.population, .generation, [], len)."""
+
+    def __init__(self, individuals, generation):
+        self.population = individuals
+        self.generation = generation
+
+    def __getitem__(self, i):
+        return self.population[i]
+
+    def __len__(self):
+        return len(self.population)
+
+
 class IdxIndividual(KeyIndividual):
     """IndexIndividual stand-in (tblup/individual.py:73-130)."""
 

@@ -13,7 +13,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(tblup_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(tblup_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_loads_and_exports_every_declared_symbol():

@@ -1,0 +1,124 @@
+"""DE step host side (no GPU): the oracle against the reference's goldens, the MT19937
+jump-ahead of libtblup_gpu.so against numpy, and the evolver factory."""
+import ctypes
+import os
+import random
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from oracle import de_oracle as D
+from tblup_amd import _native
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "de.npz")
+CASES = ["rk_rand1", "rk_rand1_f5", "rk_rand1_clip", "rk_ctb", "coev_rand1", "index_rand1_int", "index_ctb"]
+# name -> (strategy, d, generation, cr, F, clip, pre_draws, case index): tests/golden/make_golden.py DE_CASES
+META = {
+    "rk_rand1": ("de_rand_1", 1000, 1, 0.8, 0.5, False, 0, 0),
+    "rk_rand1_f5": ("de_rand_1", 700, 5, 0.8, 0.5, False, 3, 1),
+    "rk_rand1_clip": ("de_rand_1", 333, 10, 0.9, 0.5, True, 1, 2),
+    "rk_ctb": ("de_currenttobest_1", 300, 3, 0.8, 0.5, False, 7, 3),
+    "coev_rand1": ("de_rand_1", 200, 2, 0.7, 0.6, False, 2, 4),
+    "index_rand1_int": ("de_rand_1", 500, 5, 0.8, 0.5, True, 5, 5),
+    "index_ctb": ("de_currenttobest_1", 500, 4, 0.5, 0.5, True, 0, 6),
+}
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD)
+
+
+def seed_rngs(ci, pre):
+    random.seed(1000 + ci)
+    np.random.seed(2000 + ci)
+    np.random.rand(pre)
+
+
+def coev_post(child, d):
+    """CoevolutionIndividual.set_internal_genome then get_internal_genome (individual.py:184-208)."""
+    L = child[-1]
+    L = 1 if L < 1 else (d if L > d else L)
+    return np.append(child[:-1], L)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference_de_goldens(gold, name):
+    strat, d, gen, cr, F, clip, pre, ci = META[name]
+    p = "de_%s_" % name
+    parents = [np.array(r) for r in gold[p + "parents"]]
+    seed_rngs(ci, pre)
+    kids = D.de_generation(parents, list(gold[p + "fitness"]), gen, strat, d, cr, F, clip)
+    if name.startswith("coev"):
+        kids = [coev_post(k, d) for k in kids]
+    want = gold[p + "children"]
+    got = np.stack(kids)
+    assert str(got.dtype) == str(gold[p + "children_dtype"])
+    assert np.array_equal(got, want)
+    st = np.random.get_state()
+    assert np.array_equal(np.asarray(st[1], np.uint32), gold[p + "mt_key"]) and st[2] == int(gold[p + "mt_pos"])
+    assert random.random() == float(gold[p + "py_next"])
+
+
+def _jump(key, pos, n):
+    lib = _native.load()
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.empty(624, dtype=np.uint32)
+    po = ctypes.c_int32(0)
+    U32 = ctypes.POINTER(ctypes.c_uint32)
+    _native.check("tblup_mt19937_jump", lib.tblup_mt19937_jump(k.ctypes.data_as(U32), int(pos), int(n),
+                                                               out.ctypes.data_as(U32), ctypes.byref(po)))
+    return out, po.value
+
+
+@pytest.mark.parametrize("pre", [0, 1, 311, 623, 624, 1000])
+@pytest.mark.parametrize("n", [0, 1, 2, 623, 624, 625, 1247, 1248, 99999, 2 * 50000 * 3 + 5])
+def test_mt19937_jump_equals_numpy_stream(pre, n):
+    """Host GF(2) jump (mt_jump.cpp) == drawing n 32-bit words, in numpy's own (key, pos)."""
+    bg = np.random.MT19937(12345)
+    rs = np.random.RandomState(bg)
+    rs.bytes(4 * pre) if pre else None
+    st = bg.state["state"]
+    key, pos = st["key"].copy(), st["pos"]
+    got_key, got_pos = _jump(key, pos, n)
+    if n:
+        bg.random_raw(n)
+    st2 = bg.state["state"]
+    assert got_pos == st2["pos"]
+    assert np.array_equal(got_key, st2["key"])
+
+
+def test_jump_drives_legacy_rand_like_the_reference():
+    """numpy's legacy rand(L) uses two words per double: a state jumped by 2L matches."""
+    np.random.seed(5)
+    np.random.rand(3)
+    st = np.random.get_state()
+    key, pos = _jump(st[1], st[2], 2 * 4321)
+    np.random.rand(4321)
+    want = np.random.rand(50)
+    np.random.set_state(("MT19937", key, pos, 0, 0.0))
+    assert np.array_equal(np.random.rand(50), want)
+
+
+def test_get_evolver_factory():
+    from tblup_amd import evolver as E
+    args = SimpleNamespace(de_strategy="de_rand_1", dimensionality=100, crossover_rate=0.8,
+                           mutation_intensity=0.5, clip=False)
+    ev = E.get_evolver(args)
+    assert isinstance(ev, E.DERandOneEvolver) and ev.clip is False
+    args.de_strategy = "de_currenttobest_1"
+    assert isinstance(E.get_evolver(args), E.DECurrentToBestOneEvolver)
+    for bad in ("sade", "mde_pbx", "nope"):
+        args.de_strategy = bad
+        with pytest.raises(NotImplementedError):
+            E.get_evolver(args)
+
+
+def test_exclusive_randrange_consumes_like_reference():
+    from tblup_amd.evolver import exclusive_randrange
+    random.seed(3)
+    a = [exclusive_randrange(0, 5, [0, 1, 2]) for _ in range(20)]
+    random.seed(3)
+    b = [D.exclusive_randrange(0, 5, [0, 1, 2]) for _ in range(20)]
+    assert a == b and all(x in (3, 4) for x in a)

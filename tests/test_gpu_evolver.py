@@ -1,0 +1,118 @@
+"""GPU DE step (k_de.hip through tblup_de_step): children and RNG states bit-exact to the
+reference's evolvers (goldens) and to the numpy oracle at config-2 size."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from oracle import de_oracle as D
+from tests.helpers import CoevoIndividual, IdxIndividual, KeyIndividual, Pop
+from tests.test_evolver import CASES, META, coev_post, seed_rngs  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gold(golden_dir, gpu):
+    import os
+    return np.load(os.path.join(golden_dir, "de.npz"))
+
+
+def _evolver(strat, d, cr, F, clip):
+    from tblup_amd import evolver as E
+    cls = E.DERandOneEvolver if strat == "de_rand_1" else E.DECurrentToBestOneEvolver
+    return cls(d, cr, F, clip)
+
+
+def _individuals(name, parents, fitness, d):
+    inds = []
+    for g, f in zip(parents, fitness):
+        if name.startswith("coev"):
+            ind = CoevoIndividual(np.array(g[:-1]), float(g[-1]), d)
+        elif name.startswith("index"):
+            ind = IdxIndividual(np.array(g), len(g))
+        else:
+            ind = KeyIndividual(np.array(g), 10)
+        ind.fitness = float(f)
+        inds.append(ind)
+    return inds
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_de_matches_reference_goldens(gold, name):
+    strat, d, gen, cr, F, clip, pre, ci = META[name]
+    p = "de_%s_" % name
+    inds = _individuals(name, gold[p + "parents"], gold[p + "fitness"], d)
+    seed_rngs(ci, pre)
+    kids = _evolver(strat, d, cr, F, clip).evolve(Pop(inds, gen))
+    got = np.stack([np.asarray(k.get_internal_genome()) for k in kids])
+    assert str(got.dtype) == str(gold[p + "children_dtype"])
+    assert np.array_equal(got, gold[p + "children"])
+    assert len({k.uid for k in kids} | {i.uid for i in inds}) == 2 * len(inds)   # fresh uids (deepcopy)
+    st = np.random.get_state()
+    assert np.array_equal(np.asarray(st[1], np.uint32), gold[p + "mt_key"]) and st[2] == int(gold[p + "mt_pos"])
+    assert random.random() == float(gold[p + "py_next"])
+
+
+@pytest.mark.parametrize("strat", ["de_rand_1", "de_currenttobest_1"])
+def test_gpu_de_big_goldens(gold, strat):
+    d, pop = int(gold["big_d"]), int(gold["big_pop"])
+    rng = np.random.default_rng(7)
+    keys = rng.uniform(size=(pop, d))
+    fit = rng.uniform(size=pop)
+    inds = [KeyIndividual(keys[i].copy(), 1000) for i in range(pop)]
+    for ind, f in zip(inds, fit):
+        ind.fitness = float(f)
+    random.seed(31)
+    np.random.seed(32)
+    np.random.rand(11)
+    kids = _evolver(strat, d, 0.8, 0.5, False).evolve(Pop(inds, 1))
+    p = "big_%s_" % strat
+    got = np.stack([k.get_internal_genome() for k in kids])
+    assert np.array_equal(got[0, :64], gold[p + "children_row0"])
+    assert hashlib.sha256(np.ascontiguousarray(got).tobytes()).hexdigest() == str(gold[p + "children_sha256"])
+    st = np.random.get_state()
+    assert np.array_equal(np.asarray(st[1], np.uint32), gold[p + "mt_key"]) and st[2] == int(gold[p + "mt_pos"])
+    assert random.random() == float(gold[p + "py_next"])
+
+
+@pytest.mark.parametrize("gen,pre", [(1, 0), (5, 623), (7, 624)])
+def test_gpu_de_config2_vs_oracle(gpu, gen, pre):
+    """pop 256 x d 50000 (BASELINE config 2), three generations in a row against the oracle."""
+    d, pop = 50000, 256
+    rng = np.random.default_rng(gen)
+    keys = rng.uniform(size=(pop, d))
+    fit = list(rng.uniform(size=pop))
+    inds = [KeyIndividual(keys[i].copy(), 1000) for i in range(pop)]
+    for ind, f in zip(inds, fit):
+        ind.fitness = f
+    ev = _evolver("de_rand_1", d, 0.8, 0.5, False)
+    genomes = [keys[i] for i in range(pop)]
+    random.seed(gen)
+    np.random.seed(gen)
+    np.random.bytes(4 * pre)
+    for g in range(gen, gen + 3):
+        py, npst = random.getstate(), np.random.get_state()
+        kids = ev.evolve(Pop(inds, g))
+        py_after, np_after = random.getstate(), np.random.get_state()
+        random.setstate(py)
+        np.random.set_state(npst)
+        want = D.de_generation(genomes, fit, g, "de_rand_1", d, 0.8, 0.5, False)
+        assert random.getstate() == py_after
+        st = np.random.get_state()
+        assert np.array_equal(st[1], np_after[1]) and st[2] == np_after[2]
+        for k, w in zip(kids, want):
+            assert np.array_equal(k.get_internal_genome(), w)
+        inds, genomes = kids, want
+
+
+def test_gpu_de_bad_arguments_raise(gpu):
+    from tblup_amd import _native
+    from tblup_amd.evolver import GpuDEStep
+    step = GpuDEStep.get(0)
+    par = np.zeros((4, 10))
+    with pytest.raises(_native.TblupError):
+        step.step(0, par, np.array([[1, 2, 4]] * 4), np.zeros(4), 0.5, 0.8, False, 9)   # donor 4 of pop 4
+    with pytest.raises(_native.TblupError):
+        step.step(0, par, np.array([[1, 2, 3]] * 4), np.full(4, 10), 0.5, 0.8, False, 9)   # fixed >= L
