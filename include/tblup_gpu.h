@@ -170,6 +170,15 @@ int tblup_debug_grm(tblup_ctx* ctx, int split_id, const int64_t* idx, int64_t k,
                     int branch, int stage, double* out, double* z_out);
 
 /*
+ * VanRaden GRM of the selected columns over ALL animals, make_grm(data[:, idx])
+ * (tblup/utils.py:7-18): G = W W^T / (2 sum p(1-p)), W = Z - 2p, p = column mean / 2.
+ * Exact-integer A A^T on int8 MFMA plus the fp64 rank-1 centring (k_grm).  `G` is
+ * n_animals x n_animals row-major (host).  Used by the PCA splitter
+ * (pca_splitter, evaluator.py:641-663, with idx = every SNP).  Synchronous.
+ */
+int tblup_grm(tblup_ctx* ctx, const int64_t* idx, int64_t k, double* G);
+
+/*
  * One differential-evolution generation (mutation + binary crossover + clip) for a
  * population of `pop` internal genomes of length L, bit-exact to the reference:
  *   TBLUP_DE_RAND_1            DERandOneEvolver.de_rand_one   tblup/evolver.py:103-138

@@ -771,6 +771,29 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
   return 0;
 }
 
+int tblup_grm(tblup_ctx* c, const int64_t* idx, int64_t k, double* G) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (c->n == 0) return fail(TBLUP_ERR_STATE, "context has no genotype panel");
+  if (!idx || k < 1 || !G) return fail(TBLUP_ERR_ARG, "bad grm arguments");
+  const int64_t n = c->n;
+  // G = K_TT of the gblup-branch kernel form with T = every animal (p over all rows, as
+  // make_grm) and lambda = 0 (h2 = 1); V is a placeholder the solve never reaches
+  std::vector<int64_t> T(n);
+  for (int64_t i = 0; i < n; ++i) T[i] = i;
+  const int64_t V[2] = {0, 1};
+  const int sid = -0x7ffffff0;   // reserved id, dropped before returning
+  if (int rc = tblup_set_split(c, sid, T.data(), n, V, 2)) return rc;
+  std::vector<double> K((size_t)(n + 2) * n);
+  const int rc = tblup_debug_grm(c, sid, idx, k, 1.0, TBLUP_BRANCH_GBLUP, 1, K.data(), nullptr);
+  const std::string err = g_err;
+  tblup_drop_split(c, sid);
+  if (rc) return fail(rc, err);
+  for (int64_t r = 0; r < n; ++r)   // lower-triangle tiles are computed; mirror the upper triangle
+    for (int64_t cc = 0; cc < n; ++cc) G[r * n + cc] = cc <= r ? K[(size_t)r * n + cc] : K[(size_t)cc * n + r];
+  return 0;
+}
+
 // ---- differential-evolution step (k_de.hip; jump polynomials from mt_jump.cpp) ----
 
 int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint32_t* key_out, int32_t* pos_out) {

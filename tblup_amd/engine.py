@@ -166,6 +166,30 @@ class GpuBlupEngine:
             self._ctx, ctypes.c_void_p(d_keys_ptr), B, d, ld, ctypes.c_void_p(d_off_ptr), _ptr(h_off, ctypes.c_int64),
             ctypes.c_void_p(d_idx_ptr), ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def grm(self, indices=None):
+        """make_grm(data[:, indices]) over all animals (tblup/utils.py:7-18) on the GPU:
+        n x n float64.  indices=None: every SNP of the panel."""
+        idx = _as_int64(np.arange(self.n_snps) if indices is None else indices)
+        G = np.empty((self.n_animals, self.n_animals), dtype=np.float64)
+        _native.check("tblup_grm", self._lib.tblup_grm(self._ctx, _ptr(idx, ctypes.c_int64), len(idx),
+                                                       _ptr(G, ctypes.c_double)))
+        return G
+
+    def decode_randkey_tensor(self, keys, d, lengths):
+        """decode_randkey on a device tensor of key rows (B x ld float64, ld >= d, on this
+        context's device) on torch's current stream; returns host (idx, offsets)."""
+        import torch
+        B, ld = keys.shape
+        lens = np.broadcast_to(np.asarray(lengths), (B,)).astype(np.int64)
+        offsets = np.zeros(B + 1, dtype=np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        d_off = torch.from_numpy(offsets).to(keys.device)
+        d_idx = torch.empty(int(offsets[-1]), dtype=torch.int64, device=keys.device)
+        if B:
+            self.decode_randkey_device(keys.data_ptr(), B, d, keys.stride(0), d_off.data_ptr(), offsets,
+                                       d_idx.data_ptr(), torch.cuda.current_stream(keys.device).cuda_stream)
+        return d_idx.cpu().numpy(), offsets
+
     def evaluate_concat(self, idx, offsets, train, valid, h2, branch="auto"):
         """evaluate() on an already-concatenated (idx, offsets) batch."""
         sid = self.split_id(train, valid)

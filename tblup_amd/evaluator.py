@@ -30,8 +30,8 @@ def get_evaluator(args):
     """Factory with the reference's flag semantics (evaluator.py:14-55)."""
     splitter = None
     if args.splitter == "pca":
-        raise NotImplementedError(
-            "--splitter pca is not available in the MI355X evaluator yet (SURVEY.md section 8f)")
+        # evaluator.py:22-24: decorate the splitter so only the data is passed later
+        splitter = lambda data: pca_splitter(data, outliers=args.pca_outliers)  # noqa: E731
     r = args.features if args.removal_r is None else args.removal_r
     remover = SNPRemovalHandler(r, args.h2_alpha, args.heritability, args.remove_snps)
     common = dict(n_procs=args.processes, splitter=splitter, snp_remover=remover)
@@ -219,7 +219,15 @@ class BlupParallelEvaluator(ParallelEvaluator):
             d = keys[0].shape[0]
             lens = [int(i.length) for i in individuals]
             if all(k.ndim == 1 and k.shape[0] == d for k in keys) and all(1 <= n <= min(d, 8192) for n in lens):
-                idx, off = dec(np.stack(keys), lens)
+                # keys the GPU DE step left on the device (tblup_amd.keystore) decode in place
+                from .keystore import DeviceKeyStore
+                import torch
+                with torch.cuda.device(self.engine.device):
+                    dev = DeviceKeyStore.get(self.engine.device).gather(individuals, d)
+                    if dev is not None:
+                        idx, off = self.engine.decode_randkey_tensor(dev, d, lens)
+                    else:
+                        idx, off = dec(np.stack(keys), lens)
                 return [idx[off[j]:off[j + 1]] for j in range(len(individuals))]
         return [i.genome for i in individuals]
 
@@ -383,3 +391,36 @@ def _static_engine(data, labels):
         _STATIC.pop(k)[2].close()
     _STATIC[key] = (dref, lref, eng)
     return eng
+
+
+# ---------------------------------------------------------------------------
+# Splitters (evaluator.py:636-663)
+# ---------------------------------------------------------------------------
+def gpu_grm(data):
+    """make_grm(data) (tblup/utils.py:7-18) over every SNP, on the GPU (int8 MFMA, exact
+    integer A A^T + fp64 centring): a panel context opened for the call."""
+    from .engine import GpuBlupEngine
+    data = np.asarray(data)
+    eng = GpuBlupEngine(data, np.zeros(data.shape[0]), device=int(os.environ.get("LOCAL_RANK", "0")))
+    try:
+        return eng.grm()
+    finally:
+        eng.close()
+
+
+def pca_splitter(data, split=0.8, outliers=False, grm=None):
+    """PCA splitter (evaluator.py:641-663): project the GRM onto its first two principal
+    components (sklearn PCA, as the reference, including its use of numpy's global RNG by
+    the randomized solver), sort animals by squared distance from the projected mean
+    (descending when `outliers`), the first int(n * split) are the training animals.
+    The n^2 P GRM runs on the GPU (`grm` overrides it: the tests pass the oracle's)."""
+    from sklearn.decomposition import PCA
+    G = gpu_grm(data) if grm is None else grm(data)
+    proj = PCA(n_components=2)
+    x = proj.fit_transform(G)
+    centred = x - x.mean(axis=0)
+    dist = centred[:, 0] ** 2 + centred[:, 1] ** 2
+    # list.sort(key=dist, reverse=outliers) is stable in both directions: ties keep index order
+    order = np.argsort(-dist if outliers else dist, kind="stable")
+    cut = int(len(order) * split)
+    return [int(i) for i in order[:cut]], [int(i) for i in order[cut:]]

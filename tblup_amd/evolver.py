@@ -29,6 +29,7 @@ from copy import deepcopy
 import numpy as np
 
 from . import _native
+from .keystore import DeviceKeyStore
 
 
 def get_evolver(args):
@@ -76,6 +77,12 @@ class GpuDEStep:
         self._ctx = ctx
         self.device = int(device)
 
+    def _rng_state(self):
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise RuntimeError("numpy's global RandomState is not MT19937")
+        return st, np.array(st[1], dtype=np.uint32), ctypes.c_int32(int(st[2]))
+
     def step(self, strategy, parents, donors, fixed, F, cr, clip, clip_hi):
         """children (pop x L) for the current numpy global state, which is advanced
         past the generation's pop x L uniforms exactly as the reference's loop does."""
@@ -83,11 +90,7 @@ class GpuDEStep:
         pop, L = parents.shape
         donors = np.ascontiguousarray(donors, dtype=np.int32)
         fixed = np.ascontiguousarray(fixed, dtype=np.int64)
-        st = np.random.get_state()
-        if st[0] != "MT19937":
-            raise RuntimeError("numpy's global RandomState is not MT19937")
-        key = np.array(st[1], dtype=np.uint32)
-        pos = ctypes.c_int32(int(st[2]))
+        st, key, pos = self._rng_state()
         children = np.empty_like(parents)
         _native.check("tblup_de_step", self._lib.tblup_de_step(
             self._ctx, int(strategy), parents.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), pop, L,
@@ -95,6 +98,25 @@ class GpuDEStep:
             float(F), float(cr), 1 if clip else 0, float(clip_hi),
             key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
             children.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
+        return children
+
+    def step_device(self, strategy, parents, donors, fixed, F, cr, clip, clip_hi):
+        """Same on a device tensor of parents (pop x L float64, on this device); returns the
+        children as a device tensor.  Runs on torch's current stream."""
+        import torch
+        pop, L = parents.shape
+        donors = np.ascontiguousarray(donors, dtype=np.int32)
+        fixed = np.ascontiguousarray(fixed, dtype=np.int64)
+        children = torch.empty_like(parents)
+        st, key, pos = self._rng_state()
+        stream = torch.cuda.current_stream(parents.device).cuda_stream
+        _native.check("tblup_de_step_device", self._lib.tblup_de_step_device(
+            self._ctx, int(strategy), ctypes.c_void_p(parents.data_ptr()), pop, L, parents.stride(0),
+            donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+            float(F), float(cr), 1 if clip else 0, float(clip_hi),
+            key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
+            ctypes.c_void_p(children.data_ptr()), children.stride(0), ctypes.c_void_p(stream)))
         np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
         return children
 
@@ -155,14 +177,29 @@ class _GpuDEEvolver(Evolver):
         donors, fixed = self._donors(population, L)
         clip = self._clip()
         dtypes = _child_dtypes(genomes, donors, self.strategy, mi, clip)
-        children = GpuDEStep.get(self.device).step(self.strategy, np.stack(genomes), donors, fixed, mi,
-                                                   self.crossover_rate, clip, self.dimensionality - 1)
-        next_pop = []
+        step = GpuDEStep.get(self.device)
+        import torch
+        store = DeviceKeyStore.get(step.device)
+        inds = [population[i] for i in range(n)]
+        with torch.cuda.device(step.device):
+            parents = store.gather(inds, L, host_rows=lambda i: genomes[i])   # device-resident parents
+            children = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate, clip,
+                                        self.dimensionality - 1)
+            host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
+            host.copy_(children)
+        host = host.numpy()
+        next_pop, arrays = [], []
         for i in range(n):
             candidate = deepcopy(population[i])
             # an own array per child (a row view would pin the whole generation's block)
-            candidate.set_internal_genome(np.array(children[i], dtype=None if dtypes is None else dtypes[i]))
+            arr = np.array(host[i], dtype=None if dtypes is None else dtypes[i])
+            candidate.set_internal_genome(arr)
             next_pop.append(candidate)
+            arrays.append(arr)
+        if dtypes is None:   # float64 internal genomes: the device rows are the children's exact values
+            store.record(children, next_pop, arrays)
+            store.record(parents, inds, genomes)
+        store.prune([x.uid for x in inds] + [x.uid for x in next_pop])
         return next_pop
 
 

@@ -1,0 +1,114 @@
+"""Device-resident internal genomes of recent individuals, keyed by uid.
+
+The GPU DE step (tblup_amd.evolver) leaves each generation's children on the
+device; the evaluator decodes them there (k_decode_topk) and the next
+generation's DE step reads its parents there, so the population's keys cross
+PCIe once per generation (children to the host, for the reference's
+Individual objects) instead of three times (parents up, children down, keys up
+again for the decode).
+
+An entry is valid while the individual still holds the very numpy array the
+entry was recorded with (`indv._genome is <recorded array>`, arrays made
+read-only when recorded) and the same `length`: `set_internal_genome` and
+`fill` (the only ways the reference changes a genome, individual.py:103-130,
+187-208, scheduler.py:209-251) either replace the array or change the length,
+which invalidates the entry; the individual is then read from the host.
+Device memory is plumbing here: torch tensors on the context's device.
+"""
+import weakref
+
+import numpy as np
+
+
+class DeviceKeyStore:
+    _instances = {}
+
+    @classmethod
+    def get(cls, device):
+        inst = cls._instances.get(device)
+        if inst is None:
+            inst = cls._instances[device] = cls(device)
+        return inst
+
+    def __init__(self, device):
+        self.device = int(device)
+        self._entries = {}   # uid -> (tensor, row, weakref(genome array), length)
+
+    @staticmethod
+    def _key_array(indv):
+        g = getattr(indv, "_genome", None)
+        return g if isinstance(g, np.ndarray) else None
+
+    def record(self, tensor, individuals, arrays):
+        """Row i of `tensor` (pop x L, on the device) holds arrays[i]; recorded for individuals
+        whose internal genome IS that array (RandomKey / Index semantics: get_internal_genome()
+        returns `_genome`).  Individuals that derive their internal genome (Coevolution appends
+        its length) are not recorded and are read from the host."""
+        for i, indv in enumerate(individuals):
+            g = self._key_array(indv)
+            if g is None or g is not arrays[i]:
+                continue
+            g.flags.writeable = False
+            self._entries[indv.uid] = (tensor, i, weakref.ref(g), getattr(indv, "length", None))
+
+    def lookup(self, indv):
+        e = self._entries.get(indv.uid)
+        if e is None:
+            return None
+        tensor, row, ref, length = e
+        if ref() is not self._key_array(indv) or getattr(indv, "length", None) != length:
+            del self._entries[indv.uid]
+            return None
+        return tensor, row
+
+    def rows(self, individuals):
+        """(tensor, row) per individual (None where absent)."""
+        return [self.lookup(i) for i in individuals]
+
+    def gather(self, individuals, L, host_rows=None):
+        """A contiguous (len(individuals) x L) float64 device tensor of their internal genomes;
+        rows not in the store come from host_rows(i) (None -> return None if any is missing).
+        No copy when the individuals are exactly one recorded block in order."""
+        import torch
+        hits = self.rows(individuals)
+        n = len(individuals)
+        if n and all(h is not None for h in hits):
+            t0 = hits[0][0]
+            if t0.shape == (n, L) and all(h[0] is t0 and h[1] == i for i, h in enumerate(hits)):
+                return t0
+        if host_rows is None and any(h is None for h in hits):
+            return None
+        out = torch.empty((n, L), dtype=torch.float64, device="cuda:%d" % self.device)
+        by_tensor = {}
+        missing = []
+        for i, h in enumerate(hits):
+            if h is None:
+                missing.append(i)
+            elif h[0].shape[1] != L:
+                return None if host_rows is None else self._fill_missing(out, list(range(n)), host_rows)
+            else:
+                by_tensor.setdefault(id(h[0]), (h[0], [], []))
+                by_tensor[id(h[0])][1].append(i)
+                by_tensor[id(h[0])][2].append(h[1])
+        for t, dst, src in by_tensor.values():
+            di = torch.tensor(dst, device=out.device)
+            si = torch.tensor(src, device=out.device)
+            out.index_copy_(0, di, t.index_select(0, si))
+        if missing:
+            self._fill_missing(out, missing, host_rows)
+        return out
+
+    @staticmethod
+    def _fill_missing(out, idx, host_rows):
+        import torch
+        host = torch.from_numpy(np.stack([np.asarray(host_rows(i), dtype=np.float64) for i in idx]))
+        out.index_copy_(0, torch.tensor(idx, device=out.device), host.to(out.device, non_blocking=False))
+        return out
+
+    def prune(self, keep_uids):
+        keep = set(keep_uids)
+        for uid in [u for u in self._entries if u not in keep]:
+            del self._entries[uid]
+
+    def clear(self):
+        self._entries.clear()

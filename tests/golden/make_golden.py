@@ -416,6 +416,26 @@ def gen_de():
     np.savez_compressed(os.path.join(HERE, "de.npz"), **out)
 
 
+def gen_pca():
+    """pca_splitter (evaluator.py:641-663) on synthetic panels: n = 200 (sklearn's full SVD)
+    and n = 600 (randomized SVD drawing from numpy's global RNG, seeded), both directions."""
+    out = {}
+    for n, p, seed in ((200, 1000, 3), (600, 1500, 4)):
+        geno = synth_geno(np.random.default_rng(seed), n, p)
+        out["pca_%d_geno" % n] = geno
+        for outl in (False, True):
+            np.random.seed(50 + n)
+            tr, te = ref_ev.pca_splitter(geno, outliers=outl)
+            st = np.random.get_state()
+            tag = "pca_%d_%s_" % (n, "out" if outl else "in")
+            out[tag + "train"] = np.array(tr)
+            out[tag + "test"] = np.array(te)
+            out[tag + "mt_key"] = np.asarray(st[1], dtype=np.uint32)
+            out[tag + "mt_pos"] = np.int64(st[2])
+        out["pca_%d_grm" % n] = make_grm(geno)
+    np.savez_compressed(os.path.join(HERE, "pca.npz"), **out)
+
+
 if __name__ == "__main__":
     gen_grm()
     gen_blup_small()
@@ -424,4 +444,5 @@ if __name__ == "__main__":
     gen_evaluator_flow()
     gen_blup_config2()
     gen_de()
+    gen_pca()
     print("golden fixtures written to", HERE)

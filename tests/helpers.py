@@ -87,6 +87,11 @@ class Pop:
         return len(self.population)
 
 
+class RandomKeyIndividual(KeyIndividual):
+    """Same stand-in under the reference's class name: the evaluator batch-decodes
+    RandomKeyIndividual / CoevolutionIndividual genomes on the GPU (by class name)."""
+
+
 class IdxIndividual(KeyIndividual):
     """IndexIndividual stand-in (tblup/individual.py:73-130)."""
 

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from oracle import de_oracle as D
-from tests.helpers import CoevoIndividual, IdxIndividual, KeyIndividual, Pop
+from tests.helpers import CoevoIndividual, IdxIndividual, KeyIndividual, Pop, RandomKeyIndividual
 from tests.test_evolver import CASES, META, coev_post, seed_rngs  # noqa: F401
 
 pytestmark = pytest.mark.gpu
@@ -116,3 +116,67 @@ def test_gpu_de_bad_arguments_raise(gpu):
         step.step(0, par, np.array([[1, 2, 4]] * 4), np.zeros(4), 0.5, 0.8, False, 9)   # donor 4 of pop 4
     with pytest.raises(_native.TblupError):
         step.step(0, par, np.array([[1, 2, 3]] * 4), np.full(4, 10), 0.5, 0.8, False, 9)   # fixed >= L
+
+
+def test_gpu_generations_with_device_keystore(gpu, tmp_path):
+    """evolve -> evaluate -> select for 3 generations with the GPU evolver and evaluator (keys
+    stay on the device between them) equals the same loop with the host oracle DE and a
+    fresh store every generation (host-stacked decode)."""
+    from oracle import blup_oracle as O
+    from tblup_amd.evaluator import BlupParallelEvaluator
+    from tblup_amd.keystore import DeviceKeyStore
+    rng = np.random.default_rng(11)
+    n, p, k, pop = 400, 3000, 150, 24
+    geno = O.synth_geno(rng, n, p)
+    pheno = rng.standard_normal(n)
+    np.save(tmp_path / "g.npy", geno)
+    np.save(tmp_path / "y.npy", pheno)
+    keys0 = rng.uniform(size=(pop, p))
+
+    class P(Pop):
+        pass
+
+    def run(use_gpu_de):
+        random.seed(5)
+        np.random.seed(5)
+        ev = BlupParallelEvaluator(str(tmp_path / "g.npy"), str(tmp_path / "y.npy"), 0.4)
+        inds = [RandomKeyIndividual(keys0[i].copy(), k) for i in range(pop)]
+        fits = []
+        with ev:
+            popn = P(inds, 0)
+            ev.evaluate(popn, popn, 0)
+            evo = _evolver("de_rand_1", p, 0.8, 0.5, False)
+            for g in range(1, 4):
+                popn.generation = g
+                if use_gpu_de:
+                    kids = evo.evolve(popn)
+                    hits = DeviceKeyStore.get(0).rows(kids)
+                    assert all(h is not None for h in hits)
+                else:
+                    DeviceKeyStore.get(0).clear()
+                    want = D.de_generation([x.get_internal_genome() for x in popn.population],
+                                           [x.fitness for x in popn.population], g, "de_rand_1", p, 0.8, 0.5, False)
+                    kids = [RandomKeyIndividual(w, k) for w in want]
+                ev.evaluate(popn, kids, g)
+                popn.population = [c if c.fitness > q.fitness else q for q, c in zip(popn.population, kids)]
+                fits.append([x.fitness for x in kids])
+                genomes = [x.get_internal_genome().copy() for x in popn.population]
+        return fits, genomes
+
+    from tblup_amd.engine import GpuBlupEngine
+    calls = []
+    orig = GpuBlupEngine.decode_randkey_tensor
+
+    def spy(self, *a, **kw):
+        calls.append(1)
+        return orig(self, *a, **kw)
+    GpuBlupEngine.decode_randkey_tensor = spy
+    try:
+        f_gpu, g_gpu = run(True)
+    finally:
+        GpuBlupEngine.decode_randkey_tensor = orig
+    assert len(calls) == 3   # the children were decoded in place from the device key store
+    f_ref, g_ref = run(False)
+    assert f_gpu == f_ref
+    for a, b in zip(g_gpu, g_ref):
+        assert np.array_equal(a, b)

@@ -1,0 +1,84 @@
+"""End-to-end DE generation time through the drop-in Python classes at BASELINE config 2
+(2000 x 50k, k = 1000, pop 256): GPU evolve (tblup_amd.evolver) -> GPU evaluate
+(tblup_amd.evaluator, keys decoded in place from the device key store) -> selection,
+against the same generation with the host numpy evolve (oracle) and host argsort decode."""
+import json
+import os
+import random
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main(n=2000, p=50000, k=1000, pop=256, gens=4):
+    import torch  # noqa: F401
+    from oracle import blup_oracle as O
+    from oracle import de_oracle as D
+    from tests.helpers import RandomKeyIndividual, Pop
+    from tblup_amd.evaluator import BlupParallelEvaluator
+    from tblup_amd.evolver import DERandOneEvolver
+    rng = np.random.default_rng(0)
+    geno = O.synth_geno(rng, n, p)
+    pheno = rng.standard_normal(n)
+    tmp = tempfile.mkdtemp()
+    np.save(os.path.join(tmp, "g.npy"), geno)
+    np.save(os.path.join(tmp, "y.npy"), pheno)
+    random.seed(0)
+    np.random.seed(0)
+    ev = BlupParallelEvaluator(os.path.join(tmp, "g.npy"), os.path.join(tmp, "y.npy"), 0.4)
+    inds = [RandomKeyIndividual(rng.uniform(size=p), k) for _ in range(pop)]
+    evo = DERandOneEvolver(p, 0.8, 0.5, False)
+    out = {"n": n, "p": p, "k": k, "pop": pop}
+    phase = {}
+
+    def timed(obj, name):
+        fn = getattr(obj, name)
+
+        def wrap(*a, **kw):
+            t = time.perf_counter()
+            r = fn(*a, **kw)
+            phase[name] = phase.get(name, 0.0) + time.perf_counter() - t
+            return r
+        setattr(obj, name, wrap)
+    with ev:
+        for nm in ("genomes_to_evaluate", "_fitness", "_batch_genomes"):
+            timed(ev, nm)
+        timed(ev.engine, "evaluate")
+        timed(ev.engine, "decode_randkey_tensor")
+        popn = Pop(inds, 0)
+        ev.evaluate(popn, popn, 0)
+        ts = []
+        for g in range(1, gens + 1):
+            popn.generation = g
+            t0 = time.perf_counter()
+            kids = evo.evolve(popn)
+            t1 = time.perf_counter()
+            ev.evaluate(popn, kids, g)
+            t2 = time.perf_counter()
+            popn.population = [c if c.fitness > q.fitness else q for q, c in zip(popn.population, kids)]
+            ts.append((t1 - t0, t2 - t1, time.perf_counter() - t0))
+            if g == gens:
+                out["phases_last_gen_ms"] = {k: round(1e3 * v, 2) for k, v in phase.items()}
+            phase.clear()
+        best = min(ts, key=lambda t: t[2])
+        out.update({"gpu_evolve_ms": 1e3 * best[0], "gpu_evaluate_ms": 1e3 * best[1], "gpu_generation_ms": 1e3 * best[2],
+                    "gpu_generation_ms_all": [round(1e3 * t[2], 2) for t in ts]})
+        # host evolve (numpy restatement of the reference loop) + host decode, same population
+        genomes = [x.get_internal_genome() for x in popn.population]
+        t0 = time.perf_counter()
+        kids = D.de_generation(genomes, [x.fitness for x in popn.population], gens + 1, "de_rand_1", p, 0.8, 0.5,
+                               False)
+        t1 = time.perf_counter()
+        [np.argsort(c)[-k:] for c in kids]
+        t2 = time.perf_counter()
+        out.update({"host_evolve_ms": 1e3 * (t1 - t0), "host_decode_ms": 1e3 * (t2 - t1)})
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
