@@ -191,7 +191,7 @@ def main():
 
     # GPU genome decode of the same population (RandomKeyIndividual.genome, individual.py:154-156)
     # from device-resident keys: reported beside the metric, not part of it
-    decode_ms = None
+    decode_ms = de_ms = None
     if keys is not None:
         d_keys = torch.from_numpy(keys).cuda()
         d_dec = torch.empty(int(off[-1]), dtype=torch.int64, device="cuda")
@@ -207,6 +207,22 @@ def main():
         decode_ms = (time.perf_counter() - t1) / 5 * 1e3
         if not np.array_equal(d_dec.cpu().numpy(), idx):
             raise RuntimeError("GPU decode differs from the host argsort decode")
+        # GPU DE generation step on the same device-resident keys (tblup_amd.evolver,
+        # evolver.py:103-157): DE/rand/1 + binary crossover with numpy's MT19937 stream
+        # jumped per individual; reported beside the metric, not part of it
+        from tblup_amd.evolver import GpuDEStep
+        de = GpuDEStep.get(local_rank)
+        drng = np.random.default_rng(args.seed + 7)
+        donors = np.stack([drng.choice(pop, 3, replace=False) for _ in range(pop)]).astype(np.int32)
+        fixed = drng.integers(0, P, size=pop)
+        for _ in range(2):
+            de.step_device(0, d_keys, donors, fixed, 0.5, 0.8, False, P - 1)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(5):
+            de.step_device(0, d_keys, donors, fixed, 0.5, 0.8, False, P - 1)
+        torch.cuda.synchronize()
+        de_ms = (time.perf_counter() - t1) / 5 * 1e3
         del d_keys, d_dec
     fit = d_fit.cpu().numpy()
     if world > 1:
@@ -261,6 +277,7 @@ def main():
             "kernel_ms_per_step": step_ms,
             "ms_per_step_with_events": round(elapsed_events / args.steps * 1e3, 4),
             "gpu_decode_ms": None if decode_ms is None else round(decode_ms, 4),
+            "gpu_de_step_ms": None if de_ms is None else round(de_ms, 4),
             "fitness_checksum": float(np.nansum(fit)),
         }
         print(json.dumps(line), flush=True)

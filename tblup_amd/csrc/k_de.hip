@@ -14,6 +14,8 @@
 // with its jump polynomial (mt_jump.cpp), and then runs the MT19937 recurrence
 // forward in a two-block LDS ring, 312 doubles per 624-word block.  Workgroup `pop`
 // produces numpy's (key, pos) after the whole generation's draws.
+#include <cstdlib>
+
 #include "mt_jump.h"
 #include "tblup_internal.h"
 
@@ -23,6 +25,8 @@ namespace {
 constexpr int MTN = 624;
 constexpr int DE_THREADS = 640;                       // one thread per window word in the correlation
 constexpr int SEQ_WORDS = MTN + tblup_mt::MT_DEG + MTN - 1;   // base sequence read up to pos0 (<= 624) + 19937 + 623
+constexpr int SEQ_ALLOC = SEQ_WORDS + 64;                       // + alignment shift and the correlation's tail loads
+static_assert((DE_THREADS / 64) * MTN <= SEQ_WORDS, "correlation partials must fit the sequence buffer");
 
 __device__ __forceinline__ uint32_t mt_twist(uint32_t xt, uint32_t xt1, uint32_t xtm) {
   const uint32_t y = (xt & 0x80000000u) | (xt1 & 0x7fffffffu);
@@ -76,57 +80,75 @@ struct DeArgs {
   int64_t ldc;
   uint32_t* key_out;       // [624]
   int32_t* pos_out;
+  int dbg;                 // phase-ablation timing only (env TBLUP_DE_DBG; results wrong when set):
+                           // 1 no jump correlation, 2 no mask recurrence, 4 no stream
 };
 
 __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
 #pragma clang fp contract(off)
-  __shared__ uint32_t seq[SEQ_WORDS];
+  // sequence buffer, 16-B aligned at word pos0 (sq = seq + sh) so the correlation reads b128s;
+  // the slack covers the correlation's trailing loads (bits past degree 19936 are zero)
+  __shared__ __attribute__((aligned(16))) uint32_t seq[SEQ_ALLOC];
   __shared__ uint32_t ring[2 * MTN];
   const int tid = threadIdx.x;
   const int i = blockIdx.x;
   const bool is_end = i == a.pop;
   const bool jump = is_end ? a.end_jump != 0 : i > 0;
+  uint32_t* sq = seq + ((4 - (a.pos0 & 3)) & 3);
 
   // 1. the sequence that continues the base window, as far as this workgroup reads it
-  for (int t = tid; t < MTN; t += DE_THREADS) seq[t] = a.key[t];
+  for (int t = tid; t < MTN; t += DE_THREADS) sq[t] = a.key[t];
   const int need = jump ? a.pos0 + tblup_mt::MT_DEG + MTN - 1 : (i == 0 ? a.pos0 + MTN : MTN);
   for (int t0 = MTN; t0 < need; t0 += 227) {
     __syncthreads();
     const int t = t0 + tid;
-    if (tid < 227 && t < need) seq[t] = mt_twist(seq[t - 624], seq[t - 623], seq[t - 227]);
+    if (tid < 227 && t < need) sq[t] = mt_twist(sq[t - 624], sq[t - 623], sq[t - 227]);
   }
   __syncthreads();
 
-  // 2. this workgroup's start window: W[j] = XOR_{k: p_k} seq[pos0 + k + j]
+  // 2. this workgroup's start window: W[j] = XOR_{k: p_k} x[pos0 + k + j].  Wave g (of NW)
+  // takes poly words [624g/NW, 624(g+1)/NW); lane l < 63 owns outputs 10l .. 10l+9 and holds
+  // the 42 sequence words they read for one poly word in registers, so a set bit costs 10
+  // register XORs (scalar branch on the wave-uniform poly bit); the waves' partial windows are
+  // XOR-reduced through LDS.  VALU-bound: 624 x ~10k set bits XORs per workgroup.
   uint32_t w = 0;
-  if (tid < MTN) {
-    if (jump) {
-      const uint32_t* poly = a.polys + (int64_t)(is_end ? a.pop - 1 : i - 1) * MTN;
-      const uint32_t* s = seq + a.pos0 + tid;
-      uint32_t acc0 = 0, acc1 = 0;
-      for (int pw = 0; pw < MTN; ++pw) {
-        uint32_t cw = poly[pw];   // uniform: scalar load
-        const uint32_t* sp = s + 32 * pw;
-        while (cw) {
-          const int b0 = __builtin_ctz(cw);
-          cw &= cw - 1;
-          const uint32_t m1 = cw ? ~0u : 0u;
-          const int b1 = cw ? __builtin_ctz(cw) : 0;
-          cw &= cw - 1;
-          const uint32_t m2 = cw ? ~0u : 0u;
-          const int b2 = cw ? __builtin_ctz(cw) : 0;
-          cw &= cw - 1;
-          const uint32_t m3 = cw ? ~0u : 0u;
-          const int b3 = cw ? __builtin_ctz(cw) : 0;
-          cw &= cw - 1;
-          acc0 ^= sp[b0] ^ (sp[b1] & m1);
-          acc1 ^= (sp[b2] & m2) ^ (sp[b3] & m3);
-        }
+  if (jump && !(a.dbg & 1)) {
+    constexpr int NW = DE_THREADS / 64, R = 10, NL = (MTN + R - 1) / R;   // 63 lanes
+    const uint32_t* poly = a.polys + (int64_t)(is_end ? a.pop - 1 : i - 1) * MTN;
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int pw0 = MTN * g / NW, pw1 = MTN * (g + 1) / NW;
+    uint32_t acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0u;
+    if (lane < NL) {
+      const uint32_t* base = sq + a.pos0 + R * lane;
+      for (int pw = pw0; pw < pw1; ++pw) {
+        const uint32_t cw = poly[pw];   // wave-uniform: scalar load, scalar branches below
+        if (!cw) continue;
+        uint32_t v[32 + R];
+#pragma unroll
+        for (int q = 0; q < 32 + R; ++q) v[q] = base[32 * pw + q];
+#pragma unroll
+        for (int b = 0; b < 32; ++b)
+          if ((cw >> b) & 1u) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] ^= v[b + r];
+          }
       }
-      w = acc0 ^ acc1;
-    } else {
-      w = seq[(i == 0 ? a.pos0 : 0) + tid];
     }
+    __syncthreads();   // every wave is done reading the sequence: reuse it for the partials
+    if (lane < NL) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (R * lane + r < MTN) seq[g * MTN + R * lane + r] = acc[r];
+    }
+    __syncthreads();
+    if (tid < MTN) {
+#pragma unroll
+      for (int gg = 0; gg < NW; ++gg) w ^= seq[gg * MTN + tid];
+    }
+  } else if (tid < MTN) {
+    w = sq[(i == 0 ? a.pos0 : 0) + tid];
   }
   if (tid < MTN) ring[tid] = w;   // block 0 in slot 0
   __syncthreads();
@@ -138,7 +160,10 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
     return;
   }
 
-  // 3. stream: words [f, f + 2L) of the sequence from this window, one double per word pair
+  // 3. crossover mask, then the elementwise mutant / crossover / clip stream.  The mask of a
+  // segment of up to SEG elements is built in LDS (the sequence buffer is free now) from the
+  // MT19937 words [f, f + 2L) of this window, one double per word pair; the segment is then
+  // streamed with every thread (coalesced loads, many in flight) instead of 312 lanes per block.
   const int f = i == 0 ? 0 : 2;
   const int64_t L = a.L;
   const double* P = a.parent + (int64_t)i * a.ldp;
@@ -148,24 +173,56 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
   const double* X1 = a.parent + (int64_t)d1 * a.ldp;
   const double* X2 = a.parent + (int64_t)d2 * a.ldp;
   const int64_t fixed = a.fixed[i];
-  const int64_t nblocks = (f + 2 * L + MTN - 1) / MTN;
-  for (int64_t b = 0; b < nblocks; ++b) {
-    if (b > 0) mt_block(ring, (int)(b & 1), tid);
-    const uint32_t* blk = ring + (b & 1) * MTN;
-    const int q = tid;
-    if (q < MTN / 2 && !(b == 0 && q < f / 2)) {
-      const int64_t j = (MTN / 2) * b + q - f / 2;
-      if (j < L) {
-        const uint32_t hi = mt_temper(blk[2 * q]) >> 5, lo = mt_temper(blk[2 * q + 1]) >> 6;
-        const double u = ((double)hi * 67108864.0 + (double)lo) / 9007199254740992.0;
-        double v = P[j];
-        if (u < a.cr || j == fixed) {
-          if (a.strategy == 0) {
-            v = X0[j] + a.F * (X1[j] - X2[j]);
-          } else {
-            const double x = v;
-            v = (x + a.F * (X0[j] - x)) + a.F * (X1[j] - X2[j]);
+  uint32_t* mask = seq;                      // SEG bits
+  constexpr int64_t SEG = (int64_t)SEQ_WORDS * 32;
+  int64_t b = 0;                             // next ring block to consume (block 0 = the window)
+  for (int64_t lo = 0; lo < L; lo += SEG) {
+    const int64_t hi = lo + SEG < L ? lo + SEG : L;
+    __syncthreads();   // previous segment's stream has finished reading the mask
+    for (int t = tid; t < SEQ_WORDS; t += DE_THREADS) mask[t] = 0u;
+    __syncthreads();
+    // element j = 312 b + q - f/2 comes from block b, pair q
+    for (; !(a.dbg & 2) && (MTN / 2) * b - f / 2 < hi; ++b) {
+      if (b > 0) mt_block(ring, (int)(b & 1), tid);
+      const uint32_t* blk = ring + (b & 1) * MTN;
+      const int q = tid;
+      if (q < MTN / 2 && !(b == 0 && q < f / 2)) {
+        const int64_t j = (MTN / 2) * b + q - f / 2;
+        if (j >= lo && j < hi) {
+          const uint32_t w0 = mt_temper(blk[2 * q]) >> 5, w1 = mt_temper(blk[2 * q + 1]) >> 6;
+          const double u = ((double)w0 * 67108864.0 + (double)w1) / 9007199254740992.0;
+          if (u < a.cr || j == fixed) atomicOr(&mask[(j - lo) >> 5], 1u << ((j - lo) & 31));
+        }
+      }
+      if ((MTN / 2) * (b + 1) - f / 2 > hi) break;   // this block also feeds the next segment
+    }
+    __syncthreads();
+    constexpr int U = 4;
+    for (int64_t j0 = lo + tid; !(a.dbg & 4) && j0 < hi; j0 += (int64_t)U * DE_THREADS) {
+      double x[U], y0[U], y1[U], y2[U];
+      bool m[U];
+#pragma unroll
+      for (int r = 0; r < U; ++r) {
+        const int64_t j = j0 + (int64_t)r * DE_THREADS;
+        m[r] = false;
+        if (j < hi) {
+          x[r] = P[j];
+          m[r] = (mask[(j - lo) >> 5] >> ((j - lo) & 31)) & 1u;
+          if (m[r]) {
+            y0[r] = X0[j];
+            y1[r] = X1[j];
+            y2[r] = X2[j];
           }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < U; ++r) {
+        const int64_t j = j0 + (int64_t)r * DE_THREADS;
+        if (j >= hi) continue;
+        double v = x[r];
+        if (m[r]) {
+          if (a.strategy == 0) v = y0[r] + a.F * (y1[r] - y2[r]);
+          else v = (v + a.F * (y0[r] - v)) + a.F * (y1[r] - y2[r]);
         }
         if (a.clip) {   // numpy's _NPY_CLIP: MIN(MAX(v, 0), hi) with a > b ? a : b, NaN passes through
           v = (v != v || v > 0.0) ? v : 0.0;
@@ -183,8 +240,9 @@ hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, 
                           const double* parent, int64_t ldp, const int32_t* donors, const int64_t* fixed, int strategy,
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
                           uint32_t* key_out, int32_t* pos_out, hipStream_t s) {
+  static const int dbg = getenv("TBLUP_DE_DBG") ? atoi(getenv("TBLUP_DE_DBG")) : 0;
   DeArgs a{key, pos0, polys, end_jump, end_s, end_pos, parent, ldp, donors, fixed, strategy, F, cr, clip, hi, L, pop,
-           child, ldc, key_out, pos_out};
+           child, ldc, key_out, pos_out, dbg};
   hipLaunchKernelGGL(k_de_step, dim3(pop + 1), dim3(DE_THREADS), 0, s, a);
   return hipGetLastError();
 }

@@ -179,16 +179,21 @@ class GpuBlupEngine:
         """decode_randkey on a device tensor of key rows (B x ld float64, ld >= d, on this
         context's device) on torch's current stream; returns host (idx, offsets)."""
         import torch
+        from .keystore import work_stream
         B, ld = keys.shape
         lens = np.broadcast_to(np.asarray(lengths), (B,)).astype(np.int64)
         offsets = np.zeros(B + 1, dtype=np.int64)
         np.cumsum(lens, out=offsets[1:])
-        d_off = torch.from_numpy(offsets).to(keys.device)
-        d_idx = torch.empty(int(offsets[-1]), dtype=torch.int64, device=keys.device)
-        if B:
-            self.decode_randkey_device(keys.data_ptr(), B, d, keys.stride(0), d_off.data_ptr(), offsets,
-                                       d_idx.data_ptr(), torch.cuda.current_stream(keys.device).cuda_stream)
-        return d_idx.cpu().numpy(), offsets
+        ws = work_stream(keys.device.index)
+        ws.wait_stream(torch.cuda.current_stream(keys.device))
+        with torch.cuda.stream(ws):   # one stream for the copies and the library's kernel
+            d_off = torch.from_numpy(offsets).to(keys.device)
+            d_idx = torch.empty(int(offsets[-1]), dtype=torch.int64, device=keys.device)
+            if B:
+                self.decode_randkey_device(keys.data_ptr(), B, d, keys.stride(0), d_off.data_ptr(), offsets,
+                                           d_idx.data_ptr(), ws.cuda_stream)
+            out = d_idx.cpu().numpy()
+        return out, offsets
 
     def evaluate_concat(self, idx, offsets, train, valid, h2, branch="auto"):
         """evaluate() on an already-concatenated (idx, offsets) batch."""

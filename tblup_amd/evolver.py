@@ -29,7 +29,7 @@ from copy import deepcopy
 import numpy as np
 
 from . import _native
-from .keystore import DeviceKeyStore
+from .keystore import DeviceKeyStore, work_stream
 
 
 def get_evolver(args):
@@ -108,9 +108,13 @@ class GpuDEStep:
         pop, L = parents.shape
         donors = np.ascontiguousarray(donors, dtype=np.int32)
         fixed = np.ascontiguousarray(fixed, dtype=np.int64)
-        children = torch.empty_like(parents)
+        cur = torch.cuda.current_stream(parents.device)
+        ws = work_stream(self.device)
+        ws.wait_stream(cur)   # parents may come from work queued on the caller's stream
+        with torch.cuda.stream(ws):
+            children = torch.empty_like(parents)
         st, key, pos = self._rng_state()
-        stream = torch.cuda.current_stream(parents.device).cuda_stream
+        stream = ws.cuda_stream
         _native.check("tblup_de_step_device", self._lib.tblup_de_step_device(
             self._ctx, int(strategy), ctypes.c_void_p(parents.data_ptr()), pop, L, parents.stride(0),
             donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
@@ -118,6 +122,7 @@ class GpuDEStep:
             key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
             ctypes.c_void_p(children.data_ptr()), children.stride(0), ctypes.c_void_p(stream)))
         np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
+        cur.wait_stream(ws)   # (the call synchronised ws already; keeps later caller work ordered)
         return children
 
     def close(self):
@@ -141,6 +146,25 @@ def _child_dtypes(genomes, donors, strategy, mi, clip):
         r = np.where(e, mutant, t)
         out.append((np.clip(r, 0, 1) if clip else r).dtype)
     return out
+
+
+_POOL = None
+
+
+def _copy_rows(host, dtypes, workers=8):
+    global _POOL
+    n = host.shape[0]
+
+    def chunk(lo, hi):
+        return [np.array(host[i], dtype=None if dtypes is None else dtypes[i]) for i in range(lo, hi)]
+    if n * host.shape[1] < (1 << 20):
+        return chunk(0, n)
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(workers, thread_name_prefix="tblup-copy")
+    step = (n + workers - 1) // workers
+    parts = _POOL.map(lambda lo: chunk(lo, min(n, lo + step)), range(0, n, step))
+    return [a for part in parts for a in part]
 
 
 class Evolver(abc.ABC):
@@ -181,21 +205,21 @@ class _GpuDEEvolver(Evolver):
         import torch
         store = DeviceKeyStore.get(step.device)
         inds = [population[i] for i in range(n)]
-        with torch.cuda.device(step.device):
+        with torch.cuda.device(step.device), torch.cuda.stream(work_stream(step.device)):
             parents = store.gather(inds, L, host_rows=lambda i: genomes[i])   # device-resident parents
             children = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate, clip,
                                         self.dimensionality - 1)
             host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
             host.copy_(children)
         host = host.numpy()
-        next_pop, arrays = [], []
+        # an own array per child (a row view would pin the whole generation's block); the
+        # copies (first-touch page faults dominate) run in chunks on a few threads
+        arrays = _copy_rows(host, dtypes)
+        next_pop = []
         for i in range(n):
             candidate = deepcopy(population[i])
-            # an own array per child (a row view would pin the whole generation's block)
-            arr = np.array(host[i], dtype=None if dtypes is None else dtypes[i])
-            candidate.set_internal_genome(arr)
+            candidate.set_internal_genome(arrays[i])
             next_pop.append(candidate)
-            arrays.append(arr)
         if dtypes is None:   # float64 internal genomes: the device rows are the children's exact values
             store.record(children, next_pop, arrays)
             store.record(parents, inds, genomes)

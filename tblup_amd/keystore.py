@@ -20,6 +20,21 @@ import weakref
 import numpy as np
 
 
+_STREAMS = {}
+
+
+def work_stream(device):
+    """A dedicated (non-default) torch stream per device for the device-resident DE /
+    decode plumbing: its handle is passed to the C ABI, so the library's kernels and
+    torch's copies of the same tensors are ordered on one stream (the legacy default
+    stream does not order against the library's non-blocking context stream)."""
+    import torch
+    s = _STREAMS.get(device)
+    if s is None:
+        s = _STREAMS[device] = torch.cuda.Stream(device=device)
+    return s
+
+
 class DeviceKeyStore:
     _instances = {}
 
