@@ -179,6 +179,16 @@ int tblup_debug_grm(tblup_ctx* ctx, int split_id, const int64_t* idx, int64_t k,
 int tblup_grm(tblup_ctx* ctx, const int64_t* idx, int64_t k, double* G);
 
 /*
+ * Per-SNP sums over the animal rows `rows` (n_rows ids, any order): sx = sum x,
+ * sxx = sum x^2 (exact), sxy = sum x * yc (fp64; yc = the caller's centred phenotypes
+ * of those rows), for every SNP of the panel (outputs of length n_snps, host).  The data
+ * pass of the seeder's GWAS metric (sklearn f_regression over X[train],
+ * tblup/seeder.py:144-160, 202-210).  Synchronous.
+ */
+int tblup_snp_scan(tblup_ctx* ctx, const int64_t* rows, int64_t n_rows, const double* yc, int64_t* sx,
+                   int64_t* sxx, double* sxy);
+
+/*
  * One differential-evolution generation (mutation + binary crossover + clip) for a
  * population of `pop` internal genomes of length L, bit-exact to the reference:
  *   TBLUP_DE_RAND_1            DERandOneEvolver.de_rand_one   tblup/evolver.py:103-138

@@ -794,6 +794,43 @@ int tblup_grm(tblup_ctx* c, const int64_t* idx, int64_t k, double* G) {
   return 0;
 }
 
+int tblup_snp_scan(tblup_ctx* c, const int64_t* rows, int64_t n_rows, const double* yc, int64_t* sx, int64_t* sxx,
+                   double* sxy) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (c->n == 0) return fail(TBLUP_ERR_STATE, "context has no genotype panel");
+  if (!rows || n_rows < 1 || !yc || !sx || !sxx || !sxy) return fail(TBLUP_ERR_ARG, "bad scan arguments");
+  std::vector<int32_t> r32((size_t)n_rows);
+  for (int64_t i = 0; i < n_rows; ++i) {
+    if (rows[i] < 0 || rows[i] >= c->n) return fail(TBLUP_ERR_ARG, "animal row out of range");
+    r32[i] = (int32_t)rows[i];
+  }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const size_t P = (size_t)c->P;
+  DevBuf buf;
+  const size_t o_y = round_up(4 * (size_t)n_rows, 16), o_sx = o_y + 8 * (size_t)n_rows, o_sxx = o_sx + 8 * P,
+               o_sxy = o_sxx + 8 * P, bytes = o_sxy + 8 * P;
+  if (int rc = dev_alloc(c, buf, bytes)) return rc;
+  char* b = (char*)buf.p;
+  int rc = 0;
+  auto run = [&]() -> int {
+    HIPCHK(hipMemcpyAsync(b, r32.data(), 4 * (size_t)n_rows, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b + o_y, yc, 8 * (size_t)n_rows, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_snp_scan((const int8_t*)c->geno_sm.p, c->n, c->P, (const int32_t*)b, n_rows,
+                           (const double*)(b + o_y), (int64_t*)(b + o_sx), (int64_t*)(b + o_sxx),
+                           (double*)(b + o_sxy), c->stream));
+    HIPCHK(hipMemcpyAsync(sx, b + o_sx, 8 * P, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(sxx, b + o_sxx, 8 * P, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(sxy, b + o_sxy, 8 * P, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+  };
+  rc = run();
+  dev_free(c, buf);
+  return rc;
+}
+
 // ---- differential-evolution step (k_de.hip; jump polynomials from mt_jump.cpp) ----
 
 int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint32_t* key_out, int32_t* pos_out) {

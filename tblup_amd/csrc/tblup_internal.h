@@ -154,6 +154,10 @@ hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, 
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
                           uint32_t* key_out, int32_t* pos_out, hipStream_t s);
 
+// ---- launcher (k_scan.hip): per-SNP sums over a set of animals (seeder GWAS metric) ----
+hipError_t launch_snp_scan(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rows, int64_t nr,
+                           const double* yc, int64_t* sx, int64_t* sxx, double* sxy, hipStream_t s);
+
 // XCD-aware bijective remap of a 1-D block id (blocks b and b+8 share an XCD
 // under the observed round-robin placement; speed only, never correctness).
 __device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {

@@ -175,6 +175,20 @@ class GpuBlupEngine:
                                                        _ptr(G, ctypes.c_double)))
         return G
 
+    def snp_scan(self, rows, yc):
+        """Per-SNP (sum x, sum x^2, sum x*yc) over animal `rows` (k_snp_scan)."""
+        r = _as_int64(rows)
+        y = np.ascontiguousarray(yc, dtype=np.float64)
+        if y.shape != r.shape:
+            raise ValueError("yc must have one value per row")
+        sx = np.empty(self.n_snps, dtype=np.int64)
+        sxx = np.empty(self.n_snps, dtype=np.int64)
+        sxy = np.empty(self.n_snps, dtype=np.float64)
+        _native.check("tblup_snp_scan", self._lib.tblup_snp_scan(
+            self._ctx, _ptr(r, ctypes.c_int64), len(r), _ptr(y, ctypes.c_double), _ptr(sx, ctypes.c_int64),
+            _ptr(sxx, ctypes.c_int64), _ptr(sxy, ctypes.c_double)))
+        return sx, sxx, sxy
+
     def decode_randkey_tensor(self, keys, d, lengths):
         """decode_randkey on a device tensor of key rows (B x ld float64, ld >= d, on this
         context's device) on torch's current stream; returns host (idx, offsets)."""

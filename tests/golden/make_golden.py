@@ -436,6 +436,45 @@ def gen_pca():
     np.savez_compressed(os.path.join(HERE, "pca.npz"), **out)
 
 
+def gen_seed():
+    """The top-SNPs seeder (seeder.py:110-220): sklearn f_regression per fold, the SNP ranking,
+    and the first genomes of the RandomKey / Index seeders."""
+    from tblup.seeder import TopSNPsSeedStrategy, RandomKeySeeder, IndexSeeder, p_value, f_score
+    from sklearn.feature_selection import f_regression
+    rng = np.random.default_rng(21)
+    n, p = 300, 2000
+    geno = synth_geno(rng, n, p)
+    geno[:, 7] = 1                       # monomorphic SNP: force_finite path (F = 0, p = 1)
+    beta = np.zeros(p)
+    qtl = rng.choice(p, 30, replace=False)
+    beta[qtl] = rng.standard_normal(30)
+    g = geno.astype(np.float64) @ beta
+    pheno = g / g.std() * np.sqrt(0.5) + rng.standard_normal(n) * np.sqrt(0.5)
+    tmp = tempfile.mkdtemp()
+    gp, pp = os.path.join(tmp, "g.npy"), os.path.join(tmp, "y.npy")
+    np.save(gp, geno)
+    np.save(pp, pheno)
+    train = np.sort(rng.choice(n, 192, replace=False))
+
+    class Ev:
+        training_indices = list(train)
+    strat = TopSNPsSeedStrategy(Ev(), p_value, gp, pp)
+    out = {"geno": geno, "pheno": pheno, "training_indices": train, "sorted_indices": strat.indices}
+    rows = np.arange(150)
+    F, pv = f_regression(geno[rows], pheno[rows].ravel())
+    out.update({"f_rows": rows, "f_F": F, "f_p": pv, "f_score": f_score(geno[rows], pheno[rows])})
+    np.random.seed(8)
+    rk = RandomKeySeeder(strat, 40, p)
+    it = iter(rk)
+    out["rk_genomes"] = np.stack([next(it) for _ in range(3)])
+    ix = IndexSeeder(strat, 900)
+    it = iter(ix)
+    out["index_genomes"] = np.stack([next(it) for _ in range(2)])
+    out["index_random_tail"] = next(it)   # past the end: np.random.choice(indices, 900, replace=False)
+    out["mt_key"] = np.asarray(np.random.get_state()[1], dtype=np.uint32)
+    np.savez_compressed(os.path.join(HERE, "seed.npz"), **out)
+
+
 if __name__ == "__main__":
     gen_grm()
     gen_blup_small()
@@ -445,4 +484,5 @@ if __name__ == "__main__":
     gen_blup_config2()
     gen_de()
     gen_pca()
+    gen_seed()
     print("golden fixtures written to", HERE)
