@@ -224,6 +224,22 @@ def main():
         torch.cuda.synchronize()
         de_ms = (time.perf_counter() - t1) / 5 * 1e3
         del d_keys, d_dec
+    # the same two host steps the reference runs per generation (numpy evolve loop, argsort
+    # decode), timed beside them on rank 0 (oracle restatement; reported, not the metric)
+    host_ref = None
+    if cpu is not None and keys is not None:
+        import random as _random
+        from oracle import de_oracle
+        rows = [keys[i] for i in range(pop)]
+        _random.seed(args.seed)
+        t1 = time.perf_counter()
+        de_oracle.de_generation(rows, [0.0] * pop, 1, "de_rand_1", P, 0.8, 0.5, False)
+        t2 = time.perf_counter()
+        [np.argsort(r)[-k:] for r in rows]
+        t3 = time.perf_counter()
+        host_ref = {"de_step_ms": round((t2 - t1) * 1e3, 2), "decode_ms": round((t3 - t2) * 1e3, 2), "cores": 1,
+                    "kind": "port", "sample": f"one generation of {pop} x {P} keys (evolver.py:140-157, "
+                                              "individual.py:154-156), numpy on one host core"}
     fit = d_fit.cpu().numpy()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -278,6 +294,7 @@ def main():
             "ms_per_step_with_events": round(elapsed_events / args.steps * 1e3, 4),
             "gpu_decode_ms": None if decode_ms is None else round(decode_ms, 4),
             "gpu_de_step_ms": None if de_ms is None else round(de_ms, 4),
+            "host_reference_ms": host_ref,
             "fitness_checksum": float(np.nansum(fit)),
         }
         print(json.dumps(line), flush=True)

@@ -180,3 +180,31 @@ def test_gpu_generations_with_device_keystore(gpu, tmp_path):
     assert f_gpu == f_ref
     for a, b in zip(g_gpu, g_ref):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("L,pop,pre", [(1, 4, 0), (10, 4, 3), (100, 5, 624), (311, 4, 1), (312, 7, 0),
+                                       (313, 6, 622), (1000, 33, 100)])
+def test_gpu_de_small_shapes_vs_oracle(gpu, L, pop, pre):
+    """Tiny generations (< 625 stream words: the end state is rebuilt from the base window
+    without a jump), block-boundary lengths and every numpy position class."""
+    rng = np.random.default_rng(L * 7 + pop)
+    keys = rng.uniform(size=(pop, L))
+    fit = list(rng.uniform(size=pop))
+    for strat in ("de_rand_1", "de_currenttobest_1"):
+        inds = [KeyIndividual(keys[i].copy(), 1) for i in range(pop)]
+        for ind, f in zip(inds, fit):
+            ind.fitness = f
+        random.seed(L)
+        np.random.seed(pop)
+        np.random.bytes(4 * pre)
+        py, npst = random.getstate(), np.random.get_state()
+        kids = _evolver(strat, L, 0.6, 0.7, strat == "de_rand_1").evolve(Pop(inds, 2))
+        py_after, np_after = random.getstate(), np.random.get_state()
+        random.setstate(py)
+        np.random.set_state(npst)
+        want = D.de_generation([keys[i] for i in range(pop)], fit, 2, strat, L, 0.6, 0.7, strat == "de_rand_1")
+        assert random.getstate() == py_after
+        st = np.random.get_state()
+        assert np.array_equal(st[1], np_after[1]) and st[2] == np_after[2], (strat, L, pop, pre)
+        for k, w in zip(kids, want):
+            assert np.array_equal(k.get_internal_genome(), w), (strat, L, pop, pre)
