@@ -6,11 +6,12 @@
 // gives the same set whenever no tie straddles the threshold (continuous keys).
 //
 // One 1024-thread workgroup per individual:
-//   1. MSB-first radix select on the order-preserving uint64 image of the keys, 8 bits
-//      per pass, LDS histogram; stops as soon as the boundary bucket is taken whole
-//      (random keys: 2-3 passes over the 400 KB row at d = 50k)
-//   2. compaction of the selected (key, index) pairs into LDS (ties: backward chunked
-//      scan so the largest indices win)
+//   1. fast path: a strided sample (<= 4096 keys) in LDS gives a threshold with ~1.25 k
+//      keys above it; one pass over the row collects them in LDS; an exact radix select
+//      among those candidates picks the k largest (one read of the 400 KB row at d = 50k)
+//   2. fallback (candidates < k or > 8192, or a full-key tie at the k-th key): MSB-first
+//      radix select on the order-preserving uint64 image of the row, 8 bits per pass,
+//      LDS histogram, then compaction (ties: backward chunked scan, largest indices win)
 //   3. bitonic sort of the k pairs by (key, index), written out as int64 indices at the
 //      individual's offset (k may differ per individual: CoevolutionIndividual lengths)
 #include "tblup_internal.h"
@@ -25,6 +26,69 @@ constexpr int KSORT_MAX = 8192;   // LDS sort capacity (k <= 8192)
 __device__ __forceinline__ uint64_t ord_key(double x) {
   const uint64_t b = (uint64_t)__double_as_longlong(x);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// MSB-first radix select, 8 bits per pass, of the `want`-th largest of get(0..n): on return
+// the selected set is {u >> shift > prefix} plus, when `exact`, the whole bucket
+// {u >> shift == prefix}; otherwise `need` elements of that bucket remain to be chosen.
+template <typename Get>
+__device__ __forceinline__ void radix_select(Get get, int64_t n, int64_t want, int max_pass, uint32_t* hist,
+                                             int64_t* sel_sh, uint64_t& prefix, int& shift, int64_t& need,
+                                             bool& exact) {
+  const int t = threadIdx.x;
+  prefix = 0;
+  shift = 64;
+  need = want;
+  exact = false;
+  for (int pass = 0; pass < max_pass; ++pass) {
+    const int sh = 56 - 8 * pass;
+    for (int i = t; i < 256; i += DTH) hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = t; i < n; i += DTH) {
+      const uint64_t u = get(i);
+      if (pass == 0 || (u >> shift) == prefix) atomicAdd(&hist[(u >> sh) & 255], 1u);
+    }
+    __syncthreads();
+    if (t < 64) {
+      // boundary bin = the first bin from the top whose inclusive count from the top reaches
+      // `need`: lane l holds bins 4l..4l+3, a suffix scan over lanes finds the crossing lane
+      uint32_t h[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[j] = hist[4 * t + j];
+      const uint32_t sl = h[0] + h[1] + h[2] + h[3];
+      uint32_t suf = sl;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_down(suf, o);
+        if (t + o < 64) suf += v;
+      }
+      const int64_t excl = (int64_t)(suf - sl);
+      if (excl < need && need <= (int64_t)suf) {
+        int64_t above = excl;
+        int jsel = 0;
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          if (above + (int64_t)h[j] >= need) {
+            jsel = j;
+            break;
+          }
+          above += h[j];
+        }
+        const int64_t nneed = need - above;
+        const uint32_t hsel = jsel == 3 ? h[3] : jsel == 2 ? h[2] : jsel == 1 ? h[1] : h[0];
+        sel_sh[0] = (int64_t)((prefix << 8) | (uint64_t)(4 * t + jsel));
+        sel_sh[2] = nneed;
+        sel_sh[3] = ((int64_t)hsel == nneed) ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    prefix = (uint64_t)sel_sh[0];
+    need = sel_sh[2];
+    exact = sel_sh[3] != 0;
+    shift = sh;
+    __syncthreads();
+    if (exact) break;
+  }
 }
 
 }  // namespace
@@ -42,46 +106,80 @@ __global__ __launch_bounds__(DTH) void k_decode_topk(const double* __restrict__ 
   const double* row = keys + b * ld;
   const int64_t k = off[b + 1] - off[b];   // int(length) of this individual (host-checked 1..min(d, 8192))
 
-  // ---- 1. radix select ----
-  uint64_t prefix = 0;
-  int shift = 64;            // bits below the resolved prefix
-  int64_t need = k;          // how many of the elements matching `prefix` are still to take
-  bool exact = false;
-  for (int pass = 0; pass < 8; ++pass) {
-    const int sh = 56 - 8 * pass;
-    for (int i = t; i < 256; i += DTH) hist[i] = 0;
+  // ---- 1. fast path: threshold from a strided sample, ONE pass over the row ----
+  //   a. the keys at i = s*j (<= 4096 of them) into LDS; tau = lower edge of the 24-bit
+  //      bucket holding the sample's r-th largest, r ~ 1.25 k / s (so about 1.25 k keys of
+  //      the row are >= tau); b. one pass appends every (key, index) >= tau to LDS;
+  //   c. exact radix select of the k-th largest among those candidates in LDS.
+  // Falls back to the radix select over the row (section 2) when the candidates do not
+  // cover k, overflow the 8192 slots, or the k-th key is tied at full 64 bits.
+  __shared__ int fast_sh;
+  {
+    const int64_t s = (d + 4095) / 4096;
+    const int64_t ns = (d + s - 1) / s;
+    for (int64_t j = t; j < ns; j += DTH) sk[j] = ord_key(row[j * s]);
+    __syncthreads();
+    int64_t r = (5 * k) / (4 * s) + 8;
+    r = r < ns ? r : ns;
+    uint64_t pre;
+    int shf;
+    int64_t nd;
+    bool ex;
+    radix_select([&](int64_t i) { return sk[i]; }, ns, r, 3, hist, sel_sh, pre, shf, nd, ex);
+    if (t == 0) cnt_sh = 0;
     __syncthreads();
     for (int64_t i = t; i < d; i += DTH) {
       const uint64_t u = ord_key(row[i]);
-      if (pass == 0 || (u >> shift) == prefix) atomicAdd(&hist[(u >> sh) & 255], 1u);
-    }
-    __syncthreads();
-    if (t == 0) {
-      int64_t above = 0;
-      int bsel = 0;
-      for (int bin = 255; bin >= 0; --bin) {
-        if (above + (int64_t)hist[bin] >= need) {
-          bsel = bin;
-          break;
+      if ((u >> shf) >= pre) {
+        const uint32_t pos = atomicAdd(&cnt_sh, 1u);
+        if (pos < KSORT_MAX) {
+          sk[pos] = u;
+          si[pos] = (int32_t)i;
         }
-        above += hist[bin];
       }
-      const int64_t nneed = need - above;
-      sel_sh[0] = (int64_t)((prefix << 8) | (uint64_t)bsel);
-      sel_sh[2] = nneed;
-      sel_sh[3] = ((int64_t)hist[bsel] == nneed) ? 1 : 0;
     }
     __syncthreads();
-    prefix = (uint64_t)sel_sh[0];
-    need = sel_sh[2];
-    exact = sel_sh[3] != 0;
-    shift = sh;
+    const int64_t c = cnt_sh;
+    bool ok = c >= k && c <= KSORT_MAX;
+    if (ok) {
+      radix_select([&](int64_t i) { return sk[i]; }, c, k, 8, hist, sel_sh, pre, shf, nd, ex);
+      ok = ex;
+    }
+    if (ok) {
+      // keep exactly the k selected candidates: registers first, then compact from slot 0
+      uint64_t ku[KSORT_MAX / DTH];
+      int32_t ki[KSORT_MAX / DTH];
+#pragma unroll
+      for (int q = 0; q < KSORT_MAX / DTH; ++q) {
+        const int64_t e = t + (int64_t)q * DTH;
+        ku[q] = e < c ? sk[e] : 0;
+        ki[q] = e < c ? si[e] : -1;
+      }
+      __syncthreads();
+      if (t == 0) cnt_sh = 0;
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < KSORT_MAX / DTH; ++q) {
+        if (ki[q] >= 0 && (ku[q] >> shf) >= pre) {
+          const uint32_t pos = atomicAdd(&cnt_sh, 1u);
+          sk[pos] = ku[q];
+          si[pos] = ki[q];
+        }
+      }
+    }
+    if (t == 0) fast_sh = ok ? 1 : 0;
     __syncthreads();
-    if (exact) break;
   }
+
+  if (!fast_sh) {
+  // ---- 2. fallback: radix select over the row, compaction, full-key ties by index ----
+  uint64_t prefix;
+  int shift;
+  int64_t need;
+  bool exact;
+  radix_select([&](int64_t i) { return ord_key(row[i]); }, d, k, 8, hist, sel_sh, prefix, shift, need, exact);
   // selected = {u >> shift > prefix}  u  (the `need` largest-index elements with u >> shift == prefix)
 
-  // ---- 2. compaction ----
   if (t == 0) cnt_sh = 0;
   __syncthreads();
   for (int64_t i = t; i < d; i += DTH) {
@@ -132,6 +230,8 @@ __global__ __launch_bounds__(DTH) void k_decode_topk(const double* __restrict__ 
     }
   }
   __syncthreads();
+
+  }
 
   // ---- 3. bitonic sort by (key, index) ascending over the next power of two ----
   int n2 = 1;
