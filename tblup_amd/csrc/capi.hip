@@ -85,7 +85,6 @@ struct tblup_ctx {
   double bytes[TBLUP_N_KCLASS] = {0};
   int64_t mem_in_use = 0;
 
-  int skew = 0;       // TBLUP_SKEW: skewed two-group column schedule (k_chol_mixed)
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
   int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
 };
@@ -302,64 +301,23 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   // high-priority stream beside the rest of column J -- measured slower on MI355X: the
   // chip is already full during the off-diagonal launches, and sharing CUs slows the
   // critical path more than it hides.)
-  // algorithmic fp64 work of diagonal tile J for n individuals: the L = J-1 SYRK term,
-  // potrf + trtri, forward-substitution GEMV (the int8 GRM tiles are counted under KC_GRM)
-  auto diag_work = [&](int J, double n, double& f, double& b) {
+  const double Bd = (double)B;
+  for (int J = 0; J < sd.NT; ++J) {
     const double jt = (double)J;
-    f += n * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
-    b += n * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
-  };
-  // off-diagonal column J for n individuals, per tile: GEMM update 2*128^3*J, triangular
-  // solve 128^3 (fused GRM tile int-ops excluded); plus the preparation of diagonal tile J+1:
-  // 128^3 per L < J (lower half stored)
-  auto off_work = [&](int J, double n, double& f, double& b) {
-    const double jt = (double)J, nI = (double)(sd.NT - J - 1);
-    if (nI <= 0) return;
-    f += n * nI * (2.0 * T3 * jt + T3) + n * T3 * jt;
-    b += n * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * n * TILE * TILE * jt * 8.0;
-  };
-  constexpr int64_t XCDS = 8;
-  if (c->skew && B >= 2 * XCDS) {
-    // Skewed column schedule: the batch in two groups A = [0, Ba) and B = [Ba, B) one
-    // half-column apart, so every launch pairs one group's latency-bound diagonal tiles
-    // with the other group's off-diagonal tiles (k_chol_mixed):
-    //   dA(0) | oA(0)+dB(0) | dA(1)+oB(0) | oA(1)+dB(1) | ... | oA(NT-1)+dB(NT-1)
-    // Mixed launches are timed under KC_OFFDIAG with both parts' work.
-    const int64_t Ba = ((B + 1) / 2 + XCDS - 1) / XCDS * XCDS, Bb = B - Ba;
-    double f = 0, b = 0;
-    diag_work(0, (double)Ba, f, b);
-    rc = timed(c, s, KC_DIAG, f, b, [&] { return launch_chol_mixed(cl, 0, 0, Ba, -1, 0, 0, s); });
+    // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
+    // forward-substitution GEMV (the int8 GRM tiles are counted under KC_GRM)
+    const double fd = Bd * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
+    const double bd = Bd * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
+    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, s); });
     if (rc) return rc;
-    for (int J = 0; J < sd.NT; ++J) {
-      f = b = 0;
-      diag_work(J, (double)Bb, f, b);
-      off_work(J, (double)Ba, f, b);
-      rc = timed(c, s, KC_OFFDIAG, f, b, [&] { return launch_chol_mixed(cl, J, Ba, Bb, J, 0, Ba, s); });
+    const int nI = sd.NT - J - 1;
+    if (nI > 0) {
+      // per tile: GEMM update 2*128^3*J, triangular solve 128^3 (fused GRM tile int-ops excluded);
+      // plus the preparation of diagonal tile J+1: 128^3 per L < J (lower half stored)
+      const double fo = Bd * nI * (2.0 * T3 * jt + T3) + Bd * T3 * jt;
+      const double bo = Bd * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * Bd * TILE * TILE * jt * 8.0;
+      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(cl, J, s); });
       if (rc) return rc;
-      if (J + 1 < sd.NT) {
-        f = b = 0;
-        diag_work(J + 1, (double)Ba, f, b);
-        off_work(J, (double)Bb, f, b);
-        rc = timed(c, s, KC_OFFDIAG, f, b, [&] { return launch_chol_mixed(cl, J + 1, 0, Ba, J, Ba, Bb, s); });
-        if (rc) return rc;
-      }
-    }
-  } else {
-    // Column loop.  (A look-ahead schedule -- tile (J+1, J) and diagonal tile J+1 on a
-    // high-priority stream beside the rest of column J -- measured slower on MI355X: the
-    // chip is already full during the off-diagonal launches, and sharing CUs slows the
-    // critical path more than it hides.)
-    for (int J = 0; J < sd.NT; ++J) {
-      double f = 0, b = 0;
-      diag_work(J, (double)B, f, b);
-      rc = timed(c, s, KC_DIAG, f, b, [&] { return launch_chol_diag(cl, J, s); });
-      if (rc) return rc;
-      if (J + 1 < sd.NT) {
-        f = b = 0;
-        off_work(J, (double)B, f, b);
-        rc = timed(c, s, KC_OFFDIAG, f, b, [&] { return launch_chol_offdiag(cl, J, s); });
-        if (rc) return rc;
-      }
     }
   }
   if (stop_stage == 2) return 0;
@@ -421,8 +379,6 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
   const char* dbg = getenv("TBLUP_DBG_SKIP");
   c->dbg_skip = dbg ? atoi(dbg) : 0;
-  const char* skew = getenv("TBLUP_SKEW");
-  c->skew = skew ? atoi(skew) : 0;
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   if (!panel) {

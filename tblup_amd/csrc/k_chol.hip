@@ -28,7 +28,6 @@
 // become the fp64 accumulators of the Cholesky GEMM without any data movement.
 #include "i8_tile.h"
 #include <algorithm>
-#include <cstdlib>
 
 namespace tblup {
 
@@ -247,50 +246,6 @@ __device__ __forceinline__ void factor16(double* D, double* X, int l) {
   }
 }
 
-// In-place variant: X = L^{-1} replaces the block in D (the diagonal L block is read by
-// nothing after the factorisation); when Lt is non-null (debug readback) L goes to the
-// diagonal Lt tile at block (p, p): Lt[(16p + c) * 128 + 16p + i] = L[16p + i][16p + c].
-__device__ __forceinline__ void factor16_ip(double* D, double* Lt, int p, int l) {
-  const int i = l & 15, g = l >> 4;
-  double v[NB], e[NB], pvq[4];   // pvq: pivots of this lane's four output columns 4g..4g+3
-#pragma unroll
-  for (int c = 0; c < NB; ++c) {
-    v[c] = (c <= i) ? D[bo(i, c)] : D[bo(c, i)];
-    e[c] = (c == i) ? 1.0 : 0.0;
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) pvq[q] = 1.0;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const double piv = rdlane(v[j], j);
-    pvq[j & 3] = ((j >> 2) == g) ? piv : pvq[j & 3];
-    double r[NB], ej[NB];
-#pragma unroll
-    for (int c = j + 1; c < NB; ++c) r[c] = rdlane(v[c], j);
-#pragma unroll
-    for (int c = 0; c < j; ++c) ej[c] = rdlane(e[c], j);
-    const double li = v[j] * recip(piv);
-#pragma unroll
-    for (int c = j + 1; c < NB; ++c) v[c] = __builtin_fma(-li, r[c], v[c]);
-    const bool below = i > j;
-#pragma unroll
-    for (int c = 0; c < j; ++c) e[c] = below ? __builtin_fma(-li, ej[c], e[c]) : e[c];
-    e[j] = below ? -li : e[j];
-  }
-  const double rs_own = 1.0 / sqrt(v[i]);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = 4 * g + q;
-    double vc = v[0], ec = e[0];
-#pragma unroll
-    for (int cc = 1; cc < NB; ++cc) {
-      vc = (c == cc) ? v[cc] : vc;
-      ec = (c == cc) ? e[cc] : ec;
-    }
-    D[bo(i, c)] = (i >= c) ? ec * rs_own : 0.0;
-    if (Lt != nullptr && i >= c) Lt[(NB * p + c) * TILE + NB * p + i] = vc * (1.0 / sqrt(pvq[q]));
-  }
-}
 
 }  // namespace
 
@@ -764,194 +719,6 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   }
 }
 
-// X block (q, jb) of X = L^{-1} into registers (xinv_block without the store): the in-place
-// tile overwrites L row q with X row q only after every wave has read L row q.
-__device__ __forceinline__ v4d xinv_compute(const double* Tp, int q, int jb, int l) {
-  v4d sacc = {0.0, 0.0, 0.0, 0.0};
-  for (int lb = jb; lb < q; ++lb) {
-    const double* A = Tp + pk(q, lb);
-    const double* B = Tp + pk(lb, jb);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * kk + (l >> 4);
-      sacc = mfma64(A[bo(l & 15, k)], B[bo(k, l & 15)], sacc);
-    }
-  }
-  v4d xo = {0.0, 0.0, 0.0, 0.0};
-  const double* Xqq = Tp + pk(q, q);
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) xo = mfma64_nega(Xqq[bo(l & 15, 4 * kk + (l >> 4))], sacc[kk], xo);
-  return xo;
-}
-
-__device__ __forceinline__ void store_block(double* Tp, int q, int s, v4d x, int l) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) Tp[pk(q, s) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
-}
-
-// Diagonal tile J in 72 KiB of LDS (+ rsh), so that two such workgroups -- or one beside an
-// off-diagonal workgroup -- fit a CU: T -> L -> X = L^{-1} in the same packed blocks.
-//   A. the SYRK of the L = L0..J-1 terms runs first, its stage ring in the T space; then S
-//      lands there by LDS-DMA and T = S - SYRK.
-//   C. the blocked factorisation with wave 0's one-block look-ahead, as diag_tile; factor16
-//      writes X_pp over the diagonal block (L_pp is read by nothing afterwards), and block
-//      row p of X is computed in window p into registers and written over L row p (dead
-//      by then) after the window's barrier.
-//   E. as diag_tile, X read from the same blocks; the debug L_JJ^T readback is written block
-//      by block as L finalises.
-__device__ __forceinline__ void diag_tile_ip(const CholArgs& a, int64_t b, int J, int L0, double* lds,
-                                             double (*rsh)[TILE]) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int64_t ns = a.ns;
-  const int NT = a.NT;
-  const int64_t j0 = (int64_t)J * TILE;
-  const double* sc = a.scal + b * SCAL;
-  const double muf = sc[SC_MUF];
-  const int64_t nrow = (int64_t)sc[SC_NROW];
-  const int nt = a.nt;
-  double* Tp = lds;
-  double* Ld = (a.skip & FLAG_WRITE_LJJ) ? a.L + ((b * NT + J) * (int64_t)NT + J) * TT : nullptr;
-
-  // A.
-  {
-    v4d acc[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-    const bool syrk = J > L0 && !(a.skip & 2);
-    if (syrk) syrk_lower8<4>(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Tp, acc);
-    const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
-                                  : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
-#pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
-      const int chunk = (e * DW + w) * 64;
-      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
-    }
-    if (t < TILE) {
-      const int64_t gi = j0 + t;
-#pragma unroll
-      for (int tr = 0; tr < MAXT; ++tr) {
-        if (tr < nt) {
-          const int64_t o = (b * nt + tr) * ns + gi;
-          const double wv = (J > 0) ? a.w[o] : 0.0;
-          const double rv = (a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ymu[tr];
-          rsh[tr][t] = (gi < nrow) ? (rv - wv) : 0.0;
-        } else {
-          rsh[tr][t] = 0.0;
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (syrk) {
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const int e = w + DW * i;
-        if (e < NPACK) {
-          const int q = tri_q_rt(e);
-          double* blk = Tp + pk(q, e - q * (q + 1) / 2);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) blk[bo((l >> 4) + 4 * r, l & 15)] -= acc[i][r];
-        }
-      }
-      __syncthreads();
-    }
-  }
-
-  // C.
-  if (!(a.skip & 4)) {
-    if (w == 0 && !(a.skip & 256)) factor16_ip(Tp + pk(0, 0), Ld, 0, l);
-    __syncthreads();
-  }
-  for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
-    for (int q = p + 1 + w; q < ((a.skip & 512) ? 0 : NBLK); q += DW) {
-      v4d x = {0.0, 0.0, 0.0, 0.0};
-      x = mma_abt(Tp + pk(q, p), Tp + pk(p, p), x, l);
-      store_block(Tp, q, p, x, l);
-      if (Ld != nullptr) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Ld[(NB * p + (l & 15)) * TILE + NB * q + (l >> 4) + 4 * r] = x[r];
-      }
-    }
-    __syncthreads();
-    if (p + 1 == NBLK) break;
-    const int nb = NBLK - 1 - p;
-    v4d xo = {0.0, 0.0, 0.0, 0.0};
-    int xjb = -1;
-    if (w == 0) {
-      if (!(a.skip & 512)) {
-        v4d x = {0.0, 0.0, 0.0, 0.0};
-        x = mma_abt(Tp + pk(p + 1, p), Tp + pk(p + 1, p), x, l);
-        double* dst = Tp + pk(p + 1, p + 1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
-      }
-      if (!(a.skip & 256)) factor16_ip(Tp + pk(p + 1, p + 1), Ld, p + 1, l);
-    } else if (w != DW / 2) {
-      const int wi = (w < DW / 2) ? w - 1 : w - 2;   // 0 .. DW-3
-      for (int e = wi + 1; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += DW - 2) {
-        int qq = 0;
-        while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
-        const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
-        v4d x = {0.0, 0.0, 0.0, 0.0};
-        x = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), x, l);
-        double* dst = Tp + pk(q, sb);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
-      }
-      if (!(a.skip & 8) && wi < p) {
-        xo = xinv_compute(Tp, p, wi, l);
-        xjb = wi;
-      }
-    }
-    __syncthreads();
-    if (xjb >= 0) store_block(Tp, p, xjb, xo, l);   // X row p over L row p (read by nobody now)
-    __syncthreads();
-  }
-  if (a.skip & 16) return;
-
-  // D. last block row of X
-  if (!(a.skip & 4) && !(a.skip & 8)) {
-    v4d xo = {0.0, 0.0, 0.0, 0.0};
-    if (w < NBLK - 1) xo = xinv_compute(Tp, NBLK - 1, w, l);
-    __syncthreads();
-    if (w < NBLK - 1) store_block(Tp, NBLK - 1, w, xo, l);
-    __syncthreads();
-  }
-
-  // E.
-  {
-    double* Xg = a.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
-    for (int e = t; e < NPACK * BLKD; e += DTHR) {
-      const int blk = e >> 8, o = e & 255, i = o >> 4;
-      const int cpos = o & 15, c = 2 * ((cpos >> 1) ^ ((i >> 1) & 7)) + (cpos & 1);
-      Xg[blk * BLKD + bo(c, i)] = Tp[e];
-    }
-  }
-  {
-    const int i = t >> 2, q = t & 3;
-    double acc_z[MAXT] = {0.0, 0.0, 0.0, 0.0};
-    const int qi = i >> 4, ii = i & 15;
-    for (int c = q; c <= i; c += 4) {
-      const double xc = Tp[pk(qi, c >> 4) + bo(ii, c & 15)];
-#pragma unroll
-      for (int tr = 0; tr < MAXT; ++tr) acc_z[tr] += xc * rsh[tr][c];
-    }
-#pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr) {
-      double v = acc_z[tr];
-      v += __shfl_xor(v, 1);
-      v += __shfl_xor(v, 2);
-      if (q == 0 && tr < nt) a.z[(b * nt + tr) * ns + j0 + i] = v;
-    }
-  }
-}
-
-__global__ __launch_bounds__(DTHR, 4) void k_chol_diag_ip(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: ring, then T -> L -> X
-  __shared__ double rsh[MAXT][TILE];
-  diag_tile_ip(a, xcd_remap(blockIdx.x, gridDim.x), a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
-}
-
 // Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
 // K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
 __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
@@ -1092,32 +859,6 @@ __global__ __launch_bounds__(OTH, 2) void k_chol_offdiag(CholArgs a, int I0, int
   offdiag_tile(a, logical / nI, I0 + (int)(logical % nI), lds, uj_sh, ui_sh, zj_sh);
 }
 
-// One launch of the skewed column schedule (launch_chol_mixed): the in-place diagonal tiles
-// of one individual group at column Jd (first in the grid, so they start at once) beside the
-// diagonal preparations and off-diagonal tiles of the other group at column Jo.  Both
-// workgroup kinds take <= 78 KiB of LDS and <= 128 VGPRs: two share a CU, so the diagonal
-// chain's latency-bound workgroups run beside the throughput-bound tiles.
-__global__ __launch_bounds__(OTH, 4) void k_chol_mixed(CholArgs ad, int bd0, int nd, CholArgs ao, int bo0, int I0,
-                                                       int nI, int64_t n_tiles, int n_extra) {
-  __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];
-  __shared__ double sh_small[(MAXT + 2) * TILE];   // diagonal: rsh[MAXT][TILE]; tiles: uj, ui, zj[MAXT]
-  int64_t g = blockIdx.x;
-  if (g < nd) {
-    diag_tile_ip(ad, bd0 + xcd_remap(g, nd), ad.J, ad.J >= 2 ? ad.J - 1 : 0, lds,
-                 reinterpret_cast<double (*)[TILE]>(sh_small));
-    return;
-  }
-  g -= nd;
-  if (g < n_extra) {
-    syrk_partial8(ao, bo0 + xcd_remap(g, n_extra), ao.J + 1, ao.J, lds);
-    return;
-  }
-  g -= n_extra;
-  const int64_t logical = xcd_remap(g, n_tiles);
-  offdiag_tile(ao, bo0 + logical / nI, I0 + (int)(logical % nI), lds, sh_small, sh_small + TILE,
-               reinterpret_cast<double (*)[TILE]>(sh_small + 2 * TILE));
-}
-
 // K_JJ for every (individual, J) with the off-diagonal kernel's 8-wave int8 tile (A = B =
 // the rows of tile J, output in the f64 accumulator layout: a wave holds the 16 columns of
 // one column block, MFMAs only for the lower row blocks), exact counts + fp64 centring,
@@ -1205,31 +946,7 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
-  static const bool ip = getenv("TBLUP_DIAG_IP") && atoi(getenv("TBLUP_DIAG_IP")) != 0;
-  if (ip) {
-    hipLaunchKernelGGL(k_chol_diag_ip, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_chol_mixed(const CholLaunch& c, int Jd, int64_t bd0, int64_t nd, int Jo, int64_t bo0, int64_t nbo,
-                             hipStream_t s) {
-  CholArgs ad{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-              c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, Jd, c.skip};
-  CholArgs ao = ad;
-  ao.J = Jo;
-  if (Jd < 0) nd = 0;
-  const int I0 = Jo + 1;
-  const int nI = (Jo >= 0 && nbo > 0 && I0 < c.sd.NT) ? c.sd.NT - I0 : 0;
-  const int nsx = (nI > 0 && Jo >= 1) ? 1 : 0;   // preparation of diagonal tile Jo+1 (Jo+1 < NT)
-  ao.NSX = nsx;
-  const int64_t n_tiles = nbo * nI, n_extra = nbo * nsx;
-  const int64_t grid = nd + n_extra + n_tiles;
-  if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chol_mixed, dim3((unsigned)grid), dim3(OTH), 0, s, ad, (int)bd0, (int)nd, ao, (int)bo0, I0, nI,
-                     n_tiles, (int)n_extra);
   return hipGetLastError();
 }
 

@@ -140,10 +140,6 @@ struct CholLaunch {
 // then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s);
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s);
-// Skewed schedule: diagonal tiles of individuals [bd0, bd0+nd) at column Jd (Jd < 0: none)
-// beside the off-diagonal tiles (+ preparation of Jo+1) of [bo0, bo0+nbo) at column Jo.
-hipError_t launch_chol_mixed(const CholLaunch& c, int Jd, int64_t bd0, int64_t nd, int Jo, int64_t bo0, int64_t nbo,
-                             hipStream_t s);
 // all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s);
