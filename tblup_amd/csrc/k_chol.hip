@@ -417,6 +417,81 @@ __device__ __forceinline__ void i8_tt8_pk64(const uint8_t* sa, const uint8_t* sb
   __syncthreads();
 }
 
+// Off-diagonal SNP-form tile with a 2-D wave split: the stages are loaded exactly as in
+// i8_tt8_pk64, but wave w = (wr, wc) = (w >> 2, w & 3) computes row blocks 4wr..4wr+3 x
+// column blocks 2wc, 2wc+1, so each k-step unpacks 4 A + 2 B dwords for 8 MFMAs (instead of
+// 8 + 1).  The counts then go through LDS (64 blocks x 1 KiB, lane-linear 16-B slots) so
+// that wave w ends up with column block w for all 8 row blocks -- the layout GEMM1/GEMM2 use
+// (the MFMA lane mapping inside a block is the same in both layouts).
+template <int D>
+__device__ __forceinline__ void i8_tt2d_pk64(const uint8_t* sa, const uint8_t* sb, int64_t nblk, uint8_t* lds,
+                                             v4i (&cnt)[8]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  v4i c2[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) c2[m][ib] = v4i{0, 0, 0, 0};
+  if (nblk > 0) {
+    const int64_t nst = (nblk + 3) >> 2;
+    constexpr int TB = TILE * 64;
+    auto issue = [&](int64_t st) {
+      uint8_t* slot = lds + (int)(st % D) * 2 * TB;
+      __builtin_amdgcn_global_load_lds(sa + st * 64, (lds_ptr_t)(slot + w * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(sb + st * 64, (lds_ptr_t)(slot + TB + w * 1024), 16, 0, 0);
+    };
+    for (int64_t st = 0; st < D - 1 && st < nst; ++st) issue(st);
+    const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+    const int tail_ch = (int)(nblk & 3);
+    for (int64_t st = 0; st < nst; ++st) {
+      if (st + D - 2 < nst) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      if (st + D - 1 < nst) issue(st + D - 1);
+      const uint8_t* As = lds + (int)(st % D) * 2 * TB;
+      const uint8_t* Bs = As + TB;
+      const bool ztail = (st == nst - 1 && tail_ch != 0 && ch >= tail_ch);
+      uint4 bq[2], aq[4];
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        bq[ib] = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * (2 * wc + ib) + rho, ch));
+        if (ztail) bq[ib] = uint4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) aq[m] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * (4 * wr + m) + prow, ch));
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        v4i bv[2];
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib)
+          bv[ib] = unpack16(s4 == 0 ? bq[ib].x : s4 == 1 ? bq[ib].y : s4 == 2 ? bq[ib].z : bq[ib].w);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const v4i av = unpack16(s4 == 0 ? aq[m].x : s4 == 1 ? aq[m].y : s4 == 2 ? aq[m].z : aq[m].w);
+#pragma unroll
+          for (int ib = 0; ib < 2; ++ib) c2[m][ib] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[ib], c2[m][ib], 0, 0, 0);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // exchange: block (row cb, column ib) at slot ib * 8 + cb, lane l's 16 B at l
+  v4i* xs = reinterpret_cast<v4i*>(lds);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) xs[((2 * wc + ib) * 8 + 4 * wr + m) * 64 + l] = c2[m][ib];
+  __syncthreads();
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) cnt[cb] = xs[(w * 8 + cb) * 64 + l];
+  __syncthreads();
+}
+
 // Lt stage (16 k rows x 1 KiB) loaded by 8 waves: rows 2w, 2w+1.
 __device__ __forceinline__ void glds_lt_stage8w(const double* __restrict__ src, double* stage) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -763,9 +838,9 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
     const int64_t nblk = (int64_t)sc[SC_CBLK];
     if (!(a.skip & 32) && a.form == FORM_PRIMAL) {
       const int row = 16 * w + (l >> 2), pos = l & 3;
-      i8_tt8_pk64<4>(row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
-                     row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk,
-                     reinterpret_cast<uint8_t*>(lds), cnt);
+      i8_tt2d_pk64<4>(row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
+                      row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk,
+                      reinterpret_cast<uint8_t*>(lds), cnt);
     } else if (!(a.skip & 32)) {
       const int row = 16 * w + (l >> 2), pos = l & 3;
       i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
