@@ -639,6 +639,30 @@ __device__ __forceinline__ void xinv_block(const double* Tp, double* Xp, int q, 
   for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] = xo[r];
 }
 
+// z_J[i] = sum_{c <= i} X[i][c] r[c] for the NTR right-hand sides: four lanes per row
+// (c = q mod 4), shuffle-reduced.
+template <int NTR>
+__device__ __forceinline__ void diag_z(const CholArgs& a, const double* Xp, const double (*rsh)[TILE], int64_t b,
+                                       int64_t j0) {
+  const int t = threadIdx.x, i = t >> 2, q = t & 3;
+  const int qi = i >> 4, ii = i & 15;
+  double acc[NTR];
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) acc[tr] = 0.0;
+  for (int c = q; c <= i; c += 4) {
+    const double xc = Xp[pk(qi, c >> 4) + bo(ii, c & 15)];
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr) acc[tr] += xc * rsh[tr][c];
+  }
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) {
+    double v = acc[tr];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    if (q == 0) a.z[(b * NTR + tr) * a.ns + j0 + i] = v;
+  }
+}
+
 // Diagonal tile J of individual b.  T = S - sum_{L0 <= L < J} L_JL L_JL^T where S is
 // K_JJ - sum_{L < L0} (the buffer slot J&1 left by an earlier off-diagonal launch) when
 // L0 > 0, else k_diag_grm's K_JJ.
@@ -658,6 +682,21 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   const int nt = a.nt;
   double* Tp = lds;
   double* Xp = lds + NPACK * BLKD;
+
+  // forward-substitution right-hand side r = rhs_J - w_J: loads issued first so that their
+  // latency overlaps the S load and the SYRK
+  double rv[MAXT] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t gi = j0 + t;
+  if (t < TILE) {
+#pragma unroll
+    for (int tr = 0; tr < MAXT; ++tr) {
+      if (tr < nt) {
+        const int64_t o = (b * nt + tr) * ns + gi;
+        const double wv = (J > 0) ? a.w[o] : 0.0;
+        rv[tr] = ((a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ymu[tr]) - wv;
+      }
+    }
+  }
 
   // T = S - sum_{L0 <= L < J} L_JL L_JL^T: S by LDS-DMA, the SYRK through the stage ring
   {
@@ -688,18 +727,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (t < TILE) {
-    const int64_t gi = j0 + t;
 #pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr) {
-      if (tr < nt) {
-        const int64_t o = (b * nt + tr) * ns + gi;
-        const double wv = (J > 0) ? a.w[o] : 0.0;
-        const double rv = (a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ymu[tr];
-        rsh[tr][t] = (gi < nrow) ? (rv - wv) : 0.0;
-      } else {
-        rsh[tr][t] = 0.0;
-      }
-    }
+    for (int tr = 0; tr < MAXT; ++tr) rsh[tr][t] = (tr < nt && gi < nrow) ? rv[tr] : 0.0;
   }
   __syncthreads();
 
@@ -760,11 +789,14 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   // E. X into Dinv as packed lower blocks, each block transposed (block (q, jb) holds
   //    X_{q,jb}^T in the bo() layout), z_J = X r, and L_JJ^T only for the debug readback.
   {
+    // coalesced: thread writes the 16-B pair at g = 2k of Dinv, i.e. elements (r, c0), (r, c0+1)
+    // of block blk's transpose, read from X at bo(c0, r), bo(c0 + 1, r)
     double* Xg = a.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
-    for (int e = t; e < NPACK * BLKD; e += DTHR) {   // linear (conflict-free) LDS reads
-      const int blk = e >> 8, o = e & 255, i = o >> 4;
-      const int cpos = o & 15, c = 2 * ((cpos >> 1) ^ ((i >> 1) & 7)) + (cpos & 1);   // o = bo(i, c)
-      Xg[blk * BLKD + bo(c, i)] = Xp[e];
+    for (int k = t; k < ((a.skip & (1 << 14)) ? 0 : NPACK * BLKD / 2); k += DTHR) {
+      const int g = 2 * k, blk = g >> 8, o = g & 255, r = o >> 4;
+      const int c0 = 2 * (((o & 15) >> 1) ^ ((r >> 1) & 7));
+      const double* xb = Xp + blk * BLKD;
+      *reinterpret_cast<v2d*>(Xg + g) = v2d{xb[bo(c0, r)], xb[bo(c0 + 1, r)]};
     }
   }
   if (a.skip & FLAG_WRITE_LJJ) {
@@ -775,21 +807,12 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     }
   }
   // z_J[i] = sum_{c <= i} X[i][c] r[c]: four lanes per row (c = q mod 4), shuffle-reduced
-  {
-    const int i = t >> 2, q = t & 3;
-    double acc_z[MAXT] = {0.0, 0.0, 0.0, 0.0};
-    const int qi = i >> 4, ii = i & 15;
-    for (int c = q; c <= i; c += 4) {
-      const double xc = Xp[pk(qi, c >> 4) + bo(ii, c & 15)];
-#pragma unroll
-      for (int tr = 0; tr < MAXT; ++tr) acc_z[tr] += xc * rsh[tr][c];
-    }
-#pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr) {
-      double v = acc_z[tr];
-      v += __shfl_xor(v, 1);
-      v += __shfl_xor(v, 2);
-      if (q == 0 && tr < nt) a.z[(b * nt + tr) * ns + j0 + i] = v;
+  if (!(a.skip & (1 << 15))) {
+    switch (nt) {
+      case 1: diag_z<1>(a, Xp, rsh, b, j0); break;
+      case 2: diag_z<2>(a, Xp, rsh, b, j0); break;
+      case 3: diag_z<3>(a, Xp, rsh, b, j0); break;
+      default: diag_z<4>(a, Xp, rsh, b, j0); break;
     }
   }
 }
