@@ -539,6 +539,51 @@ __device__ __forceinline__ void gemm1_tt8(const double* __restrict__ ltJ, const 
   __syncthreads();
 }
 
+// GEMM1 with 32-row stages: only A (the Lt_J stage every wave reads) goes through the LDS
+// ring (2 x 32 KiB); each wave's B operand (its own 16 columns of Lt_I) is loaded straight
+// into registers one stage ahead.  Half the barriers of the 16-row A+B ring.
+__device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
+                                          double* lds, v4d (&acc)[8]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int AS = 32 * TILE;   // doubles per 32-row stage
+  const int nst = 4 * J;
+  if (nst == 0) return;
+  auto src_of = [&](int s) { return (int64_t)(s >> 2) * TT + (s & 3) * AS; };
+  auto issue_a = [&](int s) {
+    double* slot = lds + (s & 1) * AS;
+    const int64_t src = src_of(s);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * w + e;
+      __builtin_amdgcn_global_load_lds(ltJ + src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(slot + k * TILE), 16,
+                                       0, 0);
+    }
+  };
+  const double* bcol = ltI + 16 * w + (l & 15) + (l >> 4) * TILE;
+  double bc[8];
+  issue_a(0);
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) bc[kk] = bcol[4 * kk * TILE];
+  for (int s = 0; s < nst; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool more = s + 1 < nst;
+    if (more) issue_a(s + 1);
+    const double* bs = bcol + src_of(more ? s + 1 : s);
+    const double* As = lds + (s & 1) * AS;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = 4 * kk + (l >> 4);
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) acc[cb] = mfma64_nega(As[lt_off(k, 16 * cb + (l & 15))], bc[kk], acc[cb]);
+      // B of the next stage into the register this k-step has consumed
+      if (more) bc[kk] = bs[4 * kk * TILE];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // SYRK of Lt stages restricted to the 36 lower blocks, 8 waves: wave W takes blocks
 // W + 8i (5 blocks for W < 4, 4 for W >= 4).
 template <int W>
@@ -887,7 +932,7 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   }
 
   // 1. T^T = K_JI - sum_L L_JL L_IL^T
-  if (J > 0 && !(a.skip & 64)) gemm1_tt8<2>(Lb + (int64_t)J * NT * TT, Lb + (int64_t)I * NT * TT, J, lds, acc);
+  if (J > 0 && !(a.skip & 64)) gemm1_a32(Lb + (int64_t)J * NT * TT, Lb + (int64_t)I * NT * TT, J, lds, acc);
 
   // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X in the
   //    packed block layout (blocks transposed): all 36 blocks (72 KiB) land in LDS in one
@@ -945,7 +990,7 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
 // overlap the tiles) one workgroup per individual preparing diagonal tile J+1 except its
 // L = J term: S[(J+1)&1] = K - sum_{L<J} (those tiles are final already).
 // LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
-__global__ __launch_bounds__(OTH, 2) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
+__global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
   __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
   __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
   const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
