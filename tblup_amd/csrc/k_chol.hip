@@ -630,13 +630,49 @@ __device__ __forceinline__ void syrk_lower8(const double* __restrict__ src, int 
   __syncthreads();
 }
 
+// The same SYRK on 32-row stages (2 x 32 KiB ring): half the barriers per k row.
+__device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, int nst16, double* lds, v4d (&acc)[5]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (nst16 <= 0) return;
+  constexpr int AS = 32 * TILE;
+  const int nst = nst16 >> 1;   // 8 x (number of Lt tiles): always even
+  auto issue = [&](int s) {
+    double* slot = lds + (s & 1) * AS;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * w + e;
+      __builtin_amdgcn_global_load_lds(src + (int64_t)s * AS + k * TILE + 2 * (l ^ (8 * (k & 1))),
+                                       (lds_ptr_t)(slot + k * TILE), 16, 0, 0);
+    }
+  };
+  issue(0);
+  for (int s = 0; s < nst; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nst) issue(s + 1);
+    const double* As = lds + (s & 1) * AS;
+    switch (w) {
+      case 0: syrk_stage8<0>(As, acc, l); syrk_stage8<0>(As + LTS, acc, l); break;
+      case 1: syrk_stage8<1>(As, acc, l); syrk_stage8<1>(As + LTS, acc, l); break;
+      case 2: syrk_stage8<2>(As, acc, l); syrk_stage8<2>(As + LTS, acc, l); break;
+      case 3: syrk_stage8<3>(As, acc, l); syrk_stage8<3>(As + LTS, acc, l); break;
+      case 4: syrk_stage8<4>(As, acc, l); syrk_stage8<4>(As + LTS, acc, l); break;
+      case 5: syrk_stage8<5>(As, acc, l); syrk_stage8<5>(As + LTS, acc, l); break;
+      case 6: syrk_stage8<6>(As, acc, l); syrk_stage8<6>(As + LTS, acc, l); break;
+      default: syrk_stage8<7>(As, acc, l); syrk_stage8<7>(As + LTS, acc, l); break;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // S[b][Jt&1] = K_{Jt,Jt} - sum_{L < nterm} L_{Jt,L} L_{Jt,L}^T (packed blocks), 8 waves.
 __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int Jt, int nterm, double* lds) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   v4d acc[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-  if (!(a.skip & 2)) syrk_lower8<4>(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc);
+  if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc);
   const double* Kb = a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD;
   double* Pd = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
 #pragma unroll
@@ -757,7 +793,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
       // waits for all its stages (and the older S loads) and ends in a barrier
-      syrk_lower8<4>(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
+      syrk_lower8_32(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
         const int e = w + DW * i;
