@@ -293,8 +293,10 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
   const double cbar = (sd.form == FORM_PRIMAL) ? (double)d.nT : kbar;   // contraction length
   {
-    const double fg = (double)B * sd.NT * 128.0 * 129.0 * cbar;   // int ops of the diagonal GRM tiles
-    rc = timed(c, s, KC_GRM, fg, (double)B * sd.NT * 36 * 256 * 8.0, [&] { return launch_diag_grm(cl, s); });
+    // int ops of the diagonal GRM tiles J < 2 (J >= 2 run inside the column-0 off-diagonal launch)
+    const double nJ = (double)std::min(sd.NT, 2);
+    const double fg = (double)B * nJ * 128.0 * 129.0 * cbar;
+    rc = timed(c, s, KC_GRM, fg, (double)B * nJ * 36 * 256 * 8.0, [&] { return launch_diag_grm(cl, s); });
     if (rc) return rc;
   }
   // Column loop.  (A look-ahead schedule -- tile (J+1, J) and diagonal tile J+1 on a

@@ -1022,34 +1022,15 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   }
 }
 
-// Off-diagonal tiles (I, J) for I0 <= I < I0 + nI, plus (first in the grid, so they
-// overlap the tiles) one workgroup per individual preparing diagonal tile J+1 except its
-// L = J term: S[(J+1)&1] = K - sum_{L<J} (those tiles are final already).
-// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
-__global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles) {
-  __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
-  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
-  const int64_t n_extra = (int64_t)gridDim.x - n_tiles;
-  if ((int64_t)blockIdx.x < n_extra) {
-    syrk_partial8(a, xcd_remap(blockIdx.x, n_extra), a.J + 1, a.J, lds);
-    return;
-  }
-  const int64_t logical = xcd_remap(blockIdx.x - n_extra, n_tiles);
-  offdiag_tile(a, logical / nI, I0 + (int)(logical % nI), lds, uj_sh, ui_sh, zj_sh);
-}
-
 // K_JJ for every (individual, J) with the off-diagonal kernel's 8-wave int8 tile (A = B =
 // the rows of tile J, output in the f64 accumulator layout: a wave holds the 16 columns of
 // one column block, MFMAs only for the lower row blocks), exact counts + fp64 centring,
-// + lambda I, identity on padded rows; packed lower 16x16 blocks into Kd[b][J].
-__global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * TILE * 64];
-  __shared__ double u_sh[TILE];
+// + lambda I, identity on padded rows; packed lower 16x16 blocks into Kd[b][J].  J = 0, 1 run in
+// k_diag_grm8 before the column loop; J >= 2 are extra workgroups at the end of the column-0
+// off-diagonal launch (they fill its last round; the first reader is column 1's preparation).
+__device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int J, uint8_t* lds, double* u_sh) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int NT = a.NT;
-  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
-  const int64_t b = lg / NT;
-  const int J = (int)(lg % NT);
   const int64_t j0 = (int64_t)J * TILE;
   const double* sc = a.scal + b * SCAL;
   const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
@@ -1115,10 +1096,41 @@ __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a) {
   }
 }
 
+// Off-diagonal tiles (I, J) for I0 <= I < I0 + nI, plus (first in the grid, so they
+// overlap the tiles) one workgroup per individual preparing diagonal tile J+1 except its
+// L = J term: S[(J+1)&1] = K - sum_{L<J} (those tiles are final already).
+// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
+__global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles, int64_t n_kd) {
+  __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
+  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
+  const int64_t n_extra = (int64_t)gridDim.x - n_tiles - n_kd;
+  const int64_t bid = blockIdx.x;
+  if (bid < n_extra) {
+    syrk_partial8(a, xcd_remap(bid, n_extra), a.J + 1, a.J, lds);
+    return;
+  }
+  if (bid >= n_extra + n_tiles) {   // column 0 only: K_JJ for J >= 2
+    const int64_t lg = xcd_remap(bid - n_extra - n_tiles, n_kd);
+    const int nJ = a.NT - 2;
+    diag_grm_tile(a, lg / nJ, 2 + (int)(lg % nJ), reinterpret_cast<uint8_t*>(lds), uj_sh);
+    return;
+  }
+  const int64_t logical = xcd_remap(bid - n_extra, n_tiles);
+  offdiag_tile(a, logical / nI, I0 + (int)(logical % nI), lds, uj_sh, ui_sh, zj_sh);
+}
+
+__global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a, int nJ) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * TILE * 64];
+  __shared__ double u_sh[TILE];
+  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
+  diag_grm_tile(a, lg / nJ, (int)(lg % nJ), lds, u_sh);
+}
+
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip};
-  hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * c.sd.NT)), dim3(OTH), 0, s, a);
+  const int nJ = std::min(c.sd.NT, 2);
+  hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * nJ)), dim3(OTH), 0, s, a, nJ);
   return hipGetLastError();
 }
 
@@ -1136,7 +1148,9 @@ hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
   if (nI <= 0) return hipSuccess;
   a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;
   const int64_t n_tiles = c.B * nI;
-  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX)), dim3(OTH), 0, s, a, I0, nI, n_tiles);
+  const int64_t n_kd = (J == 0 && c.sd.NT > 2) ? c.B * (c.sd.NT - 2) : 0;
+  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX + n_kd)), dim3(OTH), 0, s, a, I0, nI,
+                     n_tiles, n_kd);
   return hipGetLastError();
 }
 
