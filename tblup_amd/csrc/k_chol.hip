@@ -426,6 +426,8 @@ __device__ __forceinline__ void i8_tt8_pk64(const uint8_t* sa, const uint8_t* sb
 template <int D>
 __device__ __forceinline__ void i8_tt2d_pk64(const uint8_t* sa, const uint8_t* sb, int64_t nblk, uint8_t* lds,
                                              v4i (&cnt)[8]) {
+  // D is unused: two 128-B super-stages (each = two of i8_tt8_pk64's 64-B stages, 32 KiB)
+  // alternate in the 64 KiB ring, one barrier per 512 animals
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w >> 2, wc = w & 3;
   v4i c2[4][2];
@@ -434,46 +436,57 @@ __device__ __forceinline__ void i8_tt2d_pk64(const uint8_t* sa, const uint8_t* s
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) c2[m][ib] = v4i{0, 0, 0, 0};
   if (nblk > 0) {
-    const int64_t nst = (nblk + 3) >> 2;
+    const int64_t nh = (nblk + 3) >> 2;   // 64-B half stages
+    const int64_t nst = (nh + 1) >> 1;
     constexpr int TB = TILE * 64;
     auto issue = [&](int64_t st) {
-      uint8_t* slot = lds + (int)(st % D) * 2 * TB;
-      __builtin_amdgcn_global_load_lds(sa + st * 64, (lds_ptr_t)(slot + w * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(sb + st * 64, (lds_ptr_t)(slot + TB + w * 1024), 16, 0, 0);
+      uint8_t* slot = lds + (int)(st & 1) * 4 * TB;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t hs = 2 * st + h;
+        if (hs < nh) {
+          __builtin_amdgcn_global_load_lds(sa + hs * 64, (lds_ptr_t)(slot + h * 2 * TB + w * 1024), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds(sb + hs * 64, (lds_ptr_t)(slot + h * 2 * TB + TB + w * 1024), 16, 0, 0);
+        }
+      }
     };
-    for (int64_t st = 0; st < D - 1 && st < nst; ++st) issue(st);
+    issue(0);
     const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
     const int tail_ch = (int)(nblk & 3);
     for (int64_t st = 0; st < nst; ++st) {
-      if (st + D - 2 < nst) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (st + D - 1 < nst) issue(st + D - 1);
-      const uint8_t* As = lds + (int)(st % D) * 2 * TB;
-      const uint8_t* Bs = As + TB;
-      const bool ztail = (st == nst - 1 && tail_ch != 0 && ch >= tail_ch);
-      uint4 bq[2], aq[4];
+      if (st + 1 < nst) issue(st + 1);
 #pragma unroll
-      for (int ib = 0; ib < 2; ++ib) {
-        bq[ib] = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * (2 * wc + ib) + rho, ch));
-        if (ztail) bq[ib] = uint4{0u, 0u, 0u, 0u};
-      }
+      for (int h = 0; h < 2; ++h) {
+        const int64_t hs = 2 * st + h;
+        if (hs < nh) {
+          const uint8_t* As = lds + (int)(st & 1) * 4 * TB + h * 2 * TB;
+          const uint8_t* Bs = As + TB;
+          const bool ztail = (hs == nh - 1 && tail_ch != 0 && ch >= tail_ch);
+          uint4 bq[2], aq[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) aq[m] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * (4 * wr + m) + prow, ch));
+          for (int ib = 0; ib < 2; ++ib) {
+            bq[ib] = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * (2 * wc + ib) + rho, ch));
+            if (ztail) bq[ib] = uint4{0u, 0u, 0u, 0u};
+          }
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        v4i bv[2];
+          for (int m = 0; m < 4; ++m)
+            aq[m] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * (4 * wr + m) + prow, ch));
 #pragma unroll
-        for (int ib = 0; ib < 2; ++ib)
-          bv[ib] = unpack16(s4 == 0 ? bq[ib].x : s4 == 1 ? bq[ib].y : s4 == 2 ? bq[ib].z : bq[ib].w);
+          for (int s4 = 0; s4 < 4; ++s4) {
+            v4i bv[2];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const v4i av = unpack16(s4 == 0 ? aq[m].x : s4 == 1 ? aq[m].y : s4 == 2 ? aq[m].z : aq[m].w);
+            for (int ib = 0; ib < 2; ++ib)
+              bv[ib] = unpack16(s4 == 0 ? bq[ib].x : s4 == 1 ? bq[ib].y : s4 == 2 ? bq[ib].z : bq[ib].w);
 #pragma unroll
-          for (int ib = 0; ib < 2; ++ib) c2[m][ib] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[ib], c2[m][ib], 0, 0, 0);
+            for (int m = 0; m < 4; ++m) {
+              const v4i av = unpack16(s4 == 0 ? aq[m].x : s4 == 1 ? aq[m].y : s4 == 2 ? aq[m].z : aq[m].w);
+#pragma unroll
+              for (int ib = 0; ib < 2; ++ib)
+                c2[m][ib] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv[ib], c2[m][ib], 0, 0, 0);
+            }
+          }
         }
       }
     }
