@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--profile-json", default=None, help="write the per-kernel-class event timing here")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events (no roofline)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-mfma-json", default=os.path.join(ROOT, "profiles", "pmc_mfma.json"),
+                    help="rocprofv3 MFMA-busy summary (tools/pmc_mfma.py) for the roofline's mfma_busy")
     return ap.parse_args()
 
 
@@ -267,8 +269,16 @@ def main():
                 traffic = pmc["per_launch_bytes"][dom]
         except (ValueError, OSError):
             traffic = None
+    mfma_busy = None   # PMC: fraction of SIMD cycles with an MFMA in flight (separate pass)
+    if os.path.isfile(args.pmc_mfma_json):
+        try:
+            pm = json.load(open(args.pmc_mfma_json))
+            if pm.get("config") == args.config and dom in pm.get("per_class", {}):
+                mfma_busy = pm["per_class"][dom]["mfma_busy"]
+        except (ValueError, OSError, KeyError):
+            mfma_busy = None
     roofline = {"bound": bound, "kernel": dom, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "mfma_busy": mfma_busy,
                 "launches": pd["launches"], "avg_launch_ms": round(pd["ms"] / max(pd["launches"], 1), 4)}
     step_ms = {c: round(prof[c]["ms"] / args.steps, 4) for c in prof}
 
