@@ -54,65 +54,12 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // covers all 64 banks.  One LDS-DMA instruction moves one 1 KiB k row.
 __device__ __forceinline__ int lt_off(int k, int x) { return k * TILE + 2 * ((x >> 1) ^ (8 * (k & 1))) + (x & 1); }
 
-__device__ __forceinline__ void glds_lt_stage(const double* __restrict__ src, double* stage) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int k = 4 * w + e;
-    __builtin_amdgcn_global_load_lds(src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(stage + k * TILE), 16, 0,
-                                     0);
-  }
-}
-
 // ---- int8 GRM tile in the f64 accumulator layout (offdiag) ----
 // cnt[cb][ib] = sum_s A[16cb + pi-row][s] B[32w + 16ib + col][s] with A = panel rows of tile J
 // (c) and B = panel rows of tile I (i).  Panel tiles [128 rows][64 B]; A chunk swizzle
 // (row>>2)&3 and B chunk swizzle (row>>2)&2 keep both ds_read_b128 patterns conflict-free.
 __device__ __forceinline__ int i8off_a(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 3)); }
 __device__ __forceinline__ int i8off_b(int row, int c) { return row * 64 + 16 * (c ^ ((row >> 2) & 2)); }
-
-// ---- GEMM1 of the off-diagonal kernel: acc[cb][ib] -= sum_{k < 128J} L_J[c][k] L_I[i][k] ----
-// A = Lt tiles (J, L), B = Lt tiles (I, L), L < J; LDS-DMA ring of D slots x 32 KiB.
-template <int D>
-__device__ __forceinline__ void gemm1_tt(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
-                                         double* lds, v4d (&acc)[8][2]) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int nst = 8 * J;
-  if (nst == 0) return;
-  auto issue = [&](int s) {
-    double* slot = lds + (s % D) * 2 * LTS;
-    const int64_t src = (int64_t)(s >> 3) * TT + (s & 7) * LTS;
-    glds_lt_stage(ltJ + src, slot);
-    glds_lt_stage(ltI + src, slot + LTS);
-  };
-  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
-  for (int s = 0; s < nst; ++s) {
-    if (s + D - 2 < nst) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 8) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (s + D - 1 < nst) issue(s + D - 1);
-    const double* As = lds + (s % D) * 2 * LTS;
-    const double* Bs = As + LTS;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * kk + (l >> 4);
-      double bv[2];
-#pragma unroll
-      for (int ib = 0; ib < 2; ++ib) bv[ib] = Bs[lt_off(k, 32 * w + 16 * ib + (l & 15))];
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) {
-        const double av = As[lt_off(k, 16 * cb + (l & 15))];
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) acc[cb][ib] = mfma64_nega(av, bv[ib], acc[cb][ib]);
-      }
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
 
 // ---- SYRK restricted to the 36 lower 16x16 blocks (diag kernel), A = Lt tiles (J, L) ----
 __host__ __device__ constexpr int tri_q(int e) {
@@ -127,45 +74,6 @@ __device__ __forceinline__ int tri_q_rt(int e) {
   if ((q + 1) * (q + 2) / 2 <= e) ++q;
   if (q * (q + 1) / 2 > e) --q;
   return q;
-}
-
-template <int W>
-__device__ __forceinline__ void syrk_stage(const double* As, v4d (&acc)[9], int l) {
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const int k = 4 * kk + (l >> 4);
-    double a8[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a8[q] = As[lt_off(k, 16 * q + (l & 15))];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) acc[i] = mfma64(a8[tri_q(W + 4 * i)], a8[tri_s(W + 4 * i)], acc[i]);
-  }
-}
-
-// nst consecutive 16-row stages starting at src (the Lt tiles (J, 0..) of one tile row are
-// contiguous, so stage s of the row lives at s * LTS).
-template <int D>
-__device__ __forceinline__ void syrk_lower(const double* __restrict__ src, int nst, double* lds, v4d (&acc)[9]) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (nst <= 0) return;
-  auto issue = [&](int s) { glds_lt_stage(src + (int64_t)s * LTS, lds + (s % D) * LTS); };
-  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
-  for (int s = 0; s < nst; ++s) {
-    if (s + D - 2 < nst) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (s + D - 1 < nst) issue(s + D - 1);
-    const double* As = lds + (s % D) * LTS;
-    if (w == 0) syrk_stage<0>(As, acc, l);
-    else if (w == 1) syrk_stage<1>(As, acc, l);
-    else if (w == 2) syrk_stage<2>(As, acc, l);
-    else syrk_stage<3>(As, acc, l);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
 }
 
 
@@ -505,56 +413,10 @@ __device__ __forceinline__ void i8_tt2d_pk64(const uint8_t* sa, const uint8_t* s
   __syncthreads();
 }
 
-// Lt stage (16 k rows x 1 KiB) loaded by 8 waves: rows 2w, 2w+1.
-__device__ __forceinline__ void glds_lt_stage8w(const double* __restrict__ src, double* stage) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int k = 2 * w + e;
-    __builtin_amdgcn_global_load_lds(src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(stage + k * TILE), 16, 0,
-                                     0);
-  }
-}
-
-// GEMM1: acc[cb] -= sum_{k < 128J} L_J[c][k] L_I[i][k] for the wave's 16 columns i.
-template <int D>
-__device__ __forceinline__ void gemm1_tt8(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
-                                          double* lds, v4d (&acc)[8]) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int nst = 8 * J;
-  if (nst == 0) return;
-  auto issue = [&](int s) {
-    double* slot = lds + (s % D) * 2 * LTS;
-    const int64_t src = (int64_t)(s >> 3) * TT + (s & 7) * LTS;
-    glds_lt_stage8w(ltJ + src, slot);
-    glds_lt_stage8w(ltI + src, slot + LTS);
-  };
-  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
-  for (int s = 0; s < nst; ++s) {
-    if (s + D - 2 < nst) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (s + D - 1 < nst) issue(s + D - 1);
-    const double* As = lds + (s % D) * 2 * LTS;
-    const double* Bs = As + LTS;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * kk + (l >> 4);
-      const double bv = Bs[lt_off(k, 16 * w + (l & 15))];
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) acc[cb] = mfma64_nega(As[lt_off(k, 16 * cb + (l & 15))], bv, acc[cb]);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-// GEMM1 with 32-row stages: only A (the Lt_J stage every wave reads) goes through the LDS
-// ring (2 x 32 KiB); each wave's B operand (its own 16 columns of Lt_I) is loaded straight
-// into registers one stage ahead.  Half the barriers of the 16-row A+B ring.
+// GEMM1: acc[cb] -= sum_{k < 128J} L_J[c][k] L_I[i][k] for the wave's 16 columns i, on 32-row
+// stages: only A (the Lt_J stage every wave reads) goes through the LDS ring (2 x 32 KiB);
+// each wave's B operand (its own 16 columns of Lt_I) is loaded straight into registers one
+// stage ahead.  (A 16-row A+B ring has twice the barriers and measured 2% slower.)
 __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
                                           double* lds, v4d (&acc)[8]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -613,37 +475,8 @@ __device__ __forceinline__ void syrk_stage8(const double* As, v4d (&acc)[5], int
   }
 }
 
-template <int D>
-__device__ __forceinline__ void syrk_lower8(const double* __restrict__ src, int nst, double* lds, v4d (&acc)[5]) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (nst <= 0) return;
-  auto issue = [&](int s) { glds_lt_stage8w(src + (int64_t)s * LTS, lds + (s % D) * LTS); };
-  for (int s = 0; s < D - 1 && s < nst; ++s) issue(s);
-  for (int s = 0; s < nst; ++s) {
-    if (s + D - 2 < nst) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (s + D - 1 < nst) issue(s + D - 1);
-    const double* As = lds + (s % D) * LTS;
-    switch (w) {
-      case 0: syrk_stage8<0>(As, acc, l); break;
-      case 1: syrk_stage8<1>(As, acc, l); break;
-      case 2: syrk_stage8<2>(As, acc, l); break;
-      case 3: syrk_stage8<3>(As, acc, l); break;
-      case 4: syrk_stage8<4>(As, acc, l); break;
-      case 5: syrk_stage8<5>(As, acc, l); break;
-      case 6: syrk_stage8<6>(As, acc, l); break;
-      default: syrk_stage8<7>(As, acc, l); break;
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-// The same SYRK on 32-row stages (2 x 32 KiB ring): half the barriers per k row.
+// SYRK of Lt rows restricted to the 36 lower blocks, 8 waves (wave W takes blocks W + 8i),
+// on 32-row stages through a 2 x 32 KiB LDS-DMA ring: one barrier per 32 k rows.
 __device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, int nst16, double* lds, v4d (&acc)[5]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (nst16 <= 0) return;
