@@ -146,9 +146,12 @@ def main():
 
     import torch
     import torch.distributed as dist
+    from tblup_amd import distributed as tdist
     torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    # the same process-group set-up and all-gather the drop-in evaluator uses
+    # (ParallelEvaluator.__enter__ -> init_from_env; _fitness -> allgather)
+    os.environ.setdefault("TBLUP_DIST_BACKEND", "nccl")
+    owns_group = tdist.init_from_env(local_rank)
     from tblup_amd.engine import GpuBlupEngine, concat_genomes
 
     eng = GpuBlupEngine(geno, pheno, device=local_rank)
@@ -164,7 +167,7 @@ def main():
         eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, args.h2, d_fit.data_ptr(),
                             stream_ptr=stream.cuda_stream)
         if world > 1:
-            dist.all_gather_into_tensor(full, d_fit)
+            tdist.allgather_device(full, d_fit)
 
     def timed_steps():
         if world > 1:
@@ -309,8 +312,8 @@ def main():
         }
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    if owns_group:
+        tdist.destroy()
 
 
 if __name__ == "__main__":

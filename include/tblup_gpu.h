@@ -36,7 +36,8 @@ enum {
   TBLUP_ERR_ARG = -1,      /* invalid argument (shape, index range, unknown split) */
   TBLUP_ERR_HIP = -2,      /* HIP runtime error (no device, launch or copy failure) */
   TBLUP_ERR_OOM = -3,      /* device allocation failed */
-  TBLUP_ERR_STATE = -4     /* call out of order */
+  TBLUP_ERR_STATE = -4,    /* call out of order */
+  TBLUP_ERR_INDEX = -5     /* SNP index outside [-n_snps, n_snps): numpy's IndexError for data[:, indices] */
 };
 
 enum {
@@ -99,7 +100,11 @@ int tblup_get_traits(tblup_ctx* ctx, int64_t* n_traits);
 /*
  * Evaluate `batch` individuals (one blup() call each, evaluator.py:244-314).
  *   idx      : concatenated selected SNP column indices (duplicates allowed,
- *              any order), length offsets[batch]
+ *              any order), length offsets[batch].  numpy fancy-index rules, as the
+ *              reference's data[:, indices] (evaluator.py:275/298) applies them to an
+ *              IndexIndividual genome (individual.py:93-95, unclipped DE can go
+ *              negative): -n_snps <= i < 0 addresses column i + n_snps; any index
+ *              outside [-n_snps, n_snps) fails the whole call with TBLUP_ERR_INDEX
  *   offsets  : batch+1 prefix offsets into idx; an individual may have k >= 1
  *   h2       : heritability, lambda = (1-h2)/h2
  *   branch   : TBLUP_BRANCH_*
@@ -117,9 +122,9 @@ int tblup_eval_batch(tblup_ctx* ctx, int split_id, const int64_t* idx, const int
  * d_idx / d_offsets / d_fitness / d_ebv are device pointers on the
  * context's device; h_offsets is the same batch+1 offsets on the host (used
  * for workspace sizing).  The workspace is shared with other calls on the
- * context: calls must be serialised on one stream.  Indices are NOT range-checked here
- * (out-of-range ids are clamped in-kernel); use tblup_eval_batch for checked
- * input.
+ * context: calls must be serialised on one stream.  Negative indices wrap as in
+ * tblup_eval_batch; an individual with an index outside [-n_snps, n_snps) gets a NaN
+ * fitness and raises the context's index-error flag (read it with tblup_index_error).
  */
 int tblup_eval_batch_device(tblup_ctx* ctx, int split_id, const int64_t* d_idx,
                             const int64_t* d_offsets, const int64_t* h_offsets, int64_t batch,
@@ -219,6 +224,11 @@ int tblup_de_step_device(tblup_ctx* ctx, int strategy, const double* d_parents, 
 /* Host-only: advance numpy's MT19937 (key[624], pos) state by n_words 32-bit outputs
  * (GF(2) jump-ahead; used to check the DE step's stream arithmetic without a GPU). */
 int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint32_t* key_out, int32_t* pos_out);
+
+/* Index-error flag of the device entry points: synchronises `stream` (NULL = the context's
+ * stream), sets *flag = 1 if any individual evaluated since the last call had an index
+ * outside [-n_snps, n_snps) (its fitness is NaN), and clears the flag. */
+int tblup_index_error(tblup_ctx* ctx, void* stream, int* flag);
 
 /* Device memory currently held by the context (bytes). */
 int tblup_mem_info(tblup_ctx* ctx, int64_t* bytes_in_use);

@@ -15,6 +15,7 @@ LAYOUT_ANIMAL_MAJOR = 0
 LAYOUT_SNP_MAJOR = 1
 N_KCLASS = 6
 MAX_TRAITS = 4
+ERR_INDEX = -5   # TBLUP_ERR_INDEX: numpy's IndexError for data[:, indices]
 KCLASS_NAMES = ("stats", "gather", "grm", "chol_diag", "chol_offdiag", "solve")
 
 # Every symbol of include/tblup_gpu.h with (restype, argtypes).
@@ -42,6 +43,7 @@ SIGNATURES = {
     "tblup_reset_profile": (_c.c_int, [_P]),
     "tblup_debug_grm": (_c.c_int, [_P, _c.c_int, _I64P, _c.c_int64, _c.c_double, _c.c_int, _c.c_int, _DP, _DP]),
     "tblup_mem_info": (_c.c_int, [_P, _I64P]),
+    "tblup_index_error": (_c.c_int, [_P, _P, _c.POINTER(_c.c_int)]),
     "tblup_decode_topk": (_c.c_int, [_P, _DP, _c.c_int64, _c.c_int64, _I64P, _I64P]),
     "tblup_decode_topk_device": (_c.c_int, [_P, _P, _c.c_int64, _c.c_int64, _c.c_int64, _P, _I64P, _P, _P]),
     "tblup_de_step": (_c.c_int, [_P, _c.c_int, _DP, _c.c_int64, _c.c_int64, _I32P, _I64P, _c.c_double, _c.c_double,
@@ -62,6 +64,11 @@ class TblupError(RuntimeError):
     def __init__(self, fn, code, msg):
         super().__init__(f"{fn} failed ({code}): {msg}")
         self.code = code
+
+
+class TblupIndexError(TblupError, IndexError):
+    """A selected-SNP index outside [-P, P): what numpy raises for the reference's
+    data[:, indices] (evaluator.py:275/298)."""
 
 
 _lib = None
@@ -96,7 +103,7 @@ def load():
 def check(fn_name, rc):
     if rc != 0:
         msg = load().tblup_last_error().decode(errors="replace")
-        raise TblupError(fn_name, rc, msg)
+        raise (TblupIndexError if rc == ERR_INDEX else TblupError)(fn_name, rc, msg)
     return rc
 
 

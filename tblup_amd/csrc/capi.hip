@@ -66,6 +66,7 @@ struct tblup_ctx {
   hipStream_t stream = nullptr;
   int64_t n = 0, P = 0;
   DevBuf geno_sm, colsum_all, scratch;
+  DevBuf idx_err;              // int32 device flag: an index outside [-P, P) reached k_indiv_stats
   std::vector<double> pheno;   // [n][nt] animal-major
   int nt = 1;                  // traits (tblup_set_traits)
   std::map<int, std::unique_ptr<Split>> splits;
@@ -264,7 +265,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   int rc;
   rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
     return launch_indiv_stats(d_idx, d_off, B, csT, csA, (const double*)sp.xty.p, d, sd, branch, h2,
-                              scal, u, rhs, s);
+                              scal, u, rhs, (int32_t*)c->idx_err.p, s);
   });
   if (rc) return rc;
   if (sd.form == FORM_DUAL) {
@@ -390,6 +391,8 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   const size_t gbytes = (size_t)n * (size_t)P;
   if (int rc = dev_alloc(c.get(), c->geno_sm, gbytes)) return rc;
   if (int rc = dev_alloc(c.get(), c->colsum_all, (size_t)P * 4)) return rc;
+  if (int rc = dev_alloc(c.get(), c->idx_err, 4)) return rc;
+  HIPCHK(hipMemsetAsync(c->idx_err.p, 0, 4, c->stream));
   if (layout == TBLUP_LAYOUT_SNP_MAJOR) {
     HIPCHK(hipMemcpyAsync(c->geno_sm.p, geno, gbytes, hipMemcpyHostToDevice, c->stream));
   } else {
@@ -424,6 +427,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   }
   c->geno_sm.release();
   c->colsum_all.release();
+  c->idx_err.release();
   c->scratch.release();
   c->ws.release();
   c->dec_keys.release();
@@ -548,6 +552,16 @@ int tblup_drop_split(tblup_ctx* c, int split_id) {
   return 0;
 }
 
+// numpy's fancy-index bound (the reference's data[:, indices], evaluator.py:275/298):
+// -P <= i < P is valid (negatives wrap, on the device); anything else is numpy's IndexError.
+static int check_indices(const tblup_ctx* c, const int64_t* idx, int64_t count) {
+  for (int64_t i = 0; i < count; ++i)
+    if (idx[i] < -c->P || idx[i] >= c->P)
+      return fail(TBLUP_ERR_INDEX, "index " + std::to_string(idx[i]) + " is out of bounds for axis 1 with size " +
+                                       std::to_string(c->P));
+  return 0;
+}
+
 static int validate_batch(tblup_ctx* c, int branch, double h2, const int64_t* offsets, int64_t batch) {
   if (branch < 0 || branch > 2) return fail(TBLUP_ERR_ARG, "bad branch");
   if (!(h2 > 0.0) || !(h2 <= 1.0)) return fail(TBLUP_ERR_ARG, "h2 must be in (0, 1]");
@@ -569,8 +583,7 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
   if (!idx || !fitness) return fail(TBLUP_ERR_ARG, "null idx/fitness");
   Split* sp = find_split(c, split_id);
   if (!sp) return fail(TBLUP_ERR_ARG, "unknown split id");
-  for (int64_t i = 0; i < offsets[batch]; ++i)
-    if (idx[i] < 0 || idx[i] >= c->P) return fail(TBLUP_ERR_ARG, "SNP index out of range");
+  if (int rc = check_indices(c, idx, offsets[batch])) return rc;
   HIPCHK(hipSetDevice(c->device));
   const EvalDims d = dims_of(c, *sp);
   const bool want_ebv = ebv != nullptr;
@@ -725,8 +738,7 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
   if (stage != 1 && stage != 2) return fail(TBLUP_ERR_ARG, "stage must be 1 or 2");
   int64_t offs[2] = {0, k};
   if (int rc = validate_batch(c, branch, h2, offs, 1)) return rc;
-  for (int64_t i = 0; i < k; ++i)
-    if (idx[i] < 0 || idx[i] >= c->P) return fail(TBLUP_ERR_ARG, "SNP index out of range");
+  if (int rc = check_indices(c, idx, k)) return rc;
   Split* sp = find_split(c, split_id);
   if (!sp) return fail(TBLUP_ERR_ARG, "unknown split id");
   HIPCHK(hipSetDevice(c->device));
@@ -922,6 +934,22 @@ int tblup_de_step(tblup_ctx* c, int strategy, const double* parents, int64_t pop
                                     clip_hi, mt_key, mt_pos, (double*)c->de_chi.p, L, nullptr))
     return rc;
   HIPCHK(hipMemcpy(children, c->de_chi.p, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tblup_index_error(tblup_ctx* c, void* stream, int* flag) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (!flag) return fail(TBLUP_ERR_ARG, "null flag");
+  *flag = 0;
+  if (!c->idx_err.p) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  int32_t h = 0;
+  HIPCHK(hipMemcpyAsync(&h, c->idx_err.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemsetAsync(c->idx_err.p, 0, 4, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *flag = h != 0;
   return 0;
 }
 

@@ -197,8 +197,7 @@ __device__ __forceinline__ const uint8_t* row_packed(const CholArgs& a, int64_t 
   const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
   int64_t p = a.P;
   if (r < k) {
-    p = a.idx[o0 + r];
-    p = p < 0 ? 0 : (p >= a.P ? a.P - 1 : p);
+    p = snp_col(a.idx[o0 + r], a.P);
   }
   return a.gs + p * a.gs_row;
 }

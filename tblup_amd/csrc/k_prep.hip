@@ -143,15 +143,13 @@ hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const
 // ---------------------------------------------------------------------------
 // per-individual scalars: branch, 1/N, q/N^2, 1/d, mu, lambda
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int64_t clamp_idx(int64_t p, int64_t P) { return p < 0 ? 0 : (p >= P ? P - 1 : p); }
-
 __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ csT,
                                                      const int32_t* __restrict__ csA, const double* __restrict__ xty,
                                                      int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
                                                      int64_t ns, int nt, int branch, double h2,
                                                      double* __restrict__ scal, double* __restrict__ u,
-                                                     double* __restrict__ rhs) {
+                                                     double* __restrict__ rhs, int32_t* __restrict__ err) {
   const int64_t b = blockIdx.x;
   const int64_t o0 = off[b], k = off[b + 1] - o0;
   int mode = branch;
@@ -159,8 +157,11 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
   const int32_t* cs = (mode == 1) ? csA : csT;
   const bool primal = form == FORM_PRIMAL;   // snp branch only (host guarantees)
   int64_t m1 = 0, q = 0;
+  int bad = 0;
   for (int64_t s = threadIdx.x; s < k; s += 256) {
-    const int64_t m = cs[clamp_idx(idx[o0 + s], P)];
+    const int64_t p = idx[o0 + s];
+    bad |= (p < -P || p >= P);
+    const int64_t m = cs[snp_col(p, P)];
     m1 += m;
     q += m * m;
   }
@@ -168,7 +169,8 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
   __shared__ double invd_sh;
   r1[threadIdx.x] = m1;
   r2[threadIdx.x] = q;
-  __syncthreads();
+  const int any_bad = __syncthreads_or(bad);
+  if (any_bad && threadIdx.x == 0) *err = 1;   // vector store; every writer stores 1
   for (int st = 128; st > 0; st >>= 1) {
     if ((int)threadIdx.x < st) {
       r1[threadIdx.x] += r1[threadIdx.x + st];
@@ -193,6 +195,7 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
     sc[SC_SM] = primal ? 1.0 / (double)nT : 0.0;
     sc[SC_NROW] = primal ? (double)k : (double)nT;
     sc[SC_CBLK] = primal ? (double)(nTp / KBLK) : (double)((k + KBLK - 1) / KBLK);
+    sc[SC_BAD] = any_bad ? 1.0 : 0.0;
     invd_sh = 1.0 / d;
   }
   if (!primal) return;
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
   const double invd = invd_sh;
   for (int64_t a = threadIdx.x; a < ns; a += 256) {
     const bool real = a < k;
-    const int64_t p = real ? clamp_idx(idx[o0 + a], P) : 0;
+    const int64_t p = real ? snp_col(idx[o0 + a], P) : 0;
     u[b * ns + a] = real ? (double)csT[p] : 0.0;
     for (int t = 0; t < nt; ++t) rhs[(b * nt + t) * ns + a] = real ? xty[t * P + p] * invd : 0.0;
   }
@@ -210,9 +213,10 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
 
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
                               const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
-                              int branch, double h2, double* scal, double* u, double* rhs, hipStream_t s) {
+                              int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
+                              hipStream_t s) {
   hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, colsum_T, colsum_all, xty, d.n,
-                     d.nT, d.nTp, d.P, sd.form, sd.ns, d.nt, branch, h2, scal, u, rhs);
+                     d.nT, d.nTp, d.P, sd.form, sd.ns, d.nt, branch, h2, scal, u, rhs, err);
   return hipGetLastError();
 }
 
@@ -244,7 +248,7 @@ __global__ __launch_bounds__(128) void k_gather(const int8_t* __restrict__ gs, c
     if (t < KBLK) {
       const int64_t s = kb * KBLK + t;
       if (s < k) {
-        const int64_t p = clamp_idx(idx[o0 + s], P);
+        const int64_t p = snp_col(idx[o0 + s], P);
         srow[t] = p;
         sm[t] = cs[p];
       } else {

@@ -189,8 +189,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   if (c.sd.form == FORM_PRIMAL) {
     const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b];
     for (int64_t r = t; r < kk; r += NTH) {
-      int64_t p = c.idx[o0 + r];
-      rowp[r] = (int32_t)(p < 0 ? 0 : (p >= c.d.P ? c.d.P - 1 : p));
+      rowp[r] = (int32_t)snp_col(c.idx[o0 + r], c.d.P);
     }
     __syncthreads();
   }
@@ -307,7 +306,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       for (int64_t v = t; v < nV; v += NTH) ebv[(b * nt + tr) * nV + v] = e[v];
     }
   }
-  if (t == 0) fit[b] = (nt == 1) ? fsum : fsum / (double)nt;
+  if (t == 0) fit[b] = sc[SC_BAD] != 0.0 ? __builtin_nan("") : (nt == 1) ? fsum : fsum / (double)nt;
 }
 
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s) {

@@ -50,8 +50,18 @@ enum {
   SC_SM = 8,    // multiplicative centring coefficient (dual 0, primal 1/n_T)
   SC_NROW = 9,  // real system rows (dual n_T, primal k); the rest is identity padding
   SC_CBLK = 10, // contraction blocks of 64 for the system matrix
+  SC_BAD = 11,  // 1 when an index lies outside [-P, P) (numpy would raise IndexError): fitness NaN
 };
 enum { FORM_DUAL = 0, FORM_PRIMAL = 1 };
+
+// Panel column of a selected-SNP index with numpy's fancy-index rule (the reference's
+// data[:, indices], evaluator.py:275/298): -P <= p < 0 addresses column p + P.  Indices
+// outside [-P, P) are rejected on the host (tblup_eval_batch) or flagged by k_indiv_stats
+// (device entry); the clamp below only keeps such a flagged individual's loads in bounds.
+__host__ __device__ __forceinline__ int64_t snp_col(int64_t p, int64_t P) {
+  p = p < 0 ? p + P : p;
+  return p < 0 ? 0 : (p >= P ? P - 1 : p);
+}
 constexpr int FLAG_WRITE_LJJ = 1 << 16;   // CholLaunch::skip: also store L_JJ (debug readback only)
 
 // System dimensions of one chunk.
@@ -99,7 +109,8 @@ hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const
 // primal form (sd.form): also u[b][a] = s_a and rhs[b][t][a] = xty[t][p_a] / d over the ns rows
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
                               const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
-                              int branch, double h2, double* scal, double* u, double* rhs, hipStream_t s);
+                              int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
+                              hipStream_t s);
 hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int64_t* off,
                          int64_t panel_stride, int64_t B, const int32_t* colsum_T,
                          const int32_t* colsum_all, const double* scal, const EvalDims& d,

@@ -6,7 +6,16 @@ the whole genotype panel in its own HBM, evaluates a contiguous block of the
 population, and one all-gather of the float64 fitnesses (backend "nccl" = RCCL
 over xGMI on a GPU node, "gloo" on CPU) gives every rank the full vector, so the
 host-side DE step stays identical on every rank.
+
+Under `torchrun main.py` nothing in the reference creates a process group, so the
+evaluator does (`init_from_env`, called from ParallelEvaluator.__enter__ -- the
+place where the reference starts its workers, evaluator.py:120-131): it binds the
+process to GPU LOCAL_RANK and creates the default group ("nccl" = RCCL when a GPU
+is visible, else "gloo"; TBLUP_DIST_BACKEND overrides).  bench.py uses the same
+two functions for its N > 1 path.
 """
+import os
+
 import numpy as np
 
 
@@ -21,6 +30,35 @@ def world():
     return 0, 1
 
 
+def init_from_env(device=None):
+    """Create the default process group from the torchrun environment (RANK, WORLD_SIZE,
+    MASTER_ADDR, MASTER_PORT, LOCAL_RANK) when WORLD_SIZE > 1 and no group exists yet.
+
+    With the nccl backend the process is first bound to its GPU (`device`, else LOCAL_RANK)
+    so RCCL sees one device per rank.  Returns True when this call created the group (the
+    caller then owns it and destroys it), False otherwise."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return False
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or dist.is_initialized():
+        return False
+    backend = os.environ.get("TBLUP_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    kwargs = {}
+    if backend == "nccl":
+        local = int(os.environ.get("LOCAL_RANK", "0")) if device is None else int(device)
+        torch.cuda.set_device(local)
+        kwargs["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend, **kwargs)
+    return True
+
+
+def destroy():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def shard_range(n_items, rank, world_size):
     """Contiguous block [lo, hi) of n_items owned by `rank` (sizes differ by at most 1)."""
     base, rem = divmod(n_items, world_size)
@@ -29,8 +67,11 @@ def shard_range(n_items, rank, world_size):
     return lo, hi
 
 
-def allgather_fitness(local, n_total):
-    """All-gather the per-rank fitness blocks into the full float64 vector (rank order)."""
+def allgather_fitness(local, n_total, device=None):
+    """All-gather the per-rank fitness blocks into the full float64 vector (rank order).
+
+    With nccl the buffers live on `device` (the evaluating engine's GPU; default the
+    current device), so each rank hands RCCL its own GPU's memory."""
     import torch
     import torch.distributed as dist
 
@@ -39,14 +80,27 @@ def allgather_fitness(local, n_total):
         return np.asarray(local, dtype=np.float64)
     sizes = [shard_range(n_total, r, ws) for r in range(ws)]
     maxc = max(hi - lo for lo, hi in sizes)
-    backend = dist.get_backend()
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    if dist.get_backend() == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
+    else:
+        dev = torch.device("cpu")
     buf = torch.full((maxc,), float("nan"), dtype=torch.float64, device=dev)
     if len(local):
         buf[:len(local)] = torch.as_tensor(np.asarray(local, dtype=np.float64), device=dev)
-    out = [torch.empty_like(buf) for _ in range(ws)]
-    dist.all_gather(out, buf)
+    out = torch.empty(ws * maxc, dtype=torch.float64, device=dev)
+    allgather_device(out, buf)
+    out = out.cpu().numpy()
     full = np.empty(n_total, dtype=np.float64)
     for r, (lo, hi) in enumerate(sizes):
-        full[lo:hi] = out[r][:hi - lo].cpu().numpy()
+        full[lo:hi] = out[r * maxc:r * maxc + hi - lo]
     return full
+
+
+def allgather_device(out, local):
+    """out (world * len(local),) <- every rank's `local` block in rank order: the one
+    collective per generation (RCCL all-gather over xGMI under nccl)."""
+    import torch.distributed as dist
+    if dist.get_backend() == "gloo":
+        dist.all_gather(list(out.chunk(dist.get_world_size())), local)
+    else:
+        dist.all_gather_into_tensor(out, local)

@@ -142,6 +142,14 @@ class GpuBlupEngine:
             ctypes.c_void_p(d_ebv_ptr) if d_ebv_ptr else None,
             ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def index_error(self, stream_ptr=None):
+        """True if an individual evaluated through evaluate_device since the last call had an
+        index outside [-P, P) (its fitness is NaN); synchronises the stream, clears the flag."""
+        flag = ctypes.c_int(0)
+        _native.check("tblup_index_error", self._lib.tblup_index_error(
+            self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(flag)))
+        return bool(flag.value)
+
     def decode_randkey(self, keys, lengths):
         """RandomKeyIndividual.genome for a batch (individual.py:154-156) on the GPU:
         row i -> np.argsort(keys[i])[-int(lengths[i]):] (ascending key order; equal keys

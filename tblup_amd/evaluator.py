@@ -23,7 +23,7 @@ from math import sqrt
 
 import numpy as np
 
-from .distributed import allgather_fitness, shard_range, world
+from .distributed import allgather_fitness, destroy, init_from_env, shard_range, world
 
 
 def get_evaluator(args):
@@ -82,6 +82,9 @@ class ParallelEvaluator(Evaluator):
 
     The reference spawns `n_procs` workers in __enter__; here __enter__ opens
     the GPU context for this process (device = `device`, else LOCAL_RANK, else 0).
+    Launched one process per GPU (`torchrun main.py`, WORLD_SIZE > 1) it first creates
+    the default process group (RCCL) unless the caller already has one, and then every
+    batch of individuals is sharded across the ranks; __exit__ destroys a group it created.
     `n_procs` is kept for signature compatibility.
     """
 
@@ -90,6 +93,7 @@ class ParallelEvaluator(Evaluator):
         self.n_procs = n_procs
         self.device = device
         self.engine = None
+        self._owns_group = False
 
     def _device(self):
         if self.device is not None:
@@ -103,6 +107,8 @@ class ParallelEvaluator(Evaluator):
         return GpuBlupEngine(data, labels, device=self._device())
 
     def __enter__(self):
+        if init_from_env(self._device()):
+            self._owns_group = True
         if self.engine is None:
             self.engine = self._open_engine()
         return self
@@ -111,6 +117,9 @@ class ParallelEvaluator(Evaluator):
         if self.engine is not None:
             self.engine.close()
             self.engine = None
+        if self._owns_group:
+            self._owns_group = False
+            destroy()
 
     def genomes_to_evaluate(self, population):
         raise NotImplementedError()
@@ -166,7 +175,7 @@ class BlupParallelEvaluator(ParallelEvaluator):
             return self.engine.evaluate(genomes, train_indices, validation_indices, self.h2)
         lo, hi = shard_range(total, rank, ws)
         local = self.engine.evaluate(genomes[lo:hi], train_indices, validation_indices, self.h2)
-        return allgather_fitness(local, total)
+        return allgather_fitness(local, total, getattr(self.engine, "device", None))
 
     @staticmethod
     def blup(indices, train_indices, validation_indices, data, labels, h2):
@@ -192,7 +201,7 @@ class BlupParallelEvaluator(ParallelEvaluator):
         return self.training_indices, self.validation_indices
 
     def __getstate__(self):
-        return {k: v for k, v in self.__dict__.items() if k not in ("archive", "pool", "engine")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("archive", "pool", "engine", "_owns_group")}
 
     def genomes_to_evaluate(self, population):
         """Individuals whose uid is not archived (evaluator.py:339-357)."""

@@ -29,7 +29,7 @@ from copy import deepcopy
 import numpy as np
 
 from . import _native
-from .keystore import DeviceKeyStore, work_stream
+from .keystore import DeviceKeyStore, track, work_stream
 
 
 def get_evolver(args):
@@ -152,11 +152,15 @@ _POOL = None
 
 
 def _copy_rows(host, dtypes, workers=8):
+    """An own array per child: float64 rows as TrackedGenome views (the key store mirrors
+    them on the device and must notice in-place writes), other dtypes as plain arrays."""
     global _POOL
     n = host.shape[0]
 
     def chunk(lo, hi):
-        return [np.array(host[i], dtype=None if dtypes is None else dtypes[i]) for i in range(lo, hi)]
+        if dtypes is None:
+            return [track(np.array(host[i])) for i in range(lo, hi)]
+        return [np.array(host[i], dtype=dtypes[i]) for i in range(lo, hi)]
     if n * host.shape[1] < (1 << 20):
         return chunk(0, n)
     if _POOL is None:
@@ -222,7 +226,7 @@ class _GpuDEEvolver(Evolver):
             next_pop.append(candidate)
         if dtypes is None:   # float64 internal genomes: the device rows are the children's exact values
             store.record(children, next_pop, arrays)
-            store.record(parents, inds, genomes)
+            store.record(parents, inds, genomes, adopt=True)
         store.prune([x.uid for x in inds] + [x.uid for x in next_pop])
         return next_pop
 

@@ -8,16 +8,67 @@ Individual objects) instead of three times (parents up, children down, keys up
 again for the decode).
 
 An entry is valid while the individual still holds the very numpy array the
-entry was recorded with (`indv._genome is <recorded array>`, arrays made
-read-only when recorded) and the same `length`: `set_internal_genome` and
-`fill` (the only ways the reference changes a genome, individual.py:103-130,
-187-208, scheduler.py:209-251) either replace the array or change the length,
-which invalidates the entry; the individual is then read from the host.
-Device memory is plumbing here: torch tensors on the context's device.
+entry was recorded with (`indv._genome is <recorded array>`), that array has not
+been written since, and the individual has the same `length`.
+`set_internal_genome` and `fill` (individual.py:103-130, 187-208,
+scheduler.py:209-251) replace the array or change the length; an in-place write
+(`Individual.__setitem__`, individual.py:119-120, or any numpy write through the
+array or a view of it) marks the recorded array stale -- recorded arrays are
+`TrackedGenome` views (an ndarray subclass that notices item assignment and
+in-place ufuncs) and stay writable, as the reference allows.  A stale or replaced
+genome is read from the host.  Device memory is plumbing here: torch tensors on
+the context's device.
 """
 import weakref
 
 import numpy as np
+
+
+class TrackedGenome(np.ndarray):
+    """A genome array the key store mirrors on the device.  Writes through it or through
+    any view of it (item assignment, in-place ufuncs / `out=`) mark the owning array
+    stale; values and semantics are otherwise those of the ndarray it views.  Results of
+    computations on it are plain ndarrays."""
+
+    _owner = None
+    _stale = False
+
+    def __array_finalize__(self, obj):
+        if isinstance(obj, TrackedGenome):
+            self._owner = obj._owner if obj._owner is not None else obj
+
+    def _touch(self):
+        (self._owner if self._owner is not None else self)._stale = True
+
+    def __setitem__(self, key, value):
+        self._touch()
+        super().__setitem__(key, value)
+
+    def __array_ufunc__(self, ufunc, method, *inputs, out=None, **kwargs):
+        plain = tuple(x.view(np.ndarray) if isinstance(x, TrackedGenome) else x for x in inputs)
+        if out is not None:
+            for o in out:
+                if isinstance(o, TrackedGenome):
+                    o._touch()
+            kwargs["out"] = tuple(o.view(np.ndarray) if isinstance(o, TrackedGenome) else o for o in out)
+        res = getattr(ufunc, method)(*plain, **kwargs)
+        if out is not None:
+            return out[0] if len(out) == 1 else out
+        return res
+
+    def __reduce__(self):   # pickles / deep-copies as a plain ndarray
+        return self.view(np.ndarray).__reduce__()
+
+    def __deepcopy__(self, memo):
+        return self.view(np.ndarray).copy()
+
+    def __copy__(self):
+        return self.view(np.ndarray).copy()
+
+
+def track(a):
+    """A TrackedGenome view of the float64 array `a` (no copy)."""
+    return a.view(TrackedGenome)
 
 
 _STREAMS = {}
@@ -54,16 +105,26 @@ class DeviceKeyStore:
         g = getattr(indv, "_genome", None)
         return g if isinstance(g, np.ndarray) else None
 
-    def record(self, tensor, individuals, arrays):
+    def record(self, tensor, individuals, arrays, adopt=False):
         """Row i of `tensor` (pop x L, on the device) holds arrays[i]; recorded for individuals
         whose internal genome IS that array (RandomKey / Index semantics: get_internal_genome()
-        returns `_genome`).  Individuals that derive their internal genome (Coevolution appends
-        its length) are not recorded and are read from the host."""
+        returns `_genome`) and a TrackedGenome (the evolver hands its children such views;
+        parents recorded from other arrays are not tracked and are read from the host).
+        Individuals that derive their internal genome (Coevolution appends its length) are not
+        recorded and are read from the host."""
         for i, indv in enumerate(individuals):
             g = self._key_array(indv)
             if g is None or g is not arrays[i]:
                 continue
-            g.flags.writeable = False
+            if not isinstance(g, TrackedGenome):
+                # a genome the evolver did not create (the initial population): adopt it as a
+                # tracked view of the same buffer when nothing else views that buffer
+                if not adopt or g.base is not None or g.dtype != np.float64 or not g.flags.c_contiguous:
+                    continue
+                g = track(g)
+                indv._genome = g
+            if g._stale:
+                continue
             self._entries[indv.uid] = (tensor, i, weakref.ref(g), getattr(indv, "length", None))
 
     def lookup(self, indv):
@@ -71,7 +132,8 @@ class DeviceKeyStore:
         if e is None:
             return None
         tensor, row, ref, length = e
-        if ref() is not self._key_array(indv) or getattr(indv, "length", None) != length:
+        g = ref()
+        if g is None or g is not self._key_array(indv) or g._stale or getattr(indv, "length", None) != length:
             del self._entries[indv.uid]
             return None
         return tensor, row

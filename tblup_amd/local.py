@@ -70,13 +70,22 @@ class KnockoutLocalSearch(LocalSearch):
         self.window = window
 
     def search(self):
+        """main.py:42-45 runs the search after `with evaluator:` has closed, so the
+        evaluator's context is gone; like the reference's search, which np.loads the data
+        itself (local.py:59), a short-lived GPU context is opened for the walk then."""
         evaluator = self.population.evaluator
         best = deepcopy(max(self.population, key=lambda individual: individual.fitness))
         genome = evaluator.snp_remover.combine_with_removed(best.genome)
         train, valid = evaluator.training_indices, evaluator.validation_indices
+        engine, own = evaluator.engine, evaluator.engine is None
+        if own:
+            engine = evaluator._open_engine()
+        try:
+            def evaluate_batch(subsets):
+                return engine.evaluate(subsets, train, valid, evaluator.h2)
 
-        def evaluate_batch(subsets):
-            return evaluator.engine.evaluate(subsets, train, valid, evaluator.h2)
-
-        mask, best_fitness, _ = knockout_walk(genome, best.fitness, evaluate_batch, self.window)
+            mask, best_fitness, _ = knockout_walk(genome, best.fitness, evaluate_batch, self.window)
+        finally:
+            if own:
+                engine.close()
         return genome[mask], best_fitness

@@ -17,6 +17,7 @@ in a different order than BLAS); the SNP ranking is identical unless two SNPs'
 scores differ by less than that (tests/test_seeder.py).
 """
 import abc
+import os
 
 import numpy as np
 
@@ -113,7 +114,7 @@ class SeedStrategy(abc.ABC):
         X, y = np.load(geno_path), np.load(pheno_path)
         y = np.asarray(y)
         scores = np.zeros(X.shape[1])
-        eng = GpuBlupEngine(X, np.zeros(X.shape[0]))
+        eng = GpuBlupEngine(X, np.zeros(X.shape[0]), device=int(os.environ.get("LOCAL_RANK", "0")))
         try:
             for train, _ in KFold(n_splits=self.N_SPLITS).split(self.training_indices):
                 scores += self.metric(eng, train, y[train].ravel())

@@ -40,3 +40,48 @@ def run(rank, world, port, gp, pp, keys_path, out_dir):
                "evaluated": seen, "shard": [lo, hi]}, open(os.path.join(out_dir, f"rank{rank}.json"), "w"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_main_flow(rank, world, port, case, out_dir):
+    """main.py-style run (tests/ga_driver.py) of a tests/golden/main_runs.npz case under a
+    torchrun-like environment with NO process group created by the caller: the evaluator's
+    __enter__ must create it (gloo here), shard every batch and destroy it on exit."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TBLUP_DIST_BACKEND="gloo")
+    import numpy as np
+    import torch.distributed as dist
+
+    from tblup_amd import evaluator as E
+    from tblup_amd import local as LS
+    from tests import ga_driver as D
+    from tests.helpers import OracleEngine
+
+    z = np.load(os.path.join(root, "tests", "golden", "main_runs.npz"))
+    gp, pp = os.path.join(out_dir, "geno.npy"), os.path.join(out_dir, "pheno.npy")
+    seen, inside = [], []
+
+    def get_evaluator(args):
+        ev = E.get_evaluator(args)
+
+        def open_engine():
+            inside.append(dist.is_initialized())
+            eng = OracleEngine(np.load(ev.data_path), np.load(ev.labels_path))
+            orig = eng.evaluate
+
+            def spy(genomes, *a, **k):
+                seen.append(len(genomes))
+                return orig(genomes, *a, **k)
+            eng.evaluate = spy
+            return eng
+        ev._open_engine = open_engine
+        return ev
+
+    argv = list(z["base_argv"]) + ["--geno", gp, "--pheno", pp] + list(z[case + "_argv"])
+    assert not dist.is_initialized()
+    run = D.run_main(argv, get_evaluator, D.OracleEvolver, LS.get_local_search)
+    after = dist.is_initialized()
+    D.compare(run, z, case)
+    json.dump({"seen": seen, "group_inside": inside, "group_after": after},
+              open(os.path.join(out_dir, f"main_rank{rank}.json"), "w"))

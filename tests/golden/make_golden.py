@@ -475,14 +475,166 @@ def gen_seed():
     np.savez_compressed(os.path.join(HERE, "seed.npz"), **out)
 
 
+def gen_blup_extra():
+    """numpy index semantics and float32 inputs on the 200x1000 panel (blup_extra.npz).
+
+    * IndexIndividual genomes with negative entries (individual.py:93-95 truncates the
+      internal floats with astype(int); DE without --clip leaves them negative): the
+      reference's data[:, indices] (evaluator.py:275/298) wraps them to i + P.
+    * an index >= P: numpy raises IndexError (recorded as the failure mode).
+    * float32 genotype panels: snp_blup then computes in float32 in place
+      (evaluator.py:298-309) and make_grm in float32 (utils.py:7-18).
+    """
+    from tblup.individual import IndexIndividual
+    z = np.load(os.path.join(HERE, "blup_200x1000.npz"))
+    geno, pheno, T, V = z["geno"], z["pheno"], list(z["T"]), list(z["V"])
+    n, p = geno.shape
+    data = geno.astype(np.float64)
+    rng = np.random.default_rng(404)
+    out = {}
+    neg_cases = []
+    for name, k, lo in (("neg_snp", 100, -300.0), ("neg_gblup", 300, -700.0), ("neg_dup", 90, -40.0)):
+        internal = rng.uniform(lo, p - 0.01, size=k)
+        if name == "neg_dup":
+            internal[30:60] = rng.uniform(1.0, p - 0.01, size=30)
+            internal[:30] = internal[30:60] - p      # -P + i and i address the same column
+        idx = IndexIndividual(k, p, genome=internal.copy()).genome
+        assert (idx < 0).any()
+        f, e, br = ref_blup(idx, T, V, data, pheno, 0.4)
+        neg_cases.append(name)
+        out[name + "_internal"] = internal
+        out[name + "_idx"] = idx
+        out[name + "_fitness"] = f
+        out[name + "_ebv"] = e
+        out[name + "_branch"] = br
+    out["neg_names"] = np.array(neg_cases)
+    for name, idx in (("oob_hi", np.array([3, 17, p])), ("oob_lo", np.array([3, -p - 1, 17]))):
+        try:
+            ref_blup(idx, T, V, data, pheno, 0.4)
+            out[name + "_raises"] = np.array("")
+        except Exception as exc:  # numpy's fancy-index bound check
+            out[name + "_raises"] = np.array(type(exc).__name__)
+        out[name + "_idx"] = idx
+    data32 = geno.astype(np.float32)
+    f32 = []
+    for name, k in (("f32_snp", 100), ("f32_snp_kernel", 150), ("f32_gblup", 300)):
+        idx = rng.choice(p, k, replace=False)
+        f, e, br = ref_blup(idx, T, V, data32, pheno, 0.4)
+        f64, e64, _ = ref_blup(idx, T, V, data, pheno, 0.4)
+        f32.append(name)
+        out[name + "_idx"] = idx
+        out[name + "_fitness"] = f
+        out[name + "_ebv"] = e
+        out[name + "_fitness64"] = f64
+        out[name + "_ebv64"] = e64
+        out[name + "_branch"] = br
+    out["f32_names"] = np.array(f32)
+    np.savez_compressed(os.path.join(HERE, "blup_extra.npz"), **out)
+
+
+# main.py end to end on BASELINE config 1 (200 animals x 1000 SNPs, 100 features, pop 32),
+# one worker (-p 1): name -> extra command-line flags
+MAIN_CASES = [
+    ("rk_rand1", ["--generations", "6"]),
+    ("rk_ctb", ["--generations", "4", "--de_strategy", "de_currenttobest_1"]),
+    ("index_clip", ["--generations", "4", "--individual", "index", "--clip", "true"]),
+    ("coevolve", ["--generations", "3", "--individual", "coevolve"]),
+    ("intercv", ["--generations", "3", "--regressor", "intercv_blup"]),
+    ("intracv", ["--generations", "3", "--regressor", "intracv_blup"]),
+    ("montecv", ["--generations", "3", "--regressor", "montecv_blup"]),
+    ("removal_testing_knockout", ["--generations", "4", "--remove_snps", "true", "--removal_r", "20",
+                                  "--h2_alpha", "-0.45", "--record_testing", "true", "--local_search", "knockout"]),
+    ("stop_h2", ["--generations", "8", "--stop_condition", "h2_max", "--h2_alpha", "-0.3"]),
+]
+MAIN_BASE = ["-s", "7", "-p", "1", "--population_size", "32", "--features", "100", "--heritability", "0.4"]
+
+
+def gen_main_runs():
+    """The reference's main() (main.py:10-45) run end to end, in-process, per MAIN_CASES: the
+    results / testing CSV text, archive and local-search JSON, saved split indices, every
+    generation's fitness vector (Monitor.gather_stats wrapped) and the final population's
+    decoded genomes (evaluate_testing wrapped).  Writes main_runs.npz."""
+    import json
+    import signal
+    import tblup.monitor as mon
+    sys.path.insert(0, REF)
+    import main as ref_main
+    z = np.load(os.path.join(HERE, "blup_200x1000.npz"))
+    out = {"geno": z["geno"], "pheno": z["pheno"], "base_argv": np.array(MAIN_BASE),
+           "names": np.array([c[0] for c in MAIN_CASES])}
+    rec = {}
+    orig_gs = mon.Monitor.gather_stats
+    orig_et = ref_ev.BlupParallelEvaluator.evaluate_testing
+
+    def gs(self, population):
+        rec["fit"].append([float(i.fitness) for i in population])
+        rec["len"].append([float(len(i)) for i in population])
+        return orig_gs(self, population)
+
+    def et(self, population):
+        rec["genomes"] = [np.asarray(i.genome, dtype=np.int64) for i in population]
+        return orig_et(self, population)
+
+    def alarm(*a):
+        raise TimeoutError("reference main() did not finish (a worker error hangs it)")
+
+    mon.Monitor.gather_stats = gs
+    ref_ev.BlupParallelEvaluator.evaluate_testing = et
+    cwd = os.getcwd()
+    old = signal.signal(signal.SIGALRM, alarm)
+    try:
+        for name, extra in MAIN_CASES:
+            with tempfile.TemporaryDirectory() as td:
+                gp, pp = os.path.join(td, "geno.npy"), os.path.join(td, "pheno.npy")
+                np.save(gp, z["geno"].astype(np.float64))
+                np.save(pp, z["pheno"])
+                os.chdir(td)
+                argv = MAIN_BASE + ["--geno", gp, "--pheno", pp, "-o", "run"] + extra
+                rec.clear()
+                rec.update(fit=[], len=[], genomes=None)
+                sys.argv = ["main.py"] + argv
+                signal.alarm(900)
+                ref_main.main()
+                signal.alarm(0)
+                rd = os.path.join(td, "results", "run")
+                files = sorted(os.listdir(rd))
+
+                def text(fn):
+                    f = os.path.join(rd, fn)
+                    return open(f).read() if os.path.isfile(f) else ""
+                pre = name + "_"
+                out[pre + "argv"] = np.array(extra)
+                out[pre + "files"] = np.array(files)
+                out[pre + "results_csv"] = np.array(text("007_results.csv"))
+                out[pre + "testing_csv"] = np.array(text("007_results_testing.csv"))
+                out[pre + "archive_json"] = np.array(text("007_archive.json"))
+                out[pre + "local_json"] = np.array(text("007_local.json"))
+                out[pre + "removals"] = np.array(text("007_removals.csv"))
+                for part in ("train", "validation", "testing"):
+                    out[pre + part] = np.load(os.path.join(rd, "007_%s_indices.npy" % part))
+                out[pre + "gen_fitness"] = np.array(rec["fit"])
+                out[pre + "gen_len"] = np.array(rec["len"])
+                g = rec["genomes"]
+                out[pre + "final_idx"] = np.concatenate(g)
+                out[pre + "final_off"] = np.concatenate(([0], np.cumsum([len(x) for x in g])))
+                os.chdir(cwd)
+                print("main run", name, "generations", len(rec["fit"]) - 1, "archive",
+                      list(json.loads(str(out[pre + "archive_json"])).keys()))
+    finally:
+        os.chdir(cwd)
+        signal.signal(signal.SIGALRM, old)
+        mon.Monitor.gather_stats = orig_gs
+        ref_ev.BlupParallelEvaluator.evaluate_testing = orig_et
+    np.savez_compressed(os.path.join(HERE, "main_runs.npz"), **out)
+
+
+GENERATORS = {
+    "grm": gen_grm, "blup": gen_blup_small, "edge": gen_blup_edge, "decode": gen_decode,
+    "flow": gen_evaluator_flow, "config2": gen_blup_config2, "de": gen_de, "pca": gen_pca, "seed": gen_seed,
+    "extra": gen_blup_extra, "main": gen_main_runs,
+}
+
 if __name__ == "__main__":
-    gen_grm()
-    gen_blup_small()
-    gen_blup_edge()
-    gen_decode()
-    gen_evaluator_flow()
-    gen_blup_config2()
-    gen_de()
-    gen_pca()
-    gen_seed()
+    for key in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[key]()
     print("golden fixtures written to", HERE)

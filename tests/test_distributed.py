@@ -50,3 +50,30 @@ def test_two_rank_gloo_matches_single_process(golden_dir, tmp_path):
         assert res[r]["evaluated"][0] == hi - lo      # each rank computed only its own block
     assert res[0]["testing"] == res[1]["testing"]
     np.testing.assert_allclose(res[0]["testing"], flow["flow_testing"][:31], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("case", ["rk_rand1", "removal_testing_knockout"])
+def test_two_rank_main_flow_without_preinitialised_group(golden_dir, tmp_path, case):
+    """torchrun-style main.py run on 2 ranks where nothing but the evaluator creates the
+    process group (ParallelEvaluator.__enter__, the reference's worker start-up point,
+    evaluator.py:120-131): both ranks reproduce the reference's single-process run, each
+    evaluates only its shard of every batch (32 -> 16 + 16), the group exists inside the
+    `with evaluator:` block and is gone after it (the knockout search then runs per rank on
+    a short-lived context)."""
+    from tests import dist_worker
+    z = np.load(os.path.join(golden_dir, "main_runs.npz"))
+    np.save(tmp_path / "geno.npy", z["geno"].astype(np.float64))
+    np.save(tmp_path / "pheno.npy", z["pheno"])
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=dist_worker.run_main_flow, args=(r, 2, port, case, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    res = [json.load(open(tmp_path / f"main_rank{r}.json")) for r in range(2)]
+    for r in range(2):
+        assert res[r]["group_inside"][0] is True and res[r]["group_after"] is False
+        pop_batches = [n for n in res[r]["seen"][:2]]
+        assert pop_batches == [16, 16]          # generation 0 and 1: 32 individuals over 2 ranks

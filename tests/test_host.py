@@ -1,7 +1,8 @@
-"""Host-side evaluator logic (no GPU): splits, CV folds, archive, SNP removal,
-testing evaluation — checked against flows recorded from the reference evaluator
-(tests/golden/evaluator_flow.npz).  Compute goes through tests.helpers.OracleEngine,
-a test-only stand-in with GpuBlupEngine's evaluate() contract."""
+"""Evaluator flows: splits, CV folds, archive, SNP removal, testing evaluation —
+checked against flows recorded from the reference evaluator
+(tests/golden/evaluator_flow.npz).  Each flow runs twice: on the CPU through
+tests.helpers.OracleEngine (a test-only stand-in with GpuBlupEngine's evaluate()
+contract: pins the host logic) and, marked gpu, through the HIP engine itself."""
 import os
 import random
 
@@ -27,9 +28,29 @@ def flow(golden_dir):
     return np.load(os.path.join(golden_dir, "evaluator_flow.npz"))
 
 
-def _enter_with_oracle(ev, gp, pp):
-    ev.engine = OracleEngine(np.load(gp), np.load(pp))
-    return ev
+ENGINES = ["oracle", pytest.param("hip", marks=pytest.mark.gpu)]
+TOL = {"oracle": 1e-12, "hip": 1e-9}
+
+
+@pytest.fixture(params=ENGINES)
+def engine_kind(request):
+    return request.param
+
+
+@pytest.fixture
+def entered():
+    opened = []
+
+    def enter(ev, gp, pp, kind="oracle"):
+        if kind == "oracle":
+            ev.engine = OracleEngine(np.load(gp), np.load(pp))
+        else:
+            ev.__enter__()           # the GPU context, as `with evaluator:` opens it
+            opened.append(ev)
+        return ev
+    yield enter
+    for ev in opened:
+        ev.__exit__(None, None, None)
 
 
 def test_default_split_reproduces_reference(panel):
@@ -55,7 +76,7 @@ def test_split_disjoint_like_reference_unit_test(tmp_path):
     assert not (tr & va) and not (tr & te) and not (va & te)
 
 
-def test_generation0_population_and_testing(panel, flow):
+def test_generation0_population_and_testing(panel, flow, engine_kind, entered):
     gp, pp, _ = panel
     random.seed(3)
     np.random.seed(3)
@@ -64,14 +85,16 @@ def test_generation0_population_and_testing(panel, flow):
     np.testing.assert_array_equal(ev.training_indices, flow["flow_T"])
     np.testing.assert_array_equal(ev.testing_indices, flow["flow_X"])
     pop = [KeyIndividual(k, 100) for k in flow["flow_keys"]]
-    _enter_with_oracle(ev, gp, pp)
+    entered(ev, gp, pp, engine_kind)
+    tol = TOL[engine_kind]
     ev.evaluate(pop, pop, 0)
-    np.testing.assert_allclose([p.fitness for p in pop], flow["flow_fitness"], rtol=0, atol=1e-12)
-    np.testing.assert_allclose(ev.evaluate_testing(pop), flow["flow_testing"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose([p.fitness for p in pop], flow["flow_fitness"], rtol=0, atol=tol)
+    np.testing.assert_allclose(ev.evaluate_testing(pop), flow["flow_testing"], rtol=0, atol=tol)
     # archive hit: a second evaluate computes nothing new
-    calls = ev.engine.calls
-    ev.evaluate(pop, pop, 1)
-    assert ev.engine.calls == calls
+    if engine_kind == "oracle":
+        calls = ev.engine.calls
+        ev.evaluate(pop, pop, 1)
+        assert ev.engine.calls == calls
 
 
 def test_evaluate_requires_context():
@@ -81,7 +104,7 @@ def test_evaluate_requires_context():
         ev.evaluate([], [], 0)
 
 
-def test_intergcv_folds_and_intragcv_mean(panel, flow):
+def test_intergcv_folds_and_intragcv_mean(panel, flow, engine_kind, entered):
     gp, pp, _ = panel
     random.seed(4)
     np.random.seed(4)
@@ -94,9 +117,9 @@ def test_intergcv_folds_and_intragcv_mean(panel, flow):
     np.testing.assert_array_equal(va, flow["cv_fold_valid"])
     np.testing.assert_array_equal([len(f[1]) for f in ev.fold_indices], flow["cv_fold_valid_len"])
     pop = [IdxIndividual(g, 80) for g in flow["cv_genomes"]]
-    _enter_with_oracle(ev, gp, pp)
+    entered(ev, gp, pp, engine_kind)
     ev.evaluate(pop, pop, 0)
-    np.testing.assert_allclose([p.fitness for p in pop], flow["cv_intra_fitness"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose([p.fitness for p in pop], flow["cv_intra_fitness"], rtol=0, atol=TOL[engine_kind])
     # InterGCV rotates the fold with the generation
     inter = E.InterGCVBlupParallelEvaluator.__new__(E.InterGCVBlupParallelEvaluator)
     inter.fold_indices, inter.n_folds = ev.fold_indices, 5
@@ -115,7 +138,7 @@ def test_montecarlo_split_sequence(panel, flow):
     np.testing.assert_array_equal(np.array([s[1] for s in seq]), flow["mc_split_valid"])
 
 
-def test_snp_removal_flow(panel, flow):
+def test_snp_removal_flow(panel, flow, engine_kind, entered):
     gp, pp, _ = panel
     random.seed(6)
     np.random.seed(6)
@@ -140,12 +163,13 @@ def test_snp_removal_flow(panel, flow):
         monitor = _Mon()
 
     prev_pop = _Pop(prev)
-    _enter_with_oracle(ev, gp, pp)
+    entered(ev, gp, pp, engine_kind)
+    tol = TOL[engine_kind]
     ev.evaluate(prev_pop, nxt, 1)
     np.testing.assert_array_equal(rem.removed, flow["rm_removed"])
-    np.testing.assert_allclose([p.fitness for p in nxt], flow["rm_next_fitness"], rtol=0, atol=1e-12)
-    np.testing.assert_allclose([p.fitness for p in prev_pop], flow["rm_prev_fitness"], rtol=0, atol=1e-12)
-    np.testing.assert_allclose(ev.evaluate_testing(nxt), flow["rm_testing"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose([p.fitness for p in nxt], flow["rm_next_fitness"], rtol=0, atol=tol)
+    np.testing.assert_allclose([p.fitness for p in prev_pop], flow["rm_prev_fitness"], rtol=0, atol=tol)
+    np.testing.assert_allclose(ev.evaluate_testing(nxt), flow["rm_testing"], rtol=0, atol=tol)
     assert prev_pop.monitor.events == [1]
 
 

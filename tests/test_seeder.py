@@ -18,7 +18,7 @@ def gold():
 class OracleScan:
     """TEST INFRASTRUCTURE: the per-SNP moments in numpy (stands in for the GPU scan)."""
 
-    def __init__(self, X, labels=None):
+    def __init__(self, X, labels=None, device=0):
         self.X = np.asarray(X)
 
     def snp_scan(self, rows, yc):
