@@ -34,7 +34,7 @@ def validate_genotypes(data):
     if g.ndim != 2:
         raise ValueError("genotype matrix must be 2-D (animals x SNPs)")
     if g.dtype == np.int8:
-        ok = bool(np.all((g >= 0) & (g <= 2)))
+        ok = g.size == 0 or (int(g.min()) >= 0 and int(g.max()) <= 2)
         out = g
     else:
         ok = bool(np.all((g == 0) | (g == 1) | (g == 2)))
