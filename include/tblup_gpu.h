@@ -165,6 +165,15 @@ int tblup_get_profile(tblup_ctx* ctx, double* ms, int64_t* launches, double* flo
 int tblup_reset_profile(tblup_ctx* ctx);
 
 /*
+ * Workgroup trace (profiling; enabled by TBLUP_WG_TRACE=1 at tblup_ctx_create): after an
+ * evaluation, the Cholesky launches of its last chunk left one record per workgroup,
+ * 4 x uint64 {start, end, kind << 56 | I << 40 | individual, J} with s_memrealtime
+ * timestamps (100 MHz) and kind 1 diagonal tile, 2 off-diagonal tile (I, J), 3 preparation
+ * of diagonal tile I, 4 K_II build.  *n_records = records available; copies min(cap, that).
+ */
+int tblup_get_wg_trace(tblup_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n_records);
+
+/*
  * Debug / parity readback for ONE individual: runs the pipeline up to
  * `stage` (1 = GRM block K_{RT} incl. lambda on the TT diagonal,
  * 2 = after the tile Cholesky: L in the TT lower triangle) and copies the

@@ -44,6 +44,7 @@ SIGNATURES = {
     "tblup_debug_grm": (_c.c_int, [_P, _c.c_int, _I64P, _c.c_int64, _c.c_double, _c.c_int, _c.c_int, _DP, _DP]),
     "tblup_mem_info": (_c.c_int, [_P, _I64P]),
     "tblup_index_error": (_c.c_int, [_P, _P, _c.POINTER(_c.c_int)]),
+    "tblup_get_wg_trace": (_c.c_int, [_P, _c.POINTER(_c.c_uint64), _c.c_int64, _I64P]),
     "tblup_decode_topk": (_c.c_int, [_P, _DP, _c.c_int64, _c.c_int64, _I64P, _I64P]),
     "tblup_decode_topk_device": (_c.c_int, [_P, _P, _c.c_int64, _c.c_int64, _c.c_int64, _P, _I64P, _P, _P]),
     "tblup_de_step": (_c.c_int, [_P, _c.c_int, _DP, _c.c_int64, _c.c_int64, _I32P, _I64P, _c.c_double, _c.c_double,

@@ -86,6 +86,10 @@ struct tblup_ctx {
   double bytes[TBLUP_N_KCLASS] = {0};
   int64_t mem_in_use = 0;
 
+  // TBLUP_WG_TRACE: per-workgroup start/end records of the Cholesky launches of the last chunk
+  bool wg_trace = false;
+  DevBuf wgt;
+  int64_t wgt_used = 0;
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
   int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
 };
@@ -289,8 +293,18 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
                 (const double*)sp.ymu.p, panel, pstride, d_off,
                 (const int8_t*)sp.geno.p, d_idx, d.nRp, (const uint8_t*)sp.gpk.p, d.nRp / 4, u, scal,
-                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0)};
+                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr};
   const double T3 = (double)TILE * TILE * TILE;
+  // profiling only: room for one record per Cholesky workgroup of this chunk
+  uint64_t* wgt = nullptr;
+  if (c->wg_trace) {
+    int64_t nwg = 0;
+    for (int J = 0; J < sd.NT; ++J) nwg += B + offdiag_grid(B, sd.NT, J);
+    if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
+    HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
+    wgt = (uint64_t*)c->wgt.p;
+    c->wgt_used = 0;
+  }
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
   const double cbar = (sd.form == FORM_PRIMAL) ? (double)d.nT : kbar;   // contraction length
   {
@@ -311,6 +325,10 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     // forward-substitution GEMV (the int8 GRM tiles are counted under KC_GRM)
     const double fd = Bd * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
     const double bd = Bd * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
+    if (wgt) {
+      cl.wgt = wgt + c->wgt_used * WGT_REC;
+      c->wgt_used += B;
+    }
     rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, s); });
     if (rc) return rc;
     const int nI = sd.NT - J - 1;
@@ -319,6 +337,10 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       // plus the preparation of diagonal tile J+1: 128^3 per L < J (lower half stored)
       const double fo = Bd * nI * (2.0 * T3 * jt + T3) + Bd * T3 * jt;
       const double bo = Bd * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * Bd * TILE * TILE * jt * 8.0;
+      if (wgt) {
+        cl.wgt = wgt + c->wgt_used * WGT_REC;
+        c->wgt_used += offdiag_grid(B, sd.NT, J);
+      }
       rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(cl, J, s); });
       if (rc) return rc;
     }
@@ -382,6 +404,8 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
   const char* dbg = getenv("TBLUP_DBG_SKIP");
   c->dbg_skip = dbg ? atoi(dbg) : 0;
+  const char* wt = getenv("TBLUP_WG_TRACE");
+  c->wg_trace = wt && atoi(wt) != 0;
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   if (!panel) {
@@ -430,6 +454,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->idx_err.release();
   c->scratch.release();
   c->ws.release();
+  c->wgt.release();
   c->dec_keys.release();
   c->dec_idx.release();
   c->de_polys.release();
@@ -934,6 +959,20 @@ int tblup_de_step(tblup_ctx* c, int strategy, const double* parents, int64_t pop
                                     clip_hi, mt_key, mt_pos, (double*)c->de_chi.p, L, nullptr))
     return rc;
   HIPCHK(hipMemcpy(children, c->de_chi.p, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tblup_get_wg_trace(tblup_ctx* c, uint64_t* out, int64_t cap, int64_t* n_records) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (!n_records) return fail(TBLUP_ERR_ARG, "null n_records");
+  *n_records = c->wg_trace ? c->wgt_used : 0;
+  if (!c->wg_trace || !out || cap <= 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipDeviceSynchronize());
+  const int64_t n = std::min(cap, c->wgt_used);
+  HIPCHK(hipMemcpy(out, c->wgt.p, (size_t)n * WGT_REC * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -185,6 +185,30 @@ struct CholArgs {
   int nt;                   // traits (right-hand sides)
   int NT, J;
   int skip;                 // diagnostic ablation mask (TBLUP_DBG_SKIP); 0 in production
+  uint64_t* wgt;            // workgroup trace records (TBLUP_WG_TRACE), null in production
+};
+
+// Profiling only: workgroup start / end timestamps (s_memrealtime, 100 MHz) of a launch.
+struct WgTrace {
+  uint64_t* rec;
+  uint64_t t0;
+  __device__ __forceinline__ explicit WgTrace(uint64_t* base) : rec(nullptr), t0(0) {
+    if (base) {
+      rec = base + (int64_t)blockIdx.x * WGT_REC;
+      t0 = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __device__ __forceinline__ void done(int kind, int J, int I, int64_t b) {
+    if (!rec) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+      rec[0] = t0;
+      rec[1] = t1;
+      rec[2] = ((uint64_t)kind << 56) | ((uint64_t)I << 40) | (uint64_t)b;
+      rec[3] = (uint64_t)J;
+    }
+  }
 };
 
 // Address of system row r's contraction block 0 for individual b: the gathered panel
@@ -748,8 +772,11 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
   __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
   __shared__ double rsh[MAXT][TILE];
+  WgTrace tr(a.wgt);
   // individual b on the XCD that runs its off-diagonal tiles (same L2 for L, S, X, w)
-  diag_tile(a, xcd_remap(blockIdx.x, gridDim.x), a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  diag_tile(a, b, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
+  tr.done(WGT_DIAG, a.J, a.J, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -950,18 +977,23 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, int I0, int
   __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
   const int64_t n_extra = (int64_t)gridDim.x - n_tiles - n_kd;
   const int64_t bid = blockIdx.x;
+  WgTrace tr(a.wgt);
   if (bid < n_extra) {
-    syrk_partial8(a, xcd_remap(bid, n_extra), a.J + 1, a.J, lds);
+    const int64_t b = xcd_remap(bid, n_extra);
+    syrk_partial8(a, b, a.J + 1, a.J, lds);
+    tr.done(WGT_PREP, a.J, a.J + 1, b);
     return;
   }
   if (bid >= n_extra + n_tiles) {   // column 0 only: K_JJ for J >= 2
     const int64_t lg = xcd_remap(bid - n_extra - n_tiles, n_kd);
     const int nJ = a.NT - 2;
     diag_grm_tile(a, lg / nJ, 2 + (int)(lg % nJ), reinterpret_cast<uint8_t*>(lds), uj_sh);
+    tr.done(WGT_KJJ, a.J, 2 + (int)(lg % nJ), lg / nJ);
     return;
   }
   const int64_t logical = xcd_remap(bid - n_extra, n_tiles);
   offdiag_tile(a, logical / nI, I0 + (int)(logical % nI), lds, uj_sh, ui_sh, zj_sh);
+  tr.done(WGT_TILE, a.J, I0 + (int)(logical % nI), logical / nI);
 }
 
 __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a, int nJ) {
@@ -973,7 +1005,7 @@ __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a, int nJ) {
 
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip, nullptr};
   const int nJ = std::min(c.sd.NT, 2);
   hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * nJ)), dim3(OTH), 0, s, a, nJ);
   return hipGetLastError();
@@ -981,20 +1013,20 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
 
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt};
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt};
   const int I0 = J + 1, nI = c.sd.NT - I0;
   if (nI <= 0) return hipSuccess;
   a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;
   const int64_t n_tiles = c.B * nI;
   const int64_t n_kd = (J == 0 && c.sd.NT > 2) ? c.B * (c.sd.NT - 2) : 0;
-  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)(n_tiles + c.B * a.NSX + n_kd)), dim3(OTH), 0, s, a, I0, nI,
+  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)offdiag_grid(c.B, c.sd.NT, J)), dim3(OTH), 0, s, a, I0, nI,
                      n_tiles, n_kd);
   return hipGetLastError();
 }

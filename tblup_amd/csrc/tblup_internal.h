@@ -146,7 +146,20 @@ struct CholLaunch {
   const double* u;       // [B][prow]
   const double* scal;    // [B][SCAL]
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
+  uint64_t* wgt;         // per-workgroup timestamp records of this launch (env TBLUP_WG_TRACE), else null
 };
+// workgroup trace record (profiling only): {start, end, kind << 56 | I << 40 | b, J},
+// s_memrealtime ticks (100 MHz); kinds below
+constexpr int WGT_REC = 4;
+enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4 };
+// workgroups launched by launch_chol_offdiag for column J (also the trace stride)
+inline int64_t offdiag_grid(int64_t B, int NT, int J) {
+  const int nI = NT - J - 1;
+  if (nI <= 0) return 0;
+  const int nsx = (J >= 1 && J + 1 < NT) ? 1 : 0;
+  const int64_t n_kd = (J == 0 && NT > 2) ? B * (NT - 2) : 0;
+  return B * nI + B * nsx + n_kd;
+}
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
 // then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s);

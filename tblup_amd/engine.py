@@ -261,6 +261,25 @@ class GpuBlupEngine:
         return {name: {"ms": float(ms[i]), "launches": int(la[i]), "flops": float(fl[i]), "bytes": float(by[i])}
                 for i, name in enumerate(_native.KCLASS_NAMES)}
 
+    def wg_trace(self):
+        """Per-workgroup records of the last evaluation's Cholesky launches (TBLUP_WG_TRACE=1):
+        structured array (start, end [s], kind, J, I, b)."""
+        n = ctypes.c_int64(0)
+        _native.check("tblup_get_wg_trace", self._lib.tblup_get_wg_trace(self._ctx, None, 0, ctypes.byref(n)))
+        raw = np.zeros((n.value, 4), dtype=np.uint64)
+        if n.value:
+            _native.check("tblup_get_wg_trace", self._lib.tblup_get_wg_trace(
+                self._ctx, raw.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n.value, ctypes.byref(n)))
+        out = np.zeros(len(raw), dtype=[("start", "f8"), ("end", "f8"), ("kind", "i4"), ("J", "i4"), ("I", "i4"),
+                                        ("b", "i8")])
+        out["start"] = raw[:, 0] / 1e8
+        out["end"] = raw[:, 1] / 1e8
+        out["kind"] = (raw[:, 2] >> np.uint64(56)).astype(np.int32)
+        out["I"] = ((raw[:, 2] >> np.uint64(40)) & np.uint64(0xFFFF)).astype(np.int32)
+        out["b"] = (raw[:, 2] & np.uint64((1 << 40) - 1)).astype(np.int64)
+        out["J"] = raw[:, 3].astype(np.int32)
+        return out
+
     def mem_in_use(self):
         v = ctypes.c_int64(0)
         _native.check("tblup_mem_info", self._lib.tblup_mem_info(self._ctx, ctypes.byref(v)))

@@ -1,0 +1,81 @@
+"""Per-workgroup timeline of one config-2 evaluation step (TBLUP_WG_TRACE=1).
+
+For every Cholesky launch: makespan, workgroups by kind with their mean / max duration,
+slot utilisation (sum of workgroup time / (resident slots x makespan); the off-diagonal
+kernel fits 2 workgroups per CU, the diagonal 1), the time the first / last workgroup
+starts, and the gap to the previous launch.  Writes the raw records to an .npy for later
+analysis.   usage: python tools/wg_trace.py [out.npy] [--pop N]
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["TBLUP_WG_TRACE"] = "1"
+
+import bench  # noqa: E402
+
+KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj"}
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "gpurun_out/wg_trace.npy"
+    pop = int(sys.argv[sys.argv.index("--pop") + 1]) if "--pop" in sys.argv else 256
+    import torch
+    from tblup_amd.engine import GpuBlupEngine, concat_genomes
+    cfg = bench.CONFIGS["config2"]
+    geno, pheno, T, V, genomes, _ = bench.make_workload(cfg, 1234, 0, pop)
+    eng = GpuBlupEngine(geno, pheno, device=0)
+    sid = eng.split_id(T, V)
+    idx, off = concat_genomes(list(genomes))
+    d_idx, d_off = torch.from_numpy(idx).cuda(), torch.from_numpy(off).cuda()
+    d_fit = torch.empty(pop, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(4):
+        eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(), stream_ptr=s.cuda_stream)
+    torch.cuda.synchronize()
+    rec = eng.wg_trace()
+    np.save(out, rec)
+    props = torch.cuda.get_device_properties(0)
+    cus = props.multi_processor_count
+    t0 = rec["start"].min()
+    prev_end = None
+    tot = 0.0
+    print(f"{len(rec)} workgroups, {cus} CUs")
+    launches = []
+    for J in sorted(set(rec["J"].tolist())):
+        for is_diag in (True, False):
+            m = (rec["J"] == J) & ((rec["kind"] == 1) == is_diag)
+            if not m.any():
+                continue
+            launches.append((rec[m]["start"].min(), J, is_diag, m))
+    launches.sort(key=lambda x: x[0])
+    for st, J, is_diag, m in launches:
+        r = rec[m]
+        en = r["end"].max()
+        span = en - st
+        slots = cus * (1 if is_diag else 2)
+        util = float(np.sum(r["end"] - r["start"]) / (slots * span))
+        gap = 0.0 if prev_end is None else st - prev_end
+        prev_end = en
+        tot += span
+        parts = []
+        for k in sorted(set(r["kind"].tolist())):
+            rk = r[r["kind"] == k]
+            d = (rk["end"] - rk["start"]) * 1e6
+            parts.append(f"{KIND[k]} n={len(rk)} mean={d.mean():.1f} max={d.max():.1f} us "
+                         f"last-start=+{(rk['start'].max() - st) * 1e6:.1f}")
+        first_tile = ""
+        if not is_diag:
+            nxt = r[(r["kind"] == 2) & (r["I"] == J + 1)]
+            if len(nxt):
+                first_tile = f" tile(J+1,J) done by +{(nxt['end'].max() - st) * 1e6:.1f}"
+        print(f"{'diag' if is_diag else 'off '} J={J}: start +{(st - t0) * 1e6:8.1f} span {span * 1e6:7.1f} us "
+              f"gap {gap * 1e6:5.1f} util {util:.2f}{first_tile} | " + "; ".join(parts))
+    print(f"sum of launch spans {tot * 1e6:.1f} us, first start to last end {(prev_end - t0) * 1e6:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
