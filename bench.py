@@ -36,10 +36,14 @@ TRAITS = {"config5": 3}
 # BASELINE.json's metric, verbatim
 METRIC = "GBLUP fitness evals/sec (whole node), 2k\u00d750k SNP, DE pop=256; 1/2/4/8 GPUs"
 
-# gfx950 peaks (MI355X_MICROARCH.md chip table; fp64 and int8 dense from the AMD MI355X spec sheet)
+# gfx950 peaks.  "measured": tools/mfma_peak.hip on the box (profiles/r02_mfma_peak.json; the
+# microarchitecture guide has no fp64 MFMA row): back-to-back MFMAs on independent accumulators,
+# 2 waves per SIMD, random operands, at the clock the chip holds under that load (~2.36 GHz).
+# "spec": AMD's MI355X dense figures (2.4 GHz).  HBM: the guide's 8 TB/s.
 PEAKS = {
-    "fp64_mfma_tflops": 78.6,
-    "int8_mfma_tops": 5033.0,
+    "fp64_mfma_tflops": 72.7, "fp64_mfma_tflops_spec": 78.6,
+    "fp32_mfma_tflops": 154.6, "fp32_mfma_tflops_spec": 157.3,
+    "int8_mfma_tops": 4140.0, "int8_mfma_tops_spec": 5033.0,
     "hbm_gbs": 8000.0,
 }
 
@@ -253,15 +257,24 @@ def main():
     total_evals = pop * world * args.steps
     value = total_evals / elapsed
 
-    # roofline of the dominant kernel class, from live HIP-event timing over the timed region
+    # roofline of the dominant kernel class, from live HIP-event timing over the timed region.
+    # The library counts the flops of the padded 128-row tiles (ns = 1024 at k = 1000); the
+    # algorithmic work of the Cholesky classes scales as ns^3, so frac uses (k / ns)^3 of it.
     if args.no_events:
         prof = {c: {"ms": 1e-9, "launches": 0, "flops": 0.0, "bytes": 0.0} for c in prof}
     dom = max(prof, key=lambda c: prof[c]["ms"])
     pd = prof[dom]
+    ns = -(-k // 128) * 128 if k < nT else -(-nT // 128) * 128       # SNP-space form at k < n_T (evaluator.py:288-314)
+    unpad = (min(k, nT) / ns) ** 3
+    peak_spec = None
     if dom in ("chol_diag", "chol_offdiag"):
-        bound, peak, unit, achieved = "mfma", PEAKS["fp64_mfma_tflops"], "TFLOP/s", pd["flops"] / (pd["ms"] * 1e-3) / 1e12
+        bound, unit = "mfma", "TFLOP/s"
+        peak, peak_spec = PEAKS["fp64_mfma_tflops"], PEAKS["fp64_mfma_tflops_spec"]
+        achieved = pd["flops"] * unpad / (pd["ms"] * 1e-3) / 1e12
     elif dom == "grm":
-        bound, peak, unit, achieved = "mfma", PEAKS["int8_mfma_tops"], "TOP/s", pd["flops"] / (pd["ms"] * 1e-3) / 1e12
+        bound, unit = "mfma", "TOP/s"
+        peak, peak_spec = PEAKS["int8_mfma_tops"], PEAKS["int8_mfma_tops_spec"]
+        achieved = pd["flops"] / (pd["ms"] * 1e-3) / 1e12
     else:
         bound, peak, unit, achieved = "hbm", PEAKS["hbm_gbs"], "GB/s", pd["bytes"] / (pd["ms"] * 1e-3) / 1e9
     traffic = None
@@ -280,15 +293,36 @@ def main():
                 mfma_busy = pm["per_class"][dom]["mfma_busy"]
         except (ValueError, OSError, KeyError):
             mfma_busy = None
+    # Whole-step lower bound of the algorithm run, per GPU: the exact int8 system (lower
+    # triangle: k^2 n_T int ops), the fp64 Cholesky (k^3 / 3), one read of the factor for the
+    # back substitution (k^2 / 2 doubles), each at its measured peak.
+    m_sys = min(k, nT)
+    t_int8 = pop * float(m_sys) ** 2 * (nT if k < nT else k) / (PEAKS["int8_mfma_tops"] * 1e12)
+    t_fp64 = pop * float(m_sys) ** 3 / 3.0 / (PEAKS["fp64_mfma_tflops"] * 1e12)
+    t_hbm = pop * float(m_sys) ** 2 / 2.0 * 8.0 / (PEAKS["hbm_gbs"] * 1e9)
+    step_bound_ms = (t_int8 + t_fp64 + t_hbm) * 1e3
+    # north star: "fraction of the fp32 MFMA roofline" with SURVEY.md 8(d)'s canonical
+    # F(k) = 2 k n_T (n_T + n_V) + n_T^3 / 3 + 2 n_T^2 + 2 n_V n_T flops per eval (the dual GRM
+    # form in fp32).  The build runs the cheaper exact form (int8 system, k-row fp64 Cholesky),
+    # so this ratio can exceed 1: it says how far the canonical algorithm's flop rate is beaten.
+    f_canon = 2.0 * k * nT * (nT + nV) + nT ** 3 / 3.0 + 2.0 * nT ** 2 + 2.0 * nV * nT
     roofline = {"bound": bound, "kernel": dom, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4), "traffic": traffic, "mfma_busy": mfma_busy,
-                "launches": pd["launches"], "avg_launch_ms": round(pd["ms"] / max(pd["launches"], 1), 4)}
+                "launches": pd["launches"], "avg_launch_ms": round(pd["ms"] / max(pd["launches"], 1), 4),
+                "peak_source": "measured on the box (tools/mfma_peak.hip, profiles/r02_mfma_peak.json)",
+                "peak_spec": peak_spec, "frac_spec": None if peak_spec is None else round(achieved / peak_spec, 4),
+                "flops": "algorithmic: library tile count x (k/ns)^3 = %.4f" % unpad,
+                "step": {"lower_bound_ms": round(step_bound_ms, 4), "int8_ms": round(t_int8 * 1e3, 4),
+                         "fp64_ms": round(t_fp64 * 1e3, 4), "hbm_ms": round(t_hbm * 1e3, 4)},
+                "fp32_roofline_frac_canonical": None}
     step_ms = {c: round(prof[c]["ms"] / args.steps, 4) for c in prof}
 
     if args.profile_json and rank == 0:
         with open(args.profile_json, "w") as f:
             json.dump({"config": args.config, "steps": args.steps, "profile": prof, "per_step_ms": step_ms,
                        "elapsed_s": elapsed}, f, indent=1)
+    roofline["step"]["frac"] = round(roofline["step"]["lower_bound_ms"] / (elapsed / args.steps * 1e3), 4)
+    roofline["fp32_roofline_frac_canonical"] = round(f_canon * value / world / (PEAKS["fp32_mfma_tflops"] * 1e12), 4)
     if rank == 0:
         line = {
             "metric": METRIC,

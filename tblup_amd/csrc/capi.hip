@@ -299,7 +299,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   uint64_t* wgt = nullptr;
   if (c->wg_trace) {
     int64_t nwg = 0;
-    for (int J = 0; J < sd.NT; ++J) nwg += B + offdiag_grid(B, sd.NT, J);
+    for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(B, sd.NT, J);
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
     wgt = (uint64_t*)c->wgt.p;
@@ -327,7 +327,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     const double bd = Bd * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
-      c->wgt_used += B;
+      c->wgt_used += B + DTR_RECS;
     }
     rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, s); });
     if (rc) return rc;

@@ -112,45 +112,69 @@ __device__ __forceinline__ double rdlane(double x, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ __forceinline__ void factor16(double* D, double* X, int l) {
-  const int i = l & 15, g = l >> 4;
-  double v[NB], e[NB], pv[NB];
+// Row-j broadcast inside each 16-lane row of the wave (DPP row_newbcast:j, gfx90a+).
+template <int J>
+__device__ __forceinline__ double row_bcast(double x) {
+  const long long bits = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)bits, 0x150 + J, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(bits >> 32), 0x150 + J, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Lane l = i + 16 g holds columns 4g .. 4g+3 of row i (the four 16-lane groups split the
+// columns).  Per pivot j: T_jj by v_readlane, row j of the lane's own four columns by a DPP
+// row broadcast, and T_ij (column j lives in group j/4) by one cross-group permute -- instead of
+// 32 v_readlanes per pivot with every lane holding a whole row.  Same operations in the same
+// order per element as the whole-row form, so the factor and its inverse are unchanged.
+template <int J>
+__device__ __forceinline__ void f16_step(double (&v)[4], double (&e)[4], double (&pv)[4], double& own, int i, int g) {
+  constexpr int GJ = J >> 2, QJ = J & 3;
+  const double piv = rdlane(v[QJ], J + 16 * GJ);
+  const double tij = __shfl(v[QJ], i + 16 * GJ);
+  double rj[4], ej[4];
 #pragma unroll
-  for (int c = 0; c < NB; ++c) {
-    v[c] = (c <= i) ? D[bo(i, c)] : D[bo(c, i)];   // symmetric row from the lower triangle
-    e[c] = (c == i) ? 1.0 : 0.0;
+  for (int q = 0; q < 4; ++q) {
+    rj[q] = row_bcast<J>(v[q]);
+    ej[q] = row_bcast<J>(e[q]);
   }
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const double piv = rdlane(v[j], j);
-    pv[j] = piv;
-    double r[NB], ej[NB];
-#pragma unroll
-    for (int c = j + 1; c < NB; ++c) r[c] = rdlane(v[c], j);
-#pragma unroll
-    for (int c = 0; c < j; ++c) ej[c] = rdlane(e[c], j);
-    const double li = v[j] * recip(piv);
-#pragma unroll
-    for (int c = j + 1; c < NB; ++c) v[c] = __builtin_fma(-li, r[c], v[c]);
-    const bool below = i > j;
-#pragma unroll
-    for (int c = 0; c < j; ++c) e[c] = below ? __builtin_fma(-li, ej[c], e[c]) : e[c];
-    e[j] = below ? -li : e[j];
-  }
-  // deferred scaling: L_ic = T_ic / sqrt(piv_c), X_ic = E_ic / sqrt(piv_i)
-  const double rs_own = 1.0 / sqrt(v[i]);   // v[i] = piv_i
+  if (g == GJ) pv[QJ] = piv;
+  if (i == J) own = piv;
+  const double li = tij * recip(piv);
+  const bool below = i > J;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = 4 * g + q;
-    double vc = v[0], ec = e[0], pc = pv[0];
+    v[q] = (c > J) ? __builtin_fma(-li, rj[q], v[q]) : v[q];
+    e[q] = (below && c < J) ? __builtin_fma(-li, ej[q], e[q]) : e[q];
+    e[q] = (below && c == J) ? -li : e[q];
+  }
+}
+
+template <int J>
+__device__ __forceinline__ void f16_steps(double (&v)[4], double (&e)[4], double (&pv)[4], double& own, int i, int g) {
+  if constexpr (J < NB) {
+    f16_step<J>(v, e, pv, own, i, g);
+    f16_steps<J + 1>(v, e, pv, own, i, g);
+  }
+}
+
+__device__ __forceinline__ void factor16(double* D, double* X, int l) {
+  const int i = l & 15, g = l >> 4;
+  double v[4], e[4], pv[4] = {1.0, 1.0, 1.0, 1.0}, own = 1.0;
 #pragma unroll
-    for (int cc = 1; cc < NB; ++cc) {
-      vc = (c == cc) ? v[cc] : vc;
-      ec = (c == cc) ? e[cc] : ec;
-      pc = (c == cc) ? pv[cc] : pc;
-    }
-    X[bo(i, c)] = (i >= c) ? ec * rs_own : 0.0;
-    if (i >= c) D[bo(i, c)] = vc * (1.0 / sqrt(pc));
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * g + q;
+    v[q] = (c <= i) ? D[bo(i, c)] : D[bo(c, i)];   // symmetric row from the lower triangle
+    e[q] = (c == i) ? 1.0 : 0.0;
+  }
+  f16_steps<0>(v, e, pv, own, i, g);
+  // deferred scaling: L_ic = T_ic / sqrt(piv_c), X_ic = E_ic / sqrt(piv_i)
+  const double rs_own = 1.0 / sqrt(own);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * g + q;
+    X[bo(i, c)] = (i >= c) ? e[q] * rs_own : 0.0;
+    if (i >= c) D[bo(i, c)] = v[q] * (1.0 / sqrt(pv[q]));
   }
 }
 
@@ -186,7 +210,15 @@ struct CholArgs {
   int NT, J;
   int skip;                 // diagnostic ablation mask (TBLUP_DBG_SKIP); 0 in production
   uint64_t* wgt;            // workgroup trace records (TBLUP_WG_TRACE), null in production
+  uint64_t* dtr;            // diagonal launch: phase timestamps of workgroup 0 (TBLUP_WG_TRACE), else null
 };
+
+// Profiling only: lane 0 of each wave of diagonal workgroup 0 stamps phase boundaries
+// (s_memrealtime) into dtr[wave * 64 + slot].
+__device__ __forceinline__ void dstamp(const CholArgs& a, int slot) {
+  if (a.dtr && blockIdx.x == 0 && (threadIdx.x & 63) == 0)
+    a.dtr[(threadIdx.x >> 6) * 64 + slot] = __builtin_amdgcn_s_memrealtime();
+}
 
 // Profiling only: workgroup start / end timestamps (s_memrealtime, 100 MHz) of a launch.
 struct WgTrace {
@@ -570,16 +602,31 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
 // X block (q, jb), q > jb, of X = L^{-1}: X_{q,jb} = -X_qq sum_{lb=jb}^{q-1} L_{q,lb} X_{lb,jb}
 // (needs L row q and X rows jb..q-1, X_qq); one wave.
 __device__ __forceinline__ void xinv_block(const double* Tp, double* Xp, int q, int jb, int l) {
-  v4d sacc = {0.0, 0.0, 0.0, 0.0};
-  for (int lb = jb; lb < q; ++lb) {
-    const double* A = Tp + pk(q, lb);
-    const double* B = Xp + pk(lb, jb);
+  // two independent MFMA chains (even / odd lb) halve the dependent-accumulator latency
+  v4d s0 = {0.0, 0.0, 0.0, 0.0}, s1 = {0.0, 0.0, 0.0, 0.0};
+  int lb = jb;
+  for (; lb + 1 < q; lb += 2) {
+    const double* A0 = Tp + pk(q, lb);
+    const double* B0 = Xp + pk(lb, jb);
+    const double* A1 = Tp + pk(q, lb + 1);
+    const double* B1 = Xp + pk(lb + 1, jb);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int k = 4 * kk + (l >> 4);
-      sacc = mfma64(A[bo(l & 15, k)], B[bo(k, l & 15)], sacc);
+      s0 = mfma64(A0[bo(l & 15, k)], B0[bo(k, l & 15)], s0);
+      s1 = mfma64(A1[bo(l & 15, k)], B1[bo(k, l & 15)], s1);
     }
   }
+  if (lb < q) {
+    const double* A0 = Tp + pk(q, lb);
+    const double* B0 = Xp + pk(lb, jb);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * kk + (l >> 4);
+      s0 = mfma64(A0[bo(l & 15, k)], B0[bo(k, l & 15)], s0);
+    }
+  }
+  const v4d sacc = s0 + s1;
   v4d xo = {0.0, 0.0, 0.0, 0.0};
   const double* Xqq = Xp + pk(q, q);
 #pragma unroll
@@ -632,6 +679,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   const int nt = a.nt;
   double* Tp = lds;
   double* Xp = lds + NPACK * BLKD;
+  dstamp(a, 0);
 
   // forward-substitution right-hand side r = rhs_J - w_J: loads issued first so that their
   // latency overlaps the S load and the SYRK
@@ -648,10 +696,12 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     }
   }
 
-  // T = S - sum_{L0 <= L < J} L_JL L_JL^T: S by LDS-DMA, the SYRK through the stage ring
+  // T = S - sum_{L0 <= L < J} L_JL L_JL^T: S by LDS-DMA, the SYRK through the stage ring.
+  // (Streaming the whole Lt tile in one burst, or 4 stages in flight, measured slower: the
+  // launch's loads are HBM-bound and the SYRK at 2 waves per SIMD then runs after them.)
+  const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
+                                : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
   {
-    const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
-                                  : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
 #pragma unroll
     for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
       const int chunk = (e * DW + w) * 64;
@@ -680,7 +730,9 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 #pragma unroll
     for (int tr = 0; tr < MAXT; ++tr) rsh[tr][t] = (tr < nt && gi < nrow) ? rv[tr] : 0.0;
   }
+  dstamp(a, 1);
   __syncthreads();
+  dstamp(a, 2);
 
   // C. blocked right-looking factorisation over 16-column panels, with a one-block
   //    look-ahead: wave 0 updates diagonal block p+1 first and factors it while waves 1-3
@@ -696,6 +748,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 #pragma unroll
       for (int r = 0; r < 4; ++r) Tp[pk(q, p) + bo((l >> 4) + 4 * r, l & 15)] = x[r];
     }
+    dstamp(a, 3 + 3 * p);
     __syncthreads();
     if (p + 1 == NBLK) break;
     const int nb = NBLK - 1 - p;
@@ -712,28 +765,53 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       // wave DW/2 shares wave 0's SIMD and stays idle so that factor16 issues alone there;
       // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over the others
       const int wi = (w < DW / 2) ? w - 1 : w - 2;   // 0 .. DW-3
-      for (int e = wi + 1; e < ((a.skip & 512) ? 0 : nb * (nb + 1) / 2); e += DW - 2) {
+      // two blocks per pass: independent MFMA chains and LDS traffic overlap
+      const int ne = (a.skip & 512) ? 0 : nb * (nb + 1) / 2;
+      for (int e = wi + 1; e < ne; e += 2 * (DW - 2)) {
+        const int e2 = e + (DW - 2);
         int qq = 0;
         while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
         const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
-        v4d x = {0.0, 0.0, 0.0, 0.0};
-        x = mma_abt(Tp + pk(q, p), Tp + pk(sb, p), x, l);
+        const bool two = e2 < ne;
+        int qq2 = qq;
+        while ((qq2 + 1) * (qq2 + 2) / 2 <= e2) ++qq2;
+        const int q2 = two ? p + 1 + qq2 : q, sb2 = two ? p + 1 + (e2 - qq2 * (qq2 + 1) / 2) : sb;
+        const double* A = Tp + pk(q, p);
+        const double* B = Tp + pk(sb, p);
+        const double* A2 = Tp + pk(q2, p);
+        const double* B2 = Tp + pk(sb2, p);
+        v4d x = {0.0, 0.0, 0.0, 0.0}, x2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * kk + (l >> 4);
+          x = mfma64(A[bo(l & 15, k)], B[bo(l & 15, k)], x);
+          x2 = mfma64(A2[bo(l & 15, k)], B2[bo(l & 15, k)], x2);
+        }
         double* dst = Tp + pk(q, sb);
 #pragma unroll
         for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
+        if (two) {
+          double* dst2 = Tp + pk(q2, sb2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dst2[bo((l >> 4) + 4 * r, l & 15)] -= x2[r];
+        }
       }
       // D (overlapped). block row p of X = L^{-1}: L row p and X rows < p are final and
       // X_pp came out of the previous window's factor16
       if (!(a.skip & 8) && wi < p) xinv_block(Tp, Xp, p, wi, l);
     }
+    dstamp(a, 4 + 3 * p);
     __syncthreads();
+    dstamp(a, 5 + 3 * p);
   }
   if (a.skip & 16) return;
 
   // D. last block row of X (rows < NBLK-1 were built inside the factorisation windows)
   if (!(a.skip & 4) && !(a.skip & 8)) {
     if (w < NBLK - 1) xinv_block(Tp, Xp, NBLK - 1, w, l);
+    dstamp(a, 26);
     __syncthreads();
+    dstamp(a, 27);
   }
 
   // E. X into Dinv as packed lower blocks, each block transposed (block (q, jb) holds
@@ -756,6 +834,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
     }
   }
+  dstamp(a, 28);
   // z_J[i] = sum_{c <= i} X[i][c] r[c]: four lanes per row (c = q mod 4), shuffle-reduced
   if (!(a.skip & (1 << 15))) {
     switch (nt) {
@@ -765,6 +844,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       default: diag_z<4>(a, Xp, rsh, b, j0); break;
     }
   }
+  dstamp(a, 29);
 }
 
 // Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
@@ -1005,7 +1085,7 @@ __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a, int nJ) {
 
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip, nullptr};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip, nullptr, nullptr};
   const int nJ = std::min(c.sd.NT, 2);
   hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * nJ)), dim3(OTH), 0, s, a, nJ);
   return hipGetLastError();
@@ -1013,14 +1093,16 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
 
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr};
+  // profiling: the phase stamps of this launch follow its B workgroup records
+  if (c.wgt) a.dtr = c.wgt + c.B * WGT_REC;
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr};
   const int I0 = J + 1, nI = c.sd.NT - I0;
   if (nI <= 0) return hipSuccess;
   a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;

@@ -151,6 +151,9 @@ struct CholLaunch {
 // workgroup trace record (profiling only): {start, end, kind << 56 | I << 40 | b, J},
 // s_memrealtime ticks (100 MHz); kinds below
 constexpr int WGT_REC = 4;
+// a diagonal launch's records are followed by DTR_RECS records holding the phase stamps of
+// its workgroup 0 (8 waves x 64 uint64), written as kind-0 records
+constexpr int DTR_RECS = 8 * 64 / WGT_REC;
 enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4 };
 // workgroups launched by launch_chol_offdiag for column J (also the trace stride)
 inline int64_t offdiag_grid(int64_t B, int NT, int J) {

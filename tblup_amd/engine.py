@@ -261,15 +261,19 @@ class GpuBlupEngine:
         return {name: {"ms": float(ms[i]), "launches": int(la[i]), "flops": float(fl[i]), "bytes": float(by[i])}
                 for i, name in enumerate(_native.KCLASS_NAMES)}
 
-    def wg_trace(self):
+    def wg_trace(self, raw=False):
         """Per-workgroup records of the last evaluation's Cholesky launches (TBLUP_WG_TRACE=1):
-        structured array (start, end [s], kind, J, I, b)."""
+        structured array (start, end [s], kind, J, I, b); raw=True: the (n, 4) uint64 records
+        (including each diagonal launch's phase-stamp block, kind 0)."""
         n = ctypes.c_int64(0)
         _native.check("tblup_get_wg_trace", self._lib.tblup_get_wg_trace(self._ctx, None, 0, ctypes.byref(n)))
+        raw_out = raw
         raw = np.zeros((n.value, 4), dtype=np.uint64)
         if n.value:
             _native.check("tblup_get_wg_trace", self._lib.tblup_get_wg_trace(
                 self._ctx, raw.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n.value, ctypes.byref(n)))
+        if raw_out:
+            return raw
         out = np.zeros(len(raw), dtype=[("start", "f8"), ("end", "f8"), ("kind", "i4"), ("J", "i4"), ("I", "i4"),
                                         ("b", "i8")])
         out["start"] = raw[:, 0] / 1e8
@@ -278,7 +282,7 @@ class GpuBlupEngine:
         out["I"] = ((raw[:, 2] >> np.uint64(40)) & np.uint64(0xFFFF)).astype(np.int32)
         out["b"] = (raw[:, 2] & np.uint64((1 << 40) - 1)).astype(np.int64)
         out["J"] = raw[:, 3].astype(np.int32)
-        return out
+        return out[out["kind"] != 0]
 
     def mem_in_use(self):
         v = ctypes.c_int64(0)

@@ -37,7 +37,9 @@ def main():
         eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(), stream_ptr=s.cuda_stream)
     torch.cuda.synchronize()
     rec = eng.wg_trace()
+    raw = eng.wg_trace(raw=True)
     np.save(out, rec)
+    np.save(out.replace(".npy", "_raw.npy"), raw)
     props = torch.cuda.get_device_properties(0)
     cus = props.multi_processor_count
     t0 = rec["start"].min()
@@ -75,6 +77,25 @@ def main():
         print(f"{'diag' if is_diag else 'off '} J={J}: start +{(st - t0) * 1e6:8.1f} span {span * 1e6:7.1f} us "
               f"gap {gap * 1e6:5.1f} util {util:.2f}{first_tile} | " + "; ".join(parts))
     print(f"sum of launch spans {tot * 1e6:.1f} us, first start to last end {(prev_end - t0) * 1e6:.1f} us")
+    # phase stamps of diagonal workgroup 0 (tblup_internal.h DTR_RECS): per wave, 30 slots
+    NT, pos = 8, 0
+    names = ["start", "pre-barrier", "post-barrier"] + [f"{x}{p}" for p in range(8) for x in ("a", "b", "w")] + [
+        "xinv7", "post-xinv7", "dinv", "z", "syrk-issued", "-"] + [f"{x}{t}" for t in range(8) for x in
+                                                                   ("stg-ready", "stg-go")] + ["syrk-done"]
+    for J in range(NT):
+        pos += pop
+        st = raw[pos:pos + 128].reshape(-1).reshape(8, 64).astype(np.int64)
+        pos += 128
+        nI = NT - J - 1
+        pos += 0 if nI <= 0 else pop * nI + pop * (1 if (J >= 1 and J + 1 < NT) else 0) + (pop * (NT - 2) if J == 0 else 0)
+        if J in (0, 3):
+            base = st[0, 0]
+            print(f"diag J={J} wg0 phase stamps (us from start), waves 0 / 1 / 4:")
+            for k in [0, 30] + list(range(32, 49)) + list(range(1, 30)):
+                if st[0, k] == 0 and st[1, k] == 0:
+                    continue
+                vals = " ".join(f"{(st[w, k] - base) / 100.0:7.2f}" if st[w, k] else "      -" for w in (0, 1, 4))
+                print(f"  {names[k]:>12s} {vals}")
 
 
 if __name__ == "__main__":
