@@ -173,6 +173,17 @@ struct Carve {
   }
 };
 
+// SNP (primal) form: the batched system-tile launch (k_sys_tiles) builds every exact tile up
+// front; int16 counts stay exact while n_T <= KC_MAX_NT.  TBLUP_SYS_TILES=0 keeps the in-tile
+// int8 path (A/B timing).
+bool sys_tiles(const EvalDims& d, const SysDims& sd) {
+  static const int env = [] {
+    const char* e = getenv("TBLUP_SYS_TILES");
+    return e ? atoi(e) : 1;
+  }();
+  return env != 0 && sd.form == FORM_PRIMAL && d.nT <= KC_MAX_NT && sd.NT >= 2;
+}
+
 size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k, bool with_ebv) {
   size_t s = 0;
   auto add = [&](size_t x) { s = (size_t)round_up((int64_t)(s + x), 256); };
@@ -186,6 +197,7 @@ size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_
   add((size_t)B * d.nt * sd.ns * 8);                            // rhs
   add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // next diagonal tile (minus its last SYRK term)
   add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
+  add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nt * d.nV * 8 : 0);              // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
@@ -264,6 +276,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* rhs = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* Sp = cv.take<double>((size_t)B * TBLUP_NSLOT * 36 * 256);
   double* Kdg = cv.take<double>((size_t)B * sd.NT * 36 * 256);
+  const bool use_st = sys_tiles(d, sd) && stop_stage != 1;
+  int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
@@ -293,13 +307,14 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
                 (const double*)sp.ymu.p, panel, pstride, d_off,
                 (const int8_t*)sp.geno.p, d_idx, d.nRp, (const uint8_t*)sp.gpk.p, d.nRp / 4, u, scal,
-                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr};
+                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb};
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
   if (c->wg_trace) {
     int64_t nwg = 0;
-    for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(B, sd.NT, J);
+    for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(B, sd.NT, J, use_st);
+    if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
     wgt = (uint64_t*)c->wgt.p;
@@ -307,7 +322,18 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   }
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
   const double cbar = (sd.form == FORM_PRIMAL) ? (double)d.nT : kbar;   // contraction length
-  {
+  if (use_st) {
+    // every system tile (I >= J) in one int8 launch: int ops 2 x 128^2 x n_T per tile
+    const double ntri = (double)sd.NT * (sd.NT + 1) / 2.0;
+    const double fg = (double)B * ntri * 2.0 * 128.0 * 128.0 * cbar;
+    const double bg = (double)B * ((ntri - sd.NT) * KC_TILE * 2.0 + sd.NT * 36 * 256 * 8.0);
+    if (wgt) {
+      cl.wgt = wgt + c->wgt_used * WGT_REC;
+      c->wgt_used += B * sd.NT * (sd.NT + 1) / 2;
+    }
+    rc = timed(c, s, KC_GRM, fg, bg, [&] { return launch_sys_tiles(cl, s); });
+    if (rc) return rc;
+  } else {
     // int ops of the diagonal GRM tiles J < 2 (J >= 2 run inside the column-0 off-diagonal launch)
     const double nJ = (double)std::min(sd.NT, 2);
     const double fg = (double)B * nJ * 128.0 * 129.0 * cbar;
@@ -339,7 +365,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       const double bo = Bd * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * Bd * TILE * TILE * jt * 8.0;
       if (wgt) {
         cl.wgt = wgt + c->wgt_used * WGT_REC;
-        c->wgt_used += offdiag_grid(B, sd.NT, J);
+        c->wgt_used += offdiag_grid(B, sd.NT, J, use_st);
       }
       rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(cl, J, s); });
       if (rc) return rc;

@@ -211,6 +211,7 @@ struct CholArgs {
   int skip;                 // diagnostic ablation mask (TBLUP_DBG_SKIP); 0 in production
   uint64_t* wgt;            // workgroup trace records (TBLUP_WG_TRACE), null in production
   uint64_t* dtr;            // diagonal launch: phase timestamps of workgroup 0 (TBLUP_WG_TRACE), else null
+  const int16_t* kc;        // SNP form: off-diagonal system-tile counts (k_sys_tiles), else null
 };
 
 // Profiling only: lane 0 of each wave of diagonal workgroup 0 stamps phase boundaries
@@ -878,6 +879,12 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   const double* sc = a.scal + b * SCAL;
   const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], sm = sc[SC_SM];
   const int64_t nrow = (int64_t)sc[SC_NROW];
+  int2 kcv[8];
+  if (a.kc) {
+    const int16_t* kt = a.kc + ((b * (NT * (NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE + w * 8 * 64 * 4;
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) kcv[cb] = *reinterpret_cast<const int2*>(kt + (cb * 64 + l) * 4);
+  }
   if (t < TILE) {
     uj_sh[t] = a.u[b * a.prow + j0 + t];
     ui_sh[t] = a.u[b * a.prow + i0 + t];
@@ -887,9 +894,27 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
   }
   __syncthreads();
 
-  // 0. K_JI on int8 MFMA (16x16x64, rows permuted so the counts land in the f64 layout)
+  // 0. K_JI: from k_sys_tiles' counts (SNP form; loads issued now, applied after GEMM1), or on
+  //    int8 MFMA here (16x16x64, rows permuted so the counts land in the f64 layout)
   v4d acc[8];
-  {
+  if (a.kc) {
+    // counts issued before the u / z loads above landed; exact ints -> fp64 K (same epilogue as
+    // the in-tile path below)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int il = 16 * w + (l & 15);
+    const bool ireal = i0 + il < nrow;
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const int32_t c4[4] = {(int32_t)(int16_t)(kcv[cb].x & 0xffff), (int32_t)(int16_t)(kcv[cb].x >> 16),
+                             (int32_t)(int16_t)(kcv[cb].y & 0xffff), (int32_t)(int16_t)(kcv[cb].y >> 16)};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cl = 16 * cb + (l >> 4) + 4 * r;
+        const double v = grm_value(c4[r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
+        acc[cb][r] = (ireal && j0 + cl < nrow) ? v : 0.0;
+      }
+    }
+  } else {
     v4i cnt[8];
     const int64_t nblk = (int64_t)sc[SC_CBLK];
     if (!(a.skip & 32) && a.form == FORM_PRIMAL) {
@@ -1076,6 +1101,156 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, int I0, int
   tr.done(WGT_TILE, a.J, I0 + (int)(logical % nI), logical / nI);
 }
 
+// ===========================================================================
+// SNP form: every system tile (I >= J) of the batch in one launch, before the column loop, on
+// int8 MFMA (C = A B^T over the n_T train animals, 2-bit packed split rows read in place).
+// 4 waves per workgroup; wave (qr, qc) computes a 64 x 64 quadrant = 4 x 4 blocks of 16x16x64,
+// so 16 MFMAs take 8 unpacked dwords (the 8-wave in-tile form: 6 per 8 -- the unpack VALU work
+// is what bounds the int8 tile); 256-animal stages through a 4-deep LDS-DMA ring (64 KiB, two
+// workgroups per CU).  A rows are read through pi(rho) so the counts land in the f64
+// accumulator layout.  Off-diagonal tiles store
+// the exact counts as int16 where the off-diagonal kernel's lanes read them (kc, see
+// tblup_internal.h); diagonal tiles store K_JJ + lambda I (identity on padding rows) as packed
+// fp64 blocks into Kd, exactly as k_diag_grm8 does.
+// ===========================================================================
+constexpr int STW = 4;   // waves per system-tile workgroup
+
+__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4i (&cnt)[4][4], int64_t b, int J, int qr, int qc,
+                                       int l);
+#define sys_diag_epilogue sys_diag_epilogue_impl
+
+__global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* kc, int ntri) {
+  constexpr int D = 3;                 // 64-B stages (256 animals) in the LDS ring (48 KiB: 3 workgroups per CU)
+  constexpr int TB = TILE * 64;        // one operand image of a stage: 8 KiB
+  __shared__ __attribute__((aligned(16))) uint8_t lds[D * 2 * TB];   // 64 KiB
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, qr = w >> 1, qc = w & 1;
+  WgTrace tr(a.wgt);
+  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
+  const int64_t b = lg / ntri;
+  const int t = (int)(lg % ntri);
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  const int J = t - I * (I + 1) / 2;
+  const bool compute = (I != J) || (qr >= qc);   // diagonal tile: the upper quadrant is never read
+  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
+  const double* sc = a.scal + b * SCAL;
+  const int64_t nblk = (int64_t)sc[SC_CBLK];
+  const int64_t nst = (nblk + 3) >> 2;
+  const int tail_ch = (int)(nblk & 3);
+  // loader: wave w fills rows 16 (2w + h) + (l >> 2), h = 0, 1, of both operand images
+  const uint8_t* sa[2];
+  const uint8_t* sb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 16 * (2 * w + h) + (l >> 2), pos = l & 3;
+    sa[h] = row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3));
+    sb[h] = row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2));
+  }
+  auto issue = [&](int64_t st) {
+    uint8_t* slot = lds + (int)(st % D) * 2 * TB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_global_load_lds(sa[h] + st * 64, (lds_ptr_t)(slot + (2 * w + h) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(sb[h] + st * 64, (lds_ptr_t)(slot + TB + (2 * w + h) * 1024), 16, 0, 0);
+    }
+  };
+  v4i cnt[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) cnt[m][n] = v4i{0, 0, 0, 0};
+  for (int64_t st = 0; st < D - 1 && st < nst; ++st) issue(st);
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  for (int64_t st = 0; st < nst; ++st) {
+    if (st + D - 2 < nst) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (st + D - 1 < nst) issue(st + D - 1);
+    if (compute) {
+      const uint8_t* As = lds + (int)(st % D) * 2 * TB;
+      const uint8_t* Bs = As + TB;
+      const bool ztail = (st == nst - 1 && tail_ch != 0 && ch >= tail_ch);   // past the training animals
+      uint4 aq[4], bq[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        aq[m] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * (4 * qr + m) + prow, ch));
+        bq[m] = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * (4 * qc + m) + rho, ch));
+        if (ztail) bq[m] = uint4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        v4i av[4], bv[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          av[m] = unpack16(s4 == 0 ? aq[m].x : s4 == 1 ? aq[m].y : s4 == 2 ? aq[m].z : aq[m].w);
+          bv[m] = unpack16(s4 == 0 ? bq[m].x : s4 == 1 ? bq[m].y : s4 == 2 ? bq[m].z : bq[m].w);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            cnt[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[m], bv[n], cnt[m][n], 0, 0, 0);
+      }
+    }
+  }
+  if (compute && I != J) {
+    int16_t* kt = kc + ((b * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int cb = 4 * qr + m, ib = 4 * qc + n;
+        const v4i c = cnt[m][n];
+        const int2 packed = {(int)((uint32_t)(c[0] & 0xffff) | ((uint32_t)c[1] << 16)),
+                             (int)((uint32_t)(c[2] & 0xffff) | ((uint32_t)c[3] << 16))};
+        *reinterpret_cast<int2*>(kt + ((ib * 8 + cb) * 64 + l) * 4) = packed;
+      }
+  } else if (compute) {
+    sys_diag_epilogue(a, cnt, b, J, qr, qc, l);
+  }
+  tr.done(WGT_SYS, J, I, b);
+}
+
+__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4i (&cnt)[4][4], int64_t b, int J, int qr, int qc,
+                                       int l) {
+  const double* sc = a.scal + b * SCAL;
+  const int64_t j0 = (int64_t)J * TILE;
+  const double sa_ = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
+  const int64_t nrow = (int64_t)sc[SC_NROW];
+  const double* ub = a.u + b * a.prow + j0;
+  double* Kd = a.Kd + (b * a.NT + J) * (int64_t)NPACK * BLKD;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cb = 4 * qr + m, ib = 4 * qc + n;
+      if (cb < ib) continue;
+      const int il = 16 * ib + (l & 15);
+      const int64_t gj = j0 + il;
+      const double uj = ub[il];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cl = 16 * cb + (l >> 4) + 4 * r;
+        const int64_t gi = j0 + cl;
+        const double kv = grm_value(cnt[m][n][r], ub[cl], uj, sa_, cN, invd, sm);
+        const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
+        Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
+      }
+    }
+}
+
+hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
+  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip,
+             c.wgt, nullptr, c.kc};
+  const int ntri = c.sd.NT * (c.sd.NT + 1) / 2;
+  hipLaunchKernelGGL(k_sys_tiles, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a, int nJ) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * TILE * 64];
   __shared__ double u_sh[TILE];
@@ -1085,7 +1260,7 @@ __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a, int nJ) {
 
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip, nullptr, nullptr};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip, nullptr, nullptr, c.kc};
   const int nJ = std::min(c.sd.NT, 2);
   hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * nJ)), dim3(OTH), 0, s, a, nJ);
   return hipGetLastError();
@@ -1093,7 +1268,7 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
 
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr, c.kc};
   // profiling: the phase stamps of this launch follow its B workgroup records
   if (c.wgt) a.dtr = c.wgt + c.B * WGT_REC;
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
@@ -1102,14 +1277,14 @@ hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
 
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr};
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr, c.kc};
   const int I0 = J + 1, nI = c.sd.NT - I0;
   if (nI <= 0) return hipSuccess;
   a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;
   const int64_t n_tiles = c.B * nI;
-  const int64_t n_kd = (J == 0 && c.sd.NT > 2) ? c.B * (c.sd.NT - 2) : 0;
-  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)offdiag_grid(c.B, c.sd.NT, J)), dim3(OTH), 0, s, a, I0, nI,
-                     n_tiles, n_kd);
+  const int64_t n_kd = (J == 0 && c.sd.NT > 2 && !c.kc) ? c.B * (c.sd.NT - 2) : 0;
+  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)offdiag_grid(c.B, c.sd.NT, J, c.kc != nullptr)), dim3(OTH), 0, s,
+                     a, I0, nI, n_tiles, n_kd);
   return hipGetLastError();
 }
 

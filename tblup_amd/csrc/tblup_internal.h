@@ -147,20 +147,26 @@ struct CholLaunch {
   const double* scal;    // [B][SCAL]
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
   uint64_t* wgt;         // per-workgroup timestamp records of this launch (env TBLUP_WG_TRACE), else null
+  int16_t* kc;           // SNP form: exact off-diagonal system-tile counts from k_sys_tiles, else null
 };
+// k_sys_tiles output: per individual NT(NT-1)/2 off-diagonal tiles (I > J, t = I(I-1)/2 + J) of
+// 128 x 128 int16 counts, in the order the off-diagonal kernel's lanes read them:
+// [column block ib][row block cb][lane][4].  Exact while n_T <= 8191 (counts <= 4 n_T).
+constexpr int64_t KC_TILE = (int64_t)TILE * TILE;
+constexpr int64_t KC_MAX_NT = 8191;
 // workgroup trace record (profiling only): {start, end, kind << 56 | I << 40 | b, J},
 // s_memrealtime ticks (100 MHz); kinds below
 constexpr int WGT_REC = 4;
 // a diagonal launch's records are followed by DTR_RECS records holding the phase stamps of
 // its workgroup 0 (8 waves x 64 uint64), written as kind-0 records
 constexpr int DTR_RECS = 8 * 64 / WGT_REC;
-enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4 };
+enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5 };
 // workgroups launched by launch_chol_offdiag for column J (also the trace stride)
-inline int64_t offdiag_grid(int64_t B, int NT, int J) {
+inline int64_t offdiag_grid(int64_t B, int NT, int J, bool sys_tiles) {
   const int nI = NT - J - 1;
   if (nI <= 0) return 0;
   const int nsx = (J >= 1 && J + 1 < NT) ? 1 : 0;
-  const int64_t n_kd = (J == 0 && NT > 2) ? B * (NT - 2) : 0;
+  const int64_t n_kd = (J == 0 && NT > 2 && !sys_tiles) ? B * (NT - 2) : 0;
   return B * nI + B * nsx + n_kd;
 }
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
@@ -169,6 +175,10 @@ hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s);
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s);
 // all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
+// SNP form: every (I >= J) system tile of the batch on int8 MFMA in one launch -- off-diagonal
+// counts into c.kc, diagonal tiles into Kd (replaces launch_diag_grm and the int8 phase of the
+// off-diagonal tiles)
+hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s);
 hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s);
 
 // ---- launcher (k_decode.hip): RandomKey genome decode, top-k of each key row ----

@@ -11,6 +11,7 @@ import json
 from collections import defaultdict
 
 CLASSES = {"k_indiv_stats": "stats", "k_gather": "gather", "k_grm": "grm", "k_diag_grm": "grm", "k_diag_grm8": "grm",
+           "k_sys_tiles": "grm",
            "k_chol_diag": "chol_diag", "k_chol_offdiag": "chol_offdiag", "k_solve": "solve",
            "k_de_step": "de_step", "k_decode_topk": "decode", "k_snp_scan": "snp_scan"}
 

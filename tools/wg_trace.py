@@ -17,7 +17,7 @@ os.environ["TBLUP_WG_TRACE"] = "1"
 
 import bench  # noqa: E402
 
-KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj"}
+KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys"}
 
 
 def main():
@@ -47,9 +47,12 @@ def main():
     tot = 0.0
     print(f"{len(rec)} workgroups, {cus} CUs")
     launches = []
+    sysm = rec["kind"] == 5
+    if sysm.any():
+        launches.append((rec[sysm]["start"].min(), -1, False, sysm))
     for J in sorted(set(rec["J"].tolist())):
         for is_diag in (True, False):
-            m = (rec["J"] == J) & ((rec["kind"] == 1) == is_diag)
+            m = (rec["J"] == J) & ((rec["kind"] == 1) == is_diag) & ~sysm
             if not m.any():
                 continue
             launches.append((rec[m]["start"].min(), J, is_diag, m))
@@ -78,7 +81,7 @@ def main():
               f"gap {gap * 1e6:5.1f} util {util:.2f}{first_tile} | " + "; ".join(parts))
     print(f"sum of launch spans {tot * 1e6:.1f} us, first start to last end {(prev_end - t0) * 1e6:.1f} us")
     # phase stamps of diagonal workgroup 0 (tblup_internal.h DTR_RECS): per wave, 30 slots
-    NT, pos = 8, 0
+    NT, pos = 8, int(sysm.sum())
     names = ["start", "pre-barrier", "post-barrier"] + [f"{x}{p}" for p in range(8) for x in ("a", "b", "w")] + [
         "xinv7", "post-xinv7", "dinv", "z", "syrk-issued", "-"] + [f"{x}{t}" for t in range(8) for x in
                                                                    ("stg-ready", "stg-go")] + ["syrk-done"]
@@ -87,7 +90,8 @@ def main():
         st = raw[pos:pos + 128].reshape(-1).reshape(8, 64).astype(np.int64)
         pos += 128
         nI = NT - J - 1
-        pos += 0 if nI <= 0 else pop * nI + pop * (1 if (J >= 1 and J + 1 < NT) else 0) + (pop * (NT - 2) if J == 0 else 0)
+        kjj = J == 0 and os.environ.get("TBLUP_SYS_TILES", "1") == "0"
+        pos += 0 if nI <= 0 else pop * nI + pop * (1 if (J >= 1 and J + 1 < NT) else 0) + (pop * (NT - 2) if kjj else 0)
         if J in (0, 3):
             base = st[0, 0]
             print(f"diag J={J} wg0 phase stamps (us from start), waves 0 / 1 / 4:")
