@@ -93,6 +93,16 @@ class GpuBlupEngine:
                 self._ctx, _ptr(mt, ctypes.c_double), self.n_traits))
         self._splits = OrderedDict()   # key -> (split_id, n_valid)
         self._next_split = 0
+        self._pending = None           # (event, keep-alive) of asynchronous work using the workspace
+        self._spec_stream = None
+
+    def _settle(self):
+        """Wait for asynchronous work (eval_keys_async) that uses the context's workspace; every
+        other entry point calls this first, so calls stay serialised on the context."""
+        p = self._pending
+        if p is not None:
+            self._pending = None
+            p[0].synchronize()
 
     # ------------------------------------------------------------------ splits
     def split_id(self, train, valid):
@@ -117,6 +127,7 @@ class GpuBlupEngine:
     def evaluate(self, genomes, train, valid, h2, branch="auto", return_ebv=False):
         """Fitness |pearson(EBV_V, y_V)| for each selected-index set (evaluator.py:244-314);
         multi-trait: the mean over traits, EBVs (B, t, n_valid)."""
+        self._settle()
         sid = self.split_id(train, valid)
         idx, offsets = concat_genomes(genomes)
         B = len(genomes)
@@ -154,6 +165,7 @@ class GpuBlupEngine:
         """RandomKeyIndividual.genome for a batch (individual.py:154-156) on the GPU:
         row i -> np.argsort(keys[i])[-int(lengths[i]):] (ascending key order; equal keys
         ordered by index, as a stable argsort).  Returns (idx, offsets) for evaluate_concat."""
+        self._settle()
         kk = np.ascontiguousarray(np.asarray(keys, dtype=np.float64))
         if kk.ndim != 2:
             raise ValueError("keys must be (batch, d)")
@@ -177,6 +189,7 @@ class GpuBlupEngine:
     def grm(self, indices=None):
         """make_grm(data[:, indices]) over all animals (tblup/utils.py:7-18) on the GPU:
         n x n float64.  indices=None: every SNP of the panel."""
+        self._settle()
         idx = _as_int64(np.arange(self.n_snps) if indices is None else indices)
         G = np.empty((self.n_animals, self.n_animals), dtype=np.float64)
         _native.check("tblup_grm", self._lib.tblup_grm(self._ctx, _ptr(idx, ctypes.c_int64), len(idx),
@@ -185,6 +198,7 @@ class GpuBlupEngine:
 
     def snp_scan(self, rows, yc):
         """Per-SNP (sum x, sum x^2, sum x*yc) over animal `rows` (k_snp_scan)."""
+        self._settle()
         r = _as_int64(rows)
         y = np.ascontiguousarray(yc, dtype=np.float64)
         if y.shape != r.shape:
@@ -200,6 +214,7 @@ class GpuBlupEngine:
     def decode_randkey_tensor(self, keys, d, lengths):
         """decode_randkey on a device tensor of key rows (B x ld float64, ld >= d, on this
         context's device) on torch's current stream; returns host (idx, offsets)."""
+        self._settle()
         import torch
         from .keystore import work_stream
         B, ld = keys.shape
@@ -219,6 +234,7 @@ class GpuBlupEngine:
 
     def evaluate_concat(self, idx, offsets, train, valid, h2, branch="auto"):
         """evaluate() on an already-concatenated (idx, offsets) batch."""
+        self._settle()
         sid = self.split_id(train, valid)
         idx = _as_int64(idx)
         offsets = _as_int64(offsets)
@@ -232,6 +248,7 @@ class GpuBlupEngine:
 
     def debug_grm(self, indices, train, valid, h2, branch="auto", stage=1):
         """K_{R,T} (stage 1) or the factored block (stage 2) and z for one individual."""
+        self._settle()
         sid = self.split_id(train, valid)
         idx = _as_int64(indices)
         nT, nV = len(train), len(valid)
@@ -241,6 +258,38 @@ class GpuBlupEngine:
             self._ctx, sid, _ptr(idx, ctypes.c_int64), len(idx), float(h2), _native.BRANCH[branch], int(stage),
             _ptr(out, ctypes.c_double), _ptr(z, ctypes.c_double)))
         return out, z
+
+    def eval_keys_async(self, keys, lengths, train, valid, h2):
+        """RandomKey individuals' fitness straight from a device tensor of their keys (B x ld
+        float64 on this context's device): decode (k_decode_topk) and evaluation enqueued on a
+        stream of this engine without waiting.  Returns (event, pinned host fitness tensor);
+        the result is valid once the event has completed.  Later calls on the engine wait for it."""
+        import torch
+        self._settle()
+        B, ld = keys.shape
+        lens = np.asarray(lengths, dtype=np.int64)
+        offsets = np.zeros(B + 1, dtype=np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        sid = self.split_id(train, valid)
+        dev = keys.device
+        if self._spec_stream is None:
+            self._spec_stream = torch.cuda.Stream(device=dev)
+        st = self._spec_stream
+        st.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.device(dev), torch.cuda.stream(st):
+            d_off = torch.from_numpy(offsets).to(dev, non_blocking=True)
+            d_idx = torch.empty(int(offsets[-1]), dtype=torch.int64, device=dev)
+            d_fit = torch.empty(B, dtype=torch.float64, device=dev)
+            self.decode_randkey_device(keys.data_ptr(), B, ld, keys.stride(0), d_off.data_ptr(), offsets,
+                                       d_idx.data_ptr(), st.cuda_stream)
+            self.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), offsets, h2, d_fit.data_ptr(),
+                                 stream_ptr=st.cuda_stream)
+            host = torch.empty(B, dtype=torch.float64, pin_memory=True)
+            host.copy_(d_fit, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self._pending = (ev, (keys, d_off, d_idx, d_fit, offsets))
+        return ev, host
 
     # --------------------------------------------------------------- profiling
     def set_profiling(self, enable=True):
@@ -291,6 +340,8 @@ class GpuBlupEngine:
 
     # ----------------------------------------------------------------- cleanup
     def close(self):
+        if getattr(self, "_pending", None) is not None:
+            self._settle()
         if getattr(self, "_ctx", None):
             self._lib.tblup_ctx_destroy(self._ctx)
             self._ctx = None

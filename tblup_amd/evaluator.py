@@ -155,6 +155,7 @@ class BlupParallelEvaluator(ParallelEvaluator):
         self.archive = {}
         self.snp_remover = snp_remover
         self.h2 = h2
+        self._spec = None   # speculative evaluation of the last GPU DE generation (see _speculate)
         data = np.load(data_path, mmap_mode="r")
         self.n_samples, self.n_columns = data.shape[0], data.shape[1]
         if splitter:
@@ -201,7 +202,8 @@ class BlupParallelEvaluator(ParallelEvaluator):
         return self.training_indices, self.validation_indices
 
     def __getstate__(self):
-        return {k: v for k, v in self.__dict__.items() if k not in ("archive", "pool", "engine", "_owns_group")}
+        return {k: v for k, v in self.__dict__.items()
+                if k not in ("archive", "pool", "engine", "_owns_group", "_spec")}
 
     def genomes_to_evaluate(self, population):
         """Individuals whose uid is not archived (evaluator.py:339-357)."""
@@ -240,9 +242,66 @@ class BlupParallelEvaluator(ParallelEvaluator):
                 return [idx[off[j]:off[j + 1]] for j in range(len(individuals))]
         return [i.genome for i in individuals]
 
+    # -- speculative evaluation of a GPU DE generation -----------------------------
+    _SPEC_TYPES = ("RandomKeyIndividual",)
+
+    def _speculate(self, parents, keys, generation):
+        """Called by tblup_amd.evolver right after its DE kernel, with the children's keys still
+        on the device: enqueue their decode and evaluation now (GpuBlupEngine.eval_keys_async)
+        so the GPU computes the fitnesses while the host copies the children's genomes.
+        evaluate() takes the result only when it is asked for exactly these children,
+        unchanged, at this generation; otherwise it is dropped and evaluate() runs as usual.
+        Only where evaluate() is a pure function of the genomes: the fixed split or InterGCV
+        folds (no RNG draws), no SNP removal, one process, RandomKey individuals."""
+        self._spec = None
+        if self.engine is None or type(self) not in (BlupParallelEvaluator, InterGCVBlupParallelEvaluator):
+            return False
+        if not hasattr(self.engine, "eval_keys_async") or world()[1] > 1 or not parents:
+            return False
+        if self.snp_remover is not None and self.snp_remover.should_remove():
+            return False
+        if not all(type(p).__name__ in self._SPEC_TYPES for p in parents):
+            return False
+        L = keys.shape[1]
+        lens = [int(p.length) for p in parents]
+        if not all(1 <= k <= min(L, 8192) for k in lens) or keys.device.index != self.engine.device:
+            return False
+        train, valid = self.train_validation_indices(generation)
+        event, host = self.engine.eval_keys_async(keys, lens, train, valid, self.h2)
+        self._spec = {"generation": generation, "keys": keys, "lens": lens, "event": event, "host": host,
+                      "inds": None}
+        return True
+
+    def _spec_bind(self, children):
+        if self._spec is not None:
+            self._spec["inds"] = list(children)
+
+    def _take_spec(self, population, generation):
+        spec, self._spec = self._spec, None
+        if spec is None or spec["inds"] is None or spec["generation"] != generation:
+            return None
+        inds = [population[i] for i in range(len(population))]
+        if len(inds) != len(spec["inds"]) or any(a is not b for a, b in zip(inds, spec["inds"])):
+            return None
+        if any(i.uid in self.archive or int(i.length) != k for i, k in zip(inds, spec["lens"])):
+            return None
+        # genomes untouched since the DE step: the key store still maps child i to row i of the keys
+        from .keystore import DeviceKeyStore
+        hits = DeviceKeyStore.get(self.engine.device).rows(inds)
+        if any(h is None or h[0] is not spec["keys"] or h[1] != i for i, h in enumerate(hits)):
+            return None
+        spec["event"].synchronize()
+        return spec["host"].numpy().copy()
+
     def evaluate(self, previous_population, next_population, generation):
         """evaluator.py:359-378."""
         super().evaluate(previous_population, next_population, generation)
+        fits = self._take_spec(next_population, generation)
+        if fits is not None:   # the children's fitnesses, computed while their genomes were copied
+            for i, f in enumerate(fits):
+                next_population[i].set_fitness(f)
+                self.archive[next_population[i].uid] = next_population[i].fitness
+            return next_population
         todo, where, reevaluate = self.genomes_to_evaluate(next_population)
         next_population = self._evaluate(next_population, todo, where, generation)
         if reevaluate:

@@ -151,24 +151,53 @@ def _child_dtypes(genomes, donors, strategy, mi, clip):
 _POOL = None
 
 
-def _copy_rows(host, dtypes, workers=8):
-    """An own array per child: float64 rows as TrackedGenome views (the key store mirrors
-    them on the device and must notice in-place writes), other dtypes as plain arrays."""
+def _pool(workers=8):
     global _POOL
-    n = host.shape[0]
-
-    def chunk(lo, hi):
-        if dtypes is None:
-            return [track(np.array(host[i])) for i in range(lo, hi)]
-        return [np.array(host[i], dtype=dtypes[i]) for i in range(lo, hi)]
-    if n * host.shape[1] < (1 << 20):
-        return chunk(0, n)
     if _POOL is None:
         from concurrent.futures import ThreadPoolExecutor
         _POOL = ThreadPoolExecutor(workers, thread_name_prefix="tblup-copy")
-    step = (n + workers - 1) // workers
-    parts = _POOL.map(lambda lo: chunk(lo, min(n, lo + step)), range(0, n, step))
+    return _POOL
+
+
+def _copy_rows(host, dtypes, workers=8, ready=None):
+    """An own array per child: float64 rows as TrackedGenome views (the key store mirrors
+    them on the device and must notice in-place writes), other dtypes as plain arrays.
+    ready: per-chunk callables that block until that chunk of `host` has arrived (the
+    device-to-host copy is chunked so the row copies of chunk c overlap the transfer of
+    chunk c + 1)."""
+    n = host.shape[0]
+    nchunk = workers if ready is None else len(ready)
+    step = (n + nchunk - 1) // nchunk
+
+    def chunk(c):
+        lo, hi = c * step, min(n, (c + 1) * step)
+        if ready is not None:
+            ready[c]()
+        if dtypes is None:
+            return [track(np.array(host[i])) for i in range(lo, hi)]
+        return [np.array(host[i], dtype=dtypes[i]) for i in range(lo, hi)]
+    if ready is None and n * host.shape[1] < (1 << 20):
+        return [a for c in range(nchunk) for a in chunk(c)]
+    parts = _pool(workers).map(chunk, range(nchunk))
     return [a for part in parts for a in part]
+
+
+_NO_GENOME = np.empty(0)
+
+
+def _copy_individual(indv):
+    """deepcopy(indv) as the reference's evolvers take it (evolver.py:130, 208), without
+    copying the internal genome the caller replaces right after (set_internal_genome):
+    the reference's IndexIndividual.__deepcopy__ (individual.py:110-118) deep-copies
+    `_genome`, a 400 KB array per child at L = 50k."""
+    g = getattr(indv, "_genome", None)
+    if not isinstance(g, np.ndarray):
+        return deepcopy(indv)
+    indv._genome = _NO_GENOME
+    try:
+        return deepcopy(indv)
+    finally:
+        indv._genome = g
 
 
 class Evolver(abc.ABC):
@@ -213,17 +242,32 @@ class _GpuDEEvolver(Evolver):
             parents = store.gather(inds, L, host_rows=lambda i: genomes[i])   # device-resident parents
             children = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate, clip,
                                         self.dimensionality - 1)
+            # the population's evaluator (tblup_amd) may start evaluating the children on the GPU
+            # now, while their genomes cross to the host (BlupParallelEvaluator._speculate)
+            evaluator = getattr(population, "evaluator", None)
+            spec = getattr(evaluator, "_speculate", None)
+            speculated = bool(spec is not None and dtypes is None and spec(inds, children, population.generation))
+            # children to the host in chunks, each followed by an event, so the per-row copies of
+            # one chunk overlap the transfer of the next
             host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
-            host.copy_(children)
-        host = host.numpy()
-        # an own array per child (a row view would pin the whole generation's block); the
-        # copies (first-touch page faults dominate) run in chunks on a few threads
-        arrays = _copy_rows(host, dtypes)
-        next_pop = []
+            nchunk = 8 if n >= 16 else 1
+            rows = (n + nchunk - 1) // nchunk
+            events = []
+            for c in range(nchunk):
+                lo, hi = c * rows, min(n, (c + 1) * rows)
+                if lo < hi:
+                    host[lo:hi].copy_(children[lo:hi], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+        # the candidates (new uids, the parent's other attributes) while the transfer runs
+        next_pop = [_copy_individual(population[i]) for i in range(n)]
+        # an own array per child (a row view would pin the whole generation's block)
+        arrays = _copy_rows(host.numpy(), dtypes, ready=[ev.synchronize for ev in events])
         for i in range(n):
-            candidate = deepcopy(population[i])
-            candidate.set_internal_genome(arrays[i])
-            next_pop.append(candidate)
+            next_pop[i].set_internal_genome(arrays[i])
+        if speculated:
+            evaluator._spec_bind(next_pop)
         if dtypes is None:   # float64 internal genomes: the device rows are the children's exact values
             store.record(children, next_pop, arrays)
             store.record(parents, inds, genomes, adopt=True)

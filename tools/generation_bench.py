@@ -19,7 +19,9 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
     import torch  # noqa: F401
     from oracle import blup_oracle as O
     from oracle import de_oracle as D
-    from tests.helpers import RandomKeyIndividual, Pop
+    from tests.helpers import Pop
+    # the reference's RandomKeyIndividual semantics (deepcopy copies the genome, individual.py:110-118)
+    from tests.ga_driver import RandomKeyIndividual
     from tblup_amd.evaluator import BlupParallelEvaluator
     from tblup_amd.evolver import DERandOneEvolver
     rng = np.random.default_rng(0)
@@ -31,7 +33,7 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
     random.seed(0)
     np.random.seed(0)
     ev = BlupParallelEvaluator(os.path.join(tmp, "g.npy"), os.path.join(tmp, "y.npy"), 0.4)
-    inds = [RandomKeyIndividual(rng.uniform(size=p), k) for _ in range(pop)]
+    inds = [RandomKeyIndividual(k, p, genome=rng.uniform(size=p)) for _ in range(pop)]
     evo = DERandOneEvolver(p, 0.8, 0.5, False)
     out = {"n": n, "p": p, "k": k, "pop": pop}
     phase = {}
@@ -48,9 +50,22 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
     with ev:
         for nm in ("genomes_to_evaluate", "_fitness", "_batch_genomes"):
             timed(ev, nm)
+        import tblup_amd.evolver as EVM
+        for nm in ("_copy_rows", "_child_dtypes"):
+            fn = getattr(EVM, nm)
+
+            def wrap(*a, _fn=fn, _nm=nm, **kw):
+                t = time.perf_counter()
+                r = _fn(*a, **kw)
+                phase[_nm] = phase.get(_nm, 0.0) + time.perf_counter() - t
+                return r
+            setattr(EVM, nm, wrap)
+        timed(evo, "_donors")
+        timed(EVM.GpuDEStep.get(0), "step_device")
         timed(ev.engine, "evaluate")
         timed(ev.engine, "decode_randkey_tensor")
         popn = Pop(inds, 0)
+        popn.evaluator = ev   # as tblup.Population holds it (population.py:28): lets the evolver hand over
         ev.evaluate(popn, popn, 0)
         ts = []
         for g in range(1, gens + 1):
