@@ -87,14 +87,10 @@ __device__ __forceinline__ v4d mma_abt(const double* A, const double* Bt, v4d ac
   return acc;
 }
 
-// Factor the 16x16 SPD block D in place with ONE wave (no barriers): D <- L (lower),
-// X <- L^{-1} (lower, zeros above).  Lane l holds the whole row i = l&15 of the symmetric
-// block (the four 16-lane groups hold identical copies), so the pivot row j of step j is
-// one lane's registers: it is broadcast with v_readlane (uniform, no LDS traffic).
-// Right-looking elimination with unscaled pivots; E = L'^{-1} is built by row operations
-// on I alongside (L = L' D^{1/2}, X = D^{-1/2} E):
-//   c > j : T_ic -= (T_ij / piv_j) T_jc       (every lane; the rows i <= j only touch
-//                                              their upper part, which is never read again)
+// Factor the 16x16 SPD block D with ONE wave (no barriers): X <- L^{-1} (lower, zeros above),
+// and L into D's lower triangle on the debug path.  Right-looking elimination with unscaled
+// pivots; E = L'^{-1} is built by row operations on I alongside (L = L' D^{1/2}, X = D^{-1/2} E):
+//   c > j : T_ic -= (T_ij / piv_j) T_jc
 //   i > j : E_ic -= (T_ij / piv_j) E_jc (c < j),  E_ij = -T_ij / piv_j
 // Column scaling by 1/sqrt(piv) is deferred to the end.
 __device__ __forceinline__ double recip(double p) {
@@ -112,70 +108,93 @@ __device__ __forceinline__ double rdlane(double x, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Row-j broadcast inside each 16-lane row of the wave (DPP row_newbcast:j, gfx90a+).
+// x += x[lane J of this 16-lane row] * m in one instruction (DPP64 row_newbcast on src0).  The
+// s_nop covers the DPP read-after-VALU-write hazard, which the compiler does not track inside asm.
 template <int J>
-__device__ __forceinline__ double row_bcast(double x) {
+__device__ __forceinline__ void fmac_row(double& x, double m) {
+  asm("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(m), "i"(J));
+}
+
+// Rows 0 and 2 of the wave to rows 1 and 3 (v_permlane16_swap on each 32-bit half).
+__device__ __forceinline__ double even_rows_to_odd(double x) {
   const long long bits = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_mov_dpp((int)bits, 0x150 + J, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(bits >> 32), 0x150 + J, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+  const unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __longlong_as_double(((long long)b[0] << 32) | (unsigned)a[0]);
 }
 
-// Lane l = i + 16 g holds columns 4g .. 4g+3 of row i (the four 16-lane groups split the
-// columns).  Per pivot j: T_jj by v_readlane, row j of the lane's own four columns by a DPP
-// row broadcast, and T_ij (column j lives in group j/4) by one cross-group permute -- instead of
-// 32 v_readlanes per pivot with every lane holding a whole row.  Same operations in the same
-// order per element as the whole-row form, so the factor and its inverse are unchanged.
-template <int J>
-__device__ __forceinline__ void f16_step(double (&v)[4], double (&e)[4], double (&pv)[4], double& own, int i, int g) {
-  constexpr int GJ = J >> 2, QJ = J & 3;
-  const double piv = rdlane(v[QJ], J + 16 * GJ);
-  const double tij = __shfl(v[QJ], i + 16 * GJ);
-  double rj[4], ej[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    rj[q] = row_bcast<J>(v[q]);
-    ej[q] = row_bcast<J>(e[q]);
-  }
-  if (g == GJ) pv[QJ] = piv;
-  if (i == J) own = piv;
-  const double li = tij * recip(piv);
-  const bool below = i > J;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = 4 * g + q;
-    v[q] = (c > J) ? __builtin_fma(-li, rj[q], v[q]) : v[q];
-    e[q] = (below && c < J) ? __builtin_fma(-li, ej[q], e[q]) : e[q];
-    e[q] = (below && c == J) ? -li : e[q];
+// 16x16 factor and inverse.  Lane l = i + 16 g: even groups hold row i of T in x[0..15]
+// (column c in register c), odd groups row i of E (the Gauss-Jordan inverse, starting at I)
+// with column c in register 15 - c.  Pivot j: T_jj by v_readlane, l_i = T_ij / T_jj from the
+// lane's own register j (zero for i <= j), handed from the T rows to the E rows by a
+// permlane16 swap, then every register the two halves still need -- T columns > j, E columns
+// <= j, the same registers thanks to E's reversed order -- takes x += x[row j] * (-l_i) in one
+// DPP64 fmac.  Registers outside those sets only ever receive x += 0 or hold finished columns,
+// so no per-element masks.  Same operations in the same order per element as the factor /
+// elimination T_ic -= l_i T_jc, E_ic -= l_i E_jc, so the factor and its inverse are unchanged.
+template <int J, int R>
+__device__ __forceinline__ void f16_upd(double (&x)[NB], double m) {
+  if constexpr (R < NB) {
+    if constexpr (R != J + 1) fmac_row<J>(x[R], m);
+    f16_upd<J, R + 1>(x, m);
   }
 }
 
-template <int J>
-__device__ __forceinline__ void f16_steps(double (&v)[4], double (&e)[4], double (&pv)[4], double& own, int i, int g) {
+template <int J, bool WL>
+__device__ __forceinline__ void f16_steps(double (&x)[NB], double (&ls)[NB], double& own, int i) {
   if constexpr (J < NB) {
-    f16_step<J>(v, e, pv, own, i, g);
-    f16_steps<J + 1>(v, e, pv, own, i, g);
+    const double piv = rdlane(x[J], J);
+    own = (i == J) ? piv : own;
+    if constexpr (WL) ls[J] = x[J];
+    if constexpr (J + 1 < NB) {
+      const double li = x[J] * recip(piv);
+      const double m = even_rows_to_odd((i > J) ? -li : 0.0);
+      fmac_row<J>(x[J + 1], m);                          // next pivot's column first
+      constexpr int R0 = (J + 1 < NB - 1 - J) ? J + 1 : NB - 1 - J;
+      f16_upd<J, R0>(x, m);
+    }
+    f16_steps<J + 1, WL>(x, ls, own, i);
   }
 }
 
-__device__ __forceinline__ void factor16(double* D, double* X, int l) {
-  const int i = l & 15, g = l >> 4;
-  double v[4], e[4], pv[4] = {1.0, 1.0, 1.0, 1.0}, own = 1.0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = 4 * g + q;
-    v[q] = (c <= i) ? D[bo(i, c)] : D[bo(c, i)];   // symmetric row from the lower triangle
-    e[q] = (c == i) ? 1.0 : 0.0;
+template <int C>
+__device__ __forceinline__ void f16_store_l(double* D, const double (&ls)[NB], double rs_own, int l) {
+  if constexpr (C < NB) {
+    const double rc = __builtin_amdgcn_mov_dpp(rs_own, 0x150 + C, 0xF, 0xF, true);  // lane C's 1/sqrt(piv_C)
+    if (l < 16 && l >= C) D[bo(l, C)] = ls[C] * rc;
+    f16_store_l<C + 1>(D, ls, rs_own, l);
   }
-  f16_steps<0>(v, e, pv, own, i, g);
-  // deferred scaling: L_ic = T_ic / sqrt(piv_c), X_ic = E_ic / sqrt(piv_i)
+}
+
+// D: symmetric 16x16 block (lower triangle read) -> X = L^{-1} (and, WL, L into D's lower
+// triangle; the diagonal L blocks are read back only by the debug path)
+__device__ __forceinline__ void fstamp(uint64_t* st, int slot) {
+  if (st && (threadIdx.x & 63) == 0) st[slot] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <bool WL>
+__device__ __forceinline__ void factor16(double* D, double* X, int l, uint64_t* st) {
+  const int i = l & 15;
+  fstamp(st, 50);
+  const bool t_row = ((l >> 4) & 1) == 0;
+  double x[NB], ls[NB], own = 1.0;
+#pragma unroll
+  for (int c = 0; c < NB; ++c) {
+    const double v = (c <= i) ? D[bo(i, c)] : D[bo(c, i)];   // symmetric row from the lower triangle
+    x[c] = t_row ? v : ((NB - 1 - c == i) ? 1.0 : 0.0);
+  }
+  fstamp(st, 51);
+  f16_steps<0, WL>(x, ls, own, i);
+  fstamp(st, 52);
+  // deferred scaling: X_ic = E_ic / sqrt(piv_i) (E_ic = +0 above the diagonal); L_ic = T_ic / sqrt(piv_c)
   const double rs_own = 1.0 / sqrt(own);
+  if (l >= 16 && l < 32) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = 4 * g + q;
-    X[bo(i, c)] = (i >= c) ? e[q] * rs_own : 0.0;
-    if (i >= c) D[bo(i, c)] = v[q] * (1.0 / sqrt(pv[q]));
+    for (int c = 0; c < NB; ++c) X[bo(i, c)] = x[NB - 1 - c] * rs_own;
   }
+  if constexpr (WL) f16_store_l<0>(D, ls, rs_own, l);
+  fstamp(st, 53);
 }
 
 
@@ -213,6 +232,14 @@ struct CholArgs {
   uint64_t* dtr;            // diagonal launch: phase timestamps of workgroup 0 (TBLUP_WG_TRACE), else null
   const int16_t* kc;        // SNP form: off-diagonal system-tile counts (k_sys_tiles), else null
 };
+
+// st: profiling only (phase stamps of one factorisation in diagonal workgroup 0), else null
+__device__ __forceinline__ void factor16_any(const CholArgs& a, double* D, double* X, int l, uint64_t* st = nullptr) {
+  if (a.skip & FLAG_WRITE_LJJ)
+    factor16<true>(D, X, l, st);
+  else
+    factor16<false>(D, X, l, st);
+}
 
 // Profiling only: lane 0 of each wave of diagonal workgroup 0 stamps phase boundaries
 // (s_memrealtime) into dtr[wave * 64 + slot].
@@ -739,7 +766,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   //    look-ahead: wave 0 updates diagonal block p+1 first and factors it while waves 1-3
   //    finish the rest of step p's trailing update.
   if (!(a.skip & 4)) {
-    if (w == 0 && !(a.skip & 256)) factor16(Tp + pk(0, 0), Xp + pk(0, 0), l);
+    if (w == 0 && !(a.skip & 256)) factor16_any(a, Tp + pk(0, 0), Xp + pk(0, 0), l);
     __syncthreads();
   }
   for (int p = 0; p < ((a.skip & 4) ? 0 : NBLK); ++p) {
@@ -754,6 +781,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     if (p + 1 == NBLK) break;
     const int nb = NBLK - 1 - p;
     if (w == 0) {
+      uint64_t* st = (a.dtr && blockIdx.x == 0 && p == 3) ? a.dtr : nullptr;
+      fstamp(st, 54);
       if (!(a.skip & 512)) {
         v4d x = {0.0, 0.0, 0.0, 0.0};
         x = mma_abt(Tp + pk(p + 1, p), Tp + pk(p + 1, p), x, l);
@@ -761,7 +790,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 #pragma unroll
         for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
       }
-      if (!(a.skip & 256)) factor16(Tp + pk(p + 1, p + 1), Xp + pk(p + 1, p + 1), l);
+      if (!(a.skip & 256)) factor16_any(a, Tp + pk(p + 1, p + 1), Xp + pk(p + 1, p + 1), l, st);
     } else if (w != DW / 2) {
       // wave DW/2 shares wave 0's SIMD and stays idle so that factor16 issues alone there;
       // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over the others

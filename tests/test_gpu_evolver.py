@@ -208,3 +208,4 @@ def test_gpu_de_small_shapes_vs_oracle(gpu, L, pop, pre):
         assert np.array_equal(st[1], np_after[1]) and st[2] == np_after[2], (strat, L, pop, pre)
         for k, w in zip(kids, want):
             assert np.array_equal(k.get_internal_genome(), w), (strat, L, pop, pre)
+

@@ -64,6 +64,7 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
         timed(EVM.GpuDEStep.get(0), "step_device")
         timed(ev.engine, "evaluate")
         timed(ev.engine, "decode_randkey_tensor")
+        EVM.PROFILE = {}
         popn = Pop(inds, 0)
         popn.evaluator = ev   # as tblup.Population holds it (population.py:28): lets the evolver hand over
         ev.evaluate(popn, popn, 0)
@@ -79,7 +80,9 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
             ts.append((t1 - t0, t2 - t1, time.perf_counter() - t0))
             if g == gens:
                 out["phases_last_gen_ms"] = {k: round(1e3 * v, 2) for k, v in phase.items()}
+                out["evolve_segments_last_gen_ms"] = {k: round(1e3 * v, 2) for k, v in EVM.PROFILE.items()}
             phase.clear()
+            EVM.PROFILE.clear()
         best = min(ts, key=lambda t: t[2])
         out.update({"gpu_evolve_ms": 1e3 * best[0], "gpu_evaluate_ms": 1e3 * best[1], "gpu_generation_ms": 1e3 * best[2],
                     "gpu_generation_ms_all": [round(1e3 * t[2], 2) for t in ts]})
@@ -96,4 +99,4 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
 
 
 if __name__ == "__main__":
-    main()
+    main(gens=int(sys.argv[1]) if len(sys.argv) > 1 else 4)

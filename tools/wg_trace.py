@@ -84,7 +84,8 @@ def main():
     NT, pos = 8, int(sysm.sum())
     names = ["start", "pre-barrier", "post-barrier"] + [f"{x}{p}" for p in range(8) for x in ("a", "b", "w")] + [
         "xinv7", "post-xinv7", "dinv", "z", "syrk-issued", "-"] + [f"{x}{t}" for t in range(8) for x in
-                                                                   ("stg-ready", "stg-go")] + ["syrk-done"]
+                                                                   ("stg-ready", "stg-go")] + ["syrk-done"] + [
+        "f4-upd-done", "f4-x-init", "f4-steps", "f4-stored", "f4-branch"]
     for J in range(NT):
         pos += pop
         st = raw[pos:pos + 128].reshape(-1).reshape(8, 64).astype(np.int64)
@@ -95,7 +96,7 @@ def main():
         if J in (0, 3):
             base = st[0, 0]
             print(f"diag J={J} wg0 phase stamps (us from start), waves 0 / 1 / 4:")
-            for k in [0, 30] + list(range(32, 49)) + list(range(1, 30)):
+            for k in [0, 30] + list(range(32, 49)) + list(range(1, 30)) + [54, 50, 51, 52, 53]:
                 if st[0, k] == 0 and st[1, k] == 0:
                     continue
                 vals = " ".join(f"{(st[w, k] - base) / 100.0:7.2f}" if st[w, k] else "      -" for w in (0, 1, 4))
