@@ -109,10 +109,17 @@ __device__ __forceinline__ double rdlane(double x, int lane) {
 }
 
 // x += x[lane J of this 16-lane row] * m in one instruction (DPP64 row_newbcast on src0).  The
-// s_nop covers the DPP read-after-VALU-write hazard, which the compiler does not track inside asm.
-template <int J>
+// compiler does not see inside asm, so hazards are handled here: NOP = the DPP read-after-VALU-
+// write wait for a register the previous instruction may have written (the next pivot's
+// column); the others are volatile so they keep their order, in which no fmac reads a
+// register the one before it wrote.
+template <int J, bool NOP>
 __device__ __forceinline__ void fmac_row(double& x, double m) {
-  asm("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(m), "i"(J));
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                 : "+v"(x) : "v"(m), "i"(J));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(m), "i"(J));
 }
 
 // Rows 0 and 2 of the wave to rows 1 and 3 (v_permlane16_swap on each 32-bit half).
@@ -124,6 +131,18 @@ __device__ __forceinline__ double even_rows_to_odd(double x) {
   return __longlong_as_double(((long long)b[0] << 32) | (unsigned)a[0]);
 }
 
+// v on lanes whose row (lane & 15) is below J, +0 elsewhere: the lane mask is a constant in
+// SGPRs (no compare on the pivot chain)
+template <int J>
+__device__ __forceinline__ double rows_below(double v) {
+  constexpr unsigned long long r = (0xFFFFull << (J + 1)) & 0xFFFFull;
+  constexpr unsigned long long msk = r | (r << 16) | (r << 32) | (r << 48);
+  const long long bits = __double_as_longlong(v);
+  int lo = (int)bits, hi = (int)(bits >> 32);
+  asm("v_cndmask_b32_e64 %0, 0, %0, %2\n\tv_cndmask_b32_e64 %1, 0, %1, %2" : "+v"(lo), "+v"(hi) : "s"(msk));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // 16x16 factor and inverse.  Lane l = i + 16 g: even groups hold row i of T in x[0..15]
 // (column c in register c), odd groups row i of E (the Gauss-Jordan inverse, starting at I)
 // with column c in register 15 - c.  Pivot j: T_jj by v_readlane, l_i = T_ij / T_jj from the
@@ -131,30 +150,33 @@ __device__ __forceinline__ double even_rows_to_odd(double x) {
 // permlane16 swap, then every register the two halves still need -- T columns > j, E columns
 // <= j, the same registers thanks to E's reversed order -- takes x += x[row j] * (-l_i) in one
 // DPP64 fmac.  Registers outside those sets only ever receive x += 0 or hold finished columns,
-// so no per-element masks.  Same operations in the same order per element as the factor /
-// elimination T_ic -= l_i T_jc, E_ic -= l_i E_jc, so the factor and its inverse are unchanged.
+// so no per-element masks.  The next pivot's column goes first; for j < 7 it is an E column
+// above the diagonal (E_jc = 0) for the odd groups, so it takes the multiplier before the swap
+// and the swap leaves the pivot chain.  Same operations in the same order per element as the
+// factor / elimination T_ic -= l_i T_jc, E_ic -= l_i E_jc, so the factor and its inverse are
+// unchanged.  Row i of T is final after pivot i - 1 (later multipliers are 0 there), so T_ii,
+// the pivot, is still in register i at the end.
 template <int J, int R>
 __device__ __forceinline__ void f16_upd(double (&x)[NB], double m) {
   if constexpr (R < NB) {
-    if constexpr (R != J + 1) fmac_row<J>(x[R], m);
+    if constexpr (R != J + 1) fmac_row<J, false>(x[R], m);
     f16_upd<J, R + 1>(x, m);
   }
 }
 
 template <int J, bool WL>
-__device__ __forceinline__ void f16_steps(double (&x)[NB], double (&ls)[NB], double& own, int i) {
-  if constexpr (J < NB) {
+__device__ __forceinline__ void f16_steps(double (&x)[NB], double (&ls)[NB]) {
+  if constexpr (J + 1 < NB) {
     const double piv = rdlane(x[J], J);
-    own = (i == J) ? piv : own;
     if constexpr (WL) ls[J] = x[J];
-    if constexpr (J + 1 < NB) {
-      const double li = x[J] * recip(piv);
-      const double m = even_rows_to_odd((i > J) ? -li : 0.0);
-      fmac_row<J>(x[J + 1], m);                          // next pivot's column first
-      constexpr int R0 = (J + 1 < NB - 1 - J) ? J + 1 : NB - 1 - J;
-      f16_upd<J, R0>(x, m);
-    }
-    f16_steps<J + 1, WL>(x, ls, own, i);
+    const double mt = rows_below<J>(-(x[J] * recip(piv)));
+    const double m = even_rows_to_odd(mt);
+    fmac_row<J, true>(x[J + 1], (J < 7) ? mt : m);   // next pivot's column first
+    constexpr int R0 = (J + 1 < NB - 1 - J) ? J + 1 : NB - 1 - J;
+    f16_upd<J, R0>(x, m);
+    f16_steps<J + 1, WL>(x, ls);
+  } else if constexpr (WL) {
+    ls[J] = x[J];
   }
 }
 
@@ -167,31 +189,40 @@ __device__ __forceinline__ void f16_store_l(double* D, const double (&ls)[NB], d
   }
 }
 
-// D: symmetric 16x16 block (lower triangle read) -> X = L^{-1} (and, WL, L into D's lower
-// triangle; the diagonal L blocks are read back only by the debug path)
 __device__ __forceinline__ void fstamp(uint64_t* st, int slot) {
   if (st && (threadIdx.x & 63) == 0) st[slot] = __builtin_amdgcn_s_memrealtime();
 }
 
+// D: symmetric 16x16 block (both triangles) -> X = L^{-1} (and, WL, L into D's lower triangle;
+// the diagonal L blocks are read back only by the debug path).  X must hold the reversed
+// identity (X_{i,15-i} = 1) on entry: the E rows load it as their starting point.
 template <bool WL>
 __device__ __forceinline__ void factor16(double* D, double* X, int l, uint64_t* st) {
   const int i = l & 15;
   fstamp(st, 50);
   const bool t_row = ((l >> 4) & 1) == 0;
-  double x[NB], ls[NB], own = 1.0;
+  const double* src = t_row ? D : X;
+  double x[NB], ls[NB];
 #pragma unroll
-  for (int c = 0; c < NB; ++c) {
-    const double v = (c <= i) ? D[bo(i, c)] : D[bo(c, i)];   // symmetric row from the lower triangle
-    x[c] = t_row ? v : ((NB - 1 - c == i) ? 1.0 : 0.0);
+  for (int k = 0; k < NB / 2; ++k) {
+    const v2d v = *reinterpret_cast<const v2d*>(src + bo(i, 2 * k));
+    x[2 * k] = v[0];
+    x[2 * k + 1] = v[1];
   }
   fstamp(st, 51);
-  f16_steps<0, WL>(x, ls, own, i);
+  f16_steps<0, WL>(x, ls);
   fstamp(st, 52);
+  // the pivot of row i from register i of the T rows, to the E rows by the same swap
+  double own = x[0];
+#pragma unroll
+  for (int c = 1; c < NB; ++c) own = (i == c) ? x[c] : own;
+  own = even_rows_to_odd(own);
   // deferred scaling: X_ic = E_ic / sqrt(piv_i) (E_ic = +0 above the diagonal); L_ic = T_ic / sqrt(piv_c)
   const double rs_own = 1.0 / sqrt(own);
   if (l >= 16 && l < 32) {
 #pragma unroll
-    for (int c = 0; c < NB; ++c) X[bo(i, c)] = x[NB - 1 - c] * rs_own;
+    for (int k = 0; k < NB / 2; ++k)
+      *reinterpret_cast<v2d*>(X + bo(i, 2 * k)) = v2d{x[NB - 1 - 2 * k] * rs_own, x[NB - 2 - 2 * k] * rs_own};
   }
   if constexpr (WL) f16_store_l<0>(D, ls, rs_own, l);
   fstamp(st, 53);
@@ -754,6 +785,14 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  // X's diagonal blocks start as the reversed identity (factor16's inverse rows load it); the
+  // SYRK ring that shared their space is drained
+#pragma unroll
+  for (int e = t; e < NBLK * BLKD; e += DTHR) {
+    const int p = e >> 8, o = e & 255, r = o >> 4;
+    const int c = 2 * (((o & 15) >> 1) ^ ((r >> 1) & 7)) + (o & 1);   // bo(r, c) == o
+    Xp[pk(p, p) + o] = (c == NB - 1 - r) ? 1.0 : 0.0;
+  }
   if (t < TILE) {
 #pragma unroll
     for (int tr = 0; tr < MAXT; ++tr) rsh[tr][t] = (tr < nt && gi < nrow) ? rv[tr] : 0.0;
@@ -791,14 +830,15 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
         for (int r = 0; r < 4; ++r) dst[bo((l >> 4) + 4 * r, l & 15)] -= x[r];
       }
       if (!(a.skip & 256)) factor16_any(a, Tp + pk(p + 1, p + 1), Xp + pk(p + 1, p + 1), l, st);
-    } else if (w != DW / 2) {
-      // wave DW/2 shares wave 0's SIMD and stays idle so that factor16 issues alone there;
-      // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over the others
-      const int wi = (w < DW / 2) ? w - 1 : w - 2;   // 0 .. DW-3
+    } else {
+      // trailing blocks e = 1 .. nb(nb+1)/2 - 1 (e = 0 is block (p+1, p+1)) over waves 1 .. DW-1
+      // (wave DW/2 shares wave 0's SIMD; factor16 leaves it enough issue slots)
+      const int wi = w - 1;   // 0 .. DW-2
+      constexpr int NTW = DW - 1;
       // two blocks per pass: independent MFMA chains and LDS traffic overlap
       const int ne = (a.skip & 512) ? 0 : nb * (nb + 1) / 2;
-      for (int e = wi + 1; e < ne; e += 2 * (DW - 2)) {
-        const int e2 = e + (DW - 2);
+      for (int e = wi + 1; e < ne; e += 2 * NTW) {
+        const int e2 = e + NTW;
         int qq = 0;
         while ((qq + 1) * (qq + 2) / 2 <= e) ++qq;
         const int q = p + 1 + qq, sb = p + 1 + (e - qq * (qq + 1) / 2);
