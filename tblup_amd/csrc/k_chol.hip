@@ -1171,21 +1171,31 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, int I0, int
 }
 
 // ===========================================================================
-// SNP form: every system tile (I >= J) of the batch in one launch, before the column loop, on
-// int8 MFMA (C = A B^T over the n_T train animals, 2-bit packed split rows read in place).
-// 4 waves per workgroup; wave (qr, qc) computes a 64 x 64 quadrant = 4 x 4 blocks of 16x16x64,
-// so 16 MFMAs take 8 unpacked dwords (the 8-wave in-tile form: 6 per 8 -- the unpack VALU work
-// is what bounds the int8 tile); 256-animal stages through a 4-deep LDS-DMA ring (64 KiB, two
-// workgroups per CU).  A rows are read through pi(rho) so the counts land in the f64
-// accumulator layout.  Off-diagonal tiles store
+// SNP form: every system tile (I >= J) of the batch in one launch, before the column loop:
+// C = A B^T over the n_T train animals on FP4 MFMA (16x16x128, e2m1 operands, fp32 accumulate),
+// 2-bit packed split rows read in place.  Genotype g is the e2m1 nibble 2g (0, 1.0, 2.0), so a
+// packed dword's even fields become nibbles by (x << 1) & 0x66666666 and its odd fields by
+// (x >> 1) & 0x66666666 -- 4 VALU ops per 16 animals into 4 operand dwords (the int8 form spent 7
+// per 16 animals) -- and the counts (<= 4 n_T < 2^24) accumulate exactly in fp32 at twice the
+// int8 rate.  The animals' order inside k is the same for A and B, so A B^T is unchanged.
+// 4 waves per workgroup; wave (qr, qc) computes a 64 x 64 quadrant = 4 x 4 blocks; 256-animal
+// stages through a 3-deep LDS-DMA ring (48 KiB, three workgroups per CU).  A rows are read
+// through pi(rho) so the counts land in the f64 accumulator layout.  Off-diagonal tiles store
 // the exact counts as int16 where the off-diagonal kernel's lanes read them (kc, see
 // tblup_internal.h); diagonal tiles store K_JJ + lambda I (identity on padding rows) as packed
-// fp64 blocks into Kd, exactly as k_diag_grm8 does.
+// fp64 blocks into Kd, exactly as k_diag_grm8 does.  (Rows stored as nibbles -- twice the bytes,
+// no unpack -- measured no faster: those loads then bound the launch.)
 // ===========================================================================
 constexpr int STW = 4;   // waves per system-tile workgroup
 
-__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4i (&cnt)[4][4], int64_t b, int J, int qr, int qc,
+__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
                                        int l);
+
+// two packed dwords (32 animals) -> one fp4 MFMA operand (even fields, odd fields of each)
+__device__ __forceinline__ v8i fp4_operand(uint32_t x0, uint32_t x1) {
+  constexpr uint32_t M = 0x66666666u;
+  return v8i{(int)((x0 << 1) & M), (int)((x0 >> 1) & M), (int)((x1 << 1) & M), (int)((x1 >> 1) & M), 0, 0, 0, 0};
+}
 #define sys_diag_epilogue sys_diag_epilogue_impl
 
 __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* kc, int ntri) {
@@ -1223,11 +1233,11 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
       __builtin_amdgcn_global_load_lds(sb[h] + st * 64, (lds_ptr_t)(slot + TB + (2 * w + h) * 1024), 16, 0, 0);
     }
   };
-  v4i cnt[4][4];
+  v4f cnt[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) cnt[m][n] = v4i{0, 0, 0, 0};
+    for (int n = 0; n < 4; ++n) cnt[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
   for (int64_t st = 0; st < D - 1 && st < nst; ++st) issue(st);
   const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
   for (int64_t st = 0; st < nst; ++st) {
@@ -1250,18 +1260,18 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
         if (ztail) bq[m] = uint4{0u, 0u, 0u, 0u};
       }
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        v4i av[4], bv[4];
+      for (int s2 = 0; s2 < 2; ++s2) {
+        v8i av[4], bv[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-          av[m] = unpack16(s4 == 0 ? aq[m].x : s4 == 1 ? aq[m].y : s4 == 2 ? aq[m].z : aq[m].w);
-          bv[m] = unpack16(s4 == 0 ? bq[m].x : s4 == 1 ? bq[m].y : s4 == 2 ? bq[m].z : bq[m].w);
+          av[m] = s2 == 0 ? fp4_operand(aq[m].x, aq[m].y) : fp4_operand(aq[m].z, aq[m].w);
+          bv[m] = s2 == 0 ? fp4_operand(bq[m].x, bq[m].y) : fp4_operand(bq[m].z, bq[m].w);
         }
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int n = 0; n < 4; ++n)
-            cnt[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[m], bv[n], cnt[m][n], 0, 0, 0);
+          for (int n = 0; n < 4; ++n)   // cbsz = blgp = 4: A, B in fp4; E8M0 scales 127 = 1.0
+            cnt[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av[m], bv[n], cnt[m][n], 4, 4, 0, 127, 0, 127);
       }
     }
   }
@@ -1272,9 +1282,9 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const int cb = 4 * qr + m, ib = 4 * qc + n;
-        const v4i c = cnt[m][n];
-        const int2 packed = {(int)((uint32_t)(c[0] & 0xffff) | ((uint32_t)c[1] << 16)),
-                             (int)((uint32_t)(c[2] & 0xffff) | ((uint32_t)c[3] << 16))};
+        const v4f c = cnt[m][n];
+        const int2 packed = {(int)((uint32_t)((int)c[0] & 0xffff) | ((uint32_t)(int)c[1] << 16)),
+                             (int)((uint32_t)((int)c[2] & 0xffff) | ((uint32_t)(int)c[3] << 16))};
         *reinterpret_cast<int2*>(kt + ((ib * 8 + cb) * 64 + l) * 4) = packed;
       }
   } else if (compute) {
@@ -1283,7 +1293,7 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
   tr.done(WGT_SYS, J, I, b);
 }
 
-__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4i (&cnt)[4][4], int64_t b, int J, int qr, int qc,
+__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
                                        int l) {
   const double* sc = a.scal + b * SCAL;
   const int64_t j0 = (int64_t)J * TILE;
@@ -1304,7 +1314,7 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4i (&cnt)[4][4]
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * cb + (l >> 4) + 4 * r;
         const int64_t gi = j0 + cl;
-        const double kv = grm_value(cnt[m][n][r], ub[cl], uj, sa_, cN, invd, sm);
+        const double kv = grm_value((int32_t)cnt[m][n][r], ub[cl], uj, sa_, cN, invd, sm);
         const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
         Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
       }
