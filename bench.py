@@ -2,8 +2,9 @@
 panel k = 1000, DE population 256 per GPU), one process per GPU.
 
 A "step" is one generation's fitness evaluation of the population: for every
-individual the exact-integer system tiles on int8 MFMA (SNP-space form at k < n_T,
-as sklearn's Ridge solves it; kernel/GRM form otherwise), the fused fp64 tile
+individual the exact-integer system tiles (SNP-space form at k < n_T, as sklearn's Ridge
+solves it, on FP4 MFMA with genotypes as e2m1 nibbles; kernel/GRM form otherwise, int8
+MFMA), the fused fp64 tile
 Cholesky, back substitution, prediction and Pearson fitness, plus (N > 1) the RCCL
 all-gather of the fp64 fitness vector.  Inputs
 (genotypes, split, the population's decoded index sets) are resident in HBM
@@ -44,6 +45,9 @@ PEAKS = {
     "fp64_mfma_tflops": 72.7, "fp64_mfma_tflops_spec": 78.6,
     "fp32_mfma_tflops": 154.6, "fp32_mfma_tflops_spec": 157.3,
     "int8_mfma_tops": 4140.0, "int8_mfma_tops_spec": 5033.0,
+    # FP4 16x16x128 (e2m1 A and B, fp32 accumulate): tools/fp4_probe.hip, 4 waves per SIMD
+    # (profiles/r02_fp4_probe.json); spec: the guide's ~10 PF dense FP4
+    "fp4_mfma_tops": 8811.0, "fp4_mfma_tops_spec": 10066.0,
     "hbm_gbs": 8000.0,
 }
 
@@ -273,7 +277,8 @@ def main():
         achieved = pd["flops"] * unpad / (pd["ms"] * 1e-3) / 1e12
     elif dom == "grm":
         bound, unit = "mfma", "TOP/s"
-        peak, peak_spec = PEAKS["int8_mfma_tops"], PEAKS["int8_mfma_tops_spec"]
+        sys_fmt = "fp4" if k < nT else "int8"
+        peak, peak_spec = PEAKS[sys_fmt + "_mfma_tops"], PEAKS[sys_fmt + "_mfma_tops_spec"]
         achieved = pd["flops"] / (pd["ms"] * 1e-3) / 1e12
     else:
         bound, peak, unit, achieved = "hbm", PEAKS["hbm_gbs"], "GB/s", pd["bytes"] / (pd["ms"] * 1e-3) / 1e9
@@ -293,11 +298,13 @@ def main():
                 mfma_busy = pm["per_class"][dom]["mfma_busy"]
         except (ValueError, OSError, KeyError):
             mfma_busy = None
-    # Whole-step lower bound of the algorithm run, per GPU: the exact int8 system (lower
-    # triangle: k^2 n_T int ops), the fp64 Cholesky (k^3 / 3), one read of the factor for the
-    # back substitution (k^2 / 2 doubles), each at its measured peak.
+    # Whole-step lower bound of the algorithm run, per GPU: the exact system tiles (lower
+    # triangle: k^2 n_T ops; FP4 MFMA in the SNP-space form, int8 in the kernel form), the fp64
+    # Cholesky (k^3 / 3), one read of the factor for the back substitution (k^2 / 2 doubles),
+    # each at its measured peak.
     m_sys = min(k, nT)
-    t_int8 = pop * float(m_sys) ** 2 * (nT if k < nT else k) / (PEAKS["int8_mfma_tops"] * 1e12)
+    sys_peak = PEAKS["fp4_mfma_tops"] if k < nT else PEAKS["int8_mfma_tops"]
+    t_int8 = pop * float(m_sys) ** 2 * (nT if k < nT else k) / (sys_peak * 1e12)
     t_fp64 = pop * float(m_sys) ** 3 / 3.0 / (PEAKS["fp64_mfma_tflops"] * 1e12)
     t_hbm = pop * float(m_sys) ** 2 / 2.0 * 8.0 / (PEAKS["hbm_gbs"] * 1e9)
     step_bound_ms = (t_int8 + t_fp64 + t_hbm) * 1e3
@@ -312,7 +319,8 @@ def main():
                 "peak_source": "measured on the box (tools/mfma_peak.hip, profiles/r02_mfma_peak.json)",
                 "peak_spec": peak_spec, "frac_spec": None if peak_spec is None else round(achieved / peak_spec, 4),
                 "flops": "algorithmic: library tile count x (k/ns)^3 = %.4f" % unpad,
-                "step": {"lower_bound_ms": round(step_bound_ms, 4), "int8_ms": round(t_int8 * 1e3, 4),
+                "step": {"lower_bound_ms": round(step_bound_ms, 4), "system_tiles_ms": round(t_int8 * 1e3, 4),
+                         "system_tiles_mfma": "fp4" if k < nT else "int8",
                          "fp64_ms": round(t_fp64 * 1e3, 4), "hbm_ms": round(t_hbm * 1e3, 4)},
                 "fp32_roofline_frac_canonical": None}
     step_ms = {c: round(prof[c]["ms"] / args.steps, 4) for c in prof}
@@ -329,7 +337,8 @@ def main():
             "value": round(value, 2), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "int8 GRM (exact int32 accumulate) + f64 Cholesky/solve",
+            "dtype": ("fp4 e2m1 system tiles (exact integer genotype products, fp32 accumulate)" if k < nT else
+                      "int8 GRM (exact int32 accumulate)") + " + f64 Cholesky/solve",
             "data": "synthetic (Binomial(2, U(0.05,0.5)) genotypes, N(0,1) phenotype, RandomKey individuals)",
             "config": {"workload": f"{args.config}: {n} animals x {P} SNPs, panel k={k}, pop {pop} per GPU, "
                                    f"n_train={nT}, n_valid={nV}, h2={args.h2}"
