@@ -22,7 +22,7 @@ python3 tools/pmc_mfma.py $M --out $O/pmc_mfma_$TAG.json || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o trace --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --pmc-json $O/pmc_traffic_$TAG.json --pmc-mfma-json $O/pmc_mfma_$TAG.json > $O/prof_bench_$TAG.log 2>&1 || { echo "kernel-trace failed"; tail -20 $O/prof_bench_$TAG.log; exit 1; }
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --pmc-json $O/pmc_traffic_$TAG.json --pmc-mfma-json $O/pmc_mfma_$TAG.json > $O/bench_$TAG.log 2> $O/bench_$TAG.err || { tail -20 $O/bench_$TAG.err; exit 1; }
 tail -1 $O/bench_$TAG.log | cut -c1-300
-timeout -k 10 200 python tools/generation_bench.py > $O/generation_$TAG.log 2>&1 || { tail -20 $O/generation_$TAG.log; exit 1; }
+timeout -k 10 200 python tools/generation_bench.py 12 > $O/generation_$TAG.log 2>&1 || { tail -20 $O/generation_$TAG.log; exit 1; }
 tail -1 $O/generation_$TAG.log
 timeout -k 10 300 python tools/intracv_bench.py > $O/intracv_$TAG.log 2>&1 || { tail -20 $O/intracv_$TAG.log; exit 1; }
 grep config $O/intracv_$TAG.log
@@ -33,4 +33,5 @@ timeout -k 10 300 python bench.py --config config5 --steps 10 --warmup 3 > $O/be
 timeout -k 10 300 python bench.py --pop 128 --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_pop128_$TAG.log 2> $O/bench_pop128_$TAG.err || { tail -20 $O/bench_pop128_$TAG.err; exit 1; }
 for c in config4 config5 pop128; do tail -1 $O/bench_${c}_$TAG.log | cut -c1-200; done
 timeout -k 10 100 ./tools/mfma_peak > $O/mfma_peak_$TAG.json 2>&1 || exit 1
+timeout -k 10 100 ./tools/fp4_probe > $O/fp4_probe_$TAG.json 2>&1 || exit 1
 echo evidence done
