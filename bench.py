@@ -46,7 +46,7 @@ PEAKS = {
     "fp32_mfma_tflops": 154.6, "fp32_mfma_tflops_spec": 157.3,
     "int8_mfma_tops": 4140.0, "int8_mfma_tops_spec": 5033.0,
     # FP4 16x16x128 (e2m1 A and B, fp32 accumulate): tools/fp4_probe.hip, 4 waves per SIMD
-    # (profiles/r02_fp4_probe.json); spec: the guide's ~10 PF dense FP4
+    # (profiles/r02b_fp4_probe.json); spec: the guide's ~10 PF dense FP4
     "fp4_mfma_tops": 8811.0, "fp4_mfma_tops_spec": 10066.0,
     "hbm_gbs": 8000.0,
 }
