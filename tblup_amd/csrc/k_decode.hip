@@ -6,7 +6,7 @@
 // gives the same set whenever no tie straddles the threshold (continuous keys).
 //
 // One 1024-thread workgroup per individual:
-//   1. fast path: a strided sample (<= 4096 keys) in LDS gives a threshold with ~1.25 k
+//   1. fast path: a strided sample (<= 4096 keys, in runs of 8) in LDS gives a threshold with ~1.25 k
 //      keys above it; one pass over the row collects them in LDS; an exact radix select
 //      among those candidates picks the k largest (one read of the 400 KB row at d = 50k)
 //   2. fallback (candidates < k or > 8192, or a full-key tie at the k-th key): MSB-first
@@ -115,9 +115,15 @@ __global__ __launch_bounds__(DTH) void k_decode_topk(const double* __restrict__ 
   // cover k, overflow the 8192 slots, or the k-th key is tied at full 64 bits.
   __shared__ int fast_sh;
   {
+    // the sample: runs of 8 consecutive keys (one 64-B line) every 8 s keys, so it reads about
+    // 1/s of the row's lines (a single key every s touched up to one line per sample, more
+    // bytes than the row itself at s >= 8); slots past the row hold 0, below every key
     const int64_t s = (d + 4095) / 4096;
-    const int64_t ns = (d + s - 1) / s;
-    for (int64_t j = t; j < ns; j += DTH) sk[j] = ord_key(row[j * s]);
+    const int64_t ns = 8 * ((d + 8 * s - 1) / (8 * s));
+    for (int64_t j = t; j < ns; j += DTH) {
+      const int64_t i = (j >> 3) * (8 * s) + (j & 7);
+      sk[j] = i < d ? ord_key(row[i]) : 0ull;
+    }
     __syncthreads();
     int64_t r = (5 * k) / (4 * s) + 8;
     r = r < ns ? r : ns;
