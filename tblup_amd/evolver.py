@@ -201,6 +201,74 @@ def _mark(t0, name):
     return t
 
 
+class _RowBlocks:
+    """Page-locked blocks (one per generation) whose rows are children's genomes.
+
+    A row is a view, so a block stays allocated while any genome in it lives (the reference
+    gives every child its own array, individual.py:110-118; a view is one as far as any
+    reader can tell: disjoint rows, float64, writable).  DE selection leaves survivors spread
+    over older blocks: when more than `keep` older blocks are still referenced by the
+    population, the least-referenced ones are compacted -- those individuals' genomes are
+    replaced by equal own copies (set_internal_genome, individual.py:100-101) -- so at most
+    keep + 1 generations stay page-locked.  Freed blocks go back to torch's caching host
+    allocator and are reused without new page-locking."""
+
+    def __init__(self, keep=8):
+        self.keep = keep
+        self._reg = {}   # id(block) -> weakref(block)
+
+    def rows(self, block):
+        import weakref
+        self._reg[id(block)] = weakref.ref(block)
+        return [track(block[i]) for i in range(block.shape[0])]
+
+    def _block_of(self, g):
+        b = g
+        while isinstance(b, np.ndarray):
+            r = self._reg.get(id(b))
+            if r is not None and r() is b:
+                return b
+            b = b.base
+        return None
+
+    def compact(self, individuals, store=None):
+        """Blocks that only a few members of the population still use (<= n / 64 rows), and
+        the least-used ones beyond `keep`, give those members own copies (page-locked
+        buffers from torch's caching allocator: no page faults); the key store keeps their
+        device rows."""
+        self._reg = {k: r for k, r in self._reg.items() if r() is not None}
+        if not self._reg:
+            return
+        users = {}
+        for indv in individuals:
+            g = getattr(indv, "_genome", None)
+            blk = self._block_of(g) if isinstance(g, np.ndarray) else None
+            if blk is not None:
+                users.setdefault(id(blk), []).append(indv)
+        order = sorted(users, key=lambda k: len(users[k]))
+        few = max(1, len(individuals) // 64)
+        drop = [k for i, k in enumerate(order) if len(users[k]) <= few or i < len(order) - self.keep]
+        if not drop:
+            return
+        import torch
+        for k in drop:
+            for indv in users[k]:
+                old = indv._genome
+                if indv.get_internal_genome() is not old:   # RandomKey / Index semantics only
+                    continue
+                buf = torch.empty(old.shape[0], dtype=torch.float64, pin_memory=True).numpy()
+                np.copyto(buf, old)
+                new = track(buf)
+                indv.set_internal_genome(new)
+                if store is not None:
+                    store.rebind(indv, old, new)
+
+
+_BLOCKS = _RowBlocks()
+
+# a generation's float64 children up to this many bytes cross as one page-locked block
+_BLOCK_MAX = int(os.environ.get("TBLUP_BLOCK_ROWS_MB", "1024")) << 20
+
 # children of a generation up to this many bytes get page-locked genome buffers
 _PINNED_ROWS_MAX = int(os.environ.get("TBLUP_PINNED_ROWS_MB", "2048")) << 20
 
@@ -249,6 +317,9 @@ class _GpuDEEvolver(Evolver):
         t = time.perf_counter()
         mi = 5 if population.generation % 5 == 0 else self.mutation_intensity
         n = len(population)
+        import torch
+        _BLOCKS.compact([population[i] for i in range(n)], DeviceKeyStore.get(GpuDEStep.get(self.device).device))
+        t = _mark(t, "ev_compact")
         genomes = [population[i].get_internal_genome() for i in range(n)]
         L = len(genomes[0])
         if any(len(g) != L for g in genomes):
@@ -256,12 +327,14 @@ class _GpuDEEvolver(Evolver):
         donors, fixed = self._donors(population, L)
         clip = self._clip()
         dtypes = _child_dtypes(genomes, donors, self.strategy, mi, clip)
+        t = _mark(t, "ev_donors")
         step = GpuDEStep.get(self.device)
         import torch
         store = DeviceKeyStore.get(step.device)
         inds = [population[i] for i in range(n)]
         with torch.cuda.device(step.device), torch.cuda.stream(work_stream(step.device)):
             parents = store.gather(inds, L, host_rows=lambda i: genomes[i])   # device-resident parents
+            t = _mark(t, "ev_gather")
             children = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate, clip,
                                         self.dimensionality - 1)
             t = _mark(t, "ev_prepare_step")
@@ -271,10 +344,12 @@ class _GpuDEEvolver(Evolver):
             spec = getattr(evaluator, "_speculate", None)
             speculated = bool(spec is not None and dtypes is None and spec(inds, children, population.generation))
             t = _mark(t, "ev_speculate")
-            # children to the host in chunks, each followed by an event, so the per-row copies of
-            # one chunk overlap the transfer of the next
+            # float64 children: one DMA into a page-locked block whose rows become the children's
+            # genomes (views: no host copy); otherwise chunks, each followed by an event, so the
+            # per-row copies of one chunk overlap the transfer of the next
+            block_rows = dtypes is None and n * L * 8 <= _BLOCK_MAX
             host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
-            nchunk = 8 if n >= 16 else 1
+            nchunk = 1 if block_rows else (8 if n >= 16 else 1)
             rows = (n + nchunk - 1) // nchunk
             events = []
             for c in range(nchunk):
@@ -288,13 +363,16 @@ class _GpuDEEvolver(Evolver):
         # the candidates (new uids, the parent's other attributes) while the transfer runs
         next_pop = [_copy_individual(population[i]) for i in range(n)]
         t = _mark(t, "ev_candidates")
-        # an own array per child (a row view would pin the whole generation's block); float64
-        # rows go into page-locked buffers from torch's caching host allocator, which hands back
-        # the buffers of dead genomes: no page faults on the copy
-        dest = None
-        if dtypes is None and n * L * 8 <= _PINNED_ROWS_MAX:
-            dest = [torch.empty(L, dtype=torch.float64, pin_memory=True).numpy() for _ in range(n)]
-        arrays = _copy_rows(host.numpy(), dtypes, ready=[ev.synchronize for ev in events], dest=dest)
+        if block_rows:
+            events[-1].synchronize()
+            arrays = _BLOCKS.rows(host.numpy())
+        else:
+            # an own array per child; float64 rows go into page-locked buffers from torch's caching
+            # host allocator, which hands back the buffers of dead genomes: no page faults on the copy
+            dest = None
+            if dtypes is None and n * L * 8 <= _PINNED_ROWS_MAX:
+                dest = [torch.empty(L, dtype=torch.float64, pin_memory=True).numpy() for _ in range(n)]
+            arrays = _copy_rows(host.numpy(), dtypes, ready=[ev.synchronize for ev in events], dest=dest)
         t = _mark(t, "ev_arrays")
         for i in range(n):
             next_pop[i].set_internal_genome(arrays[i])

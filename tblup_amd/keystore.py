@@ -138,6 +138,13 @@ class DeviceKeyStore:
             return None
         return tensor, row
 
+    def rebind(self, indv, old, new):
+        """indv's genome array `old` was replaced by the equal-valued TrackedGenome `new`
+        (the evolver compacting page-locked blocks): keep its device row."""
+        e = self._entries.get(indv.uid)
+        if e is not None and e[2]() is old and not old._stale:
+            self._entries[indv.uid] = (e[0], e[1], weakref.ref(new), e[3])
+
     def rows(self, individuals):
         """(tensor, row) per individual (None where absent)."""
         return [self.lookup(i) for i in individuals]
