@@ -247,7 +247,10 @@ class _RowBlocks:
                 users.setdefault(id(blk), []).append(indv)
         order = sorted(users, key=lambda k: len(users[k]))
         few = max(1, len(individuals) // 64)
-        drop = [k for i, k in enumerate(order) if len(users[k]) <= few or i < len(order) - self.keep]
+        # at most `keep` older blocks, fewer when they are large (about 2 GiB page-locked)
+        big = max(r().nbytes for r in self._reg.values())
+        keep = max(1, min(self.keep, (2 << 30) // max(big, 1)))
+        drop = [k for i, k in enumerate(order) if len(users[k]) <= few or i < len(order) - keep]
         if not drop:
             return
         import torch
