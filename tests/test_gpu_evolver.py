@@ -209,3 +209,60 @@ def test_gpu_de_small_shapes_vs_oracle(gpu, L, pop, pre):
         for k, w in zip(kids, want):
             assert np.array_equal(k.get_internal_genome(), w), (strat, L, pop, pre)
 
+
+
+def test_gpu_block_rows_many_generations(gpu, tmp_path):
+    """14 generations of evolve -> evaluate -> select with the children's genomes as rows of
+    page-locked per-generation blocks: equal to the host-oracle loop generation by generation,
+    the blocks still in use stay bounded (compaction), compacted genomes keep their device
+    rows, and rows are independent arrays (an in-place write touches one child only)."""
+    from oracle import blup_oracle as O
+    from tblup_amd import evolver as EVM
+    from tblup_amd.evaluator import BlupParallelEvaluator
+    from tblup_amd.keystore import DeviceKeyStore
+    rng = np.random.default_rng(12)
+    n, p, k, pop, gens = 300, 2000, 100, 48, 14
+    geno = O.synth_geno(rng, n, p)
+    pheno = rng.standard_normal(n)
+    np.save(tmp_path / "g.npy", geno)
+    np.save(tmp_path / "y.npy", pheno)
+    keys0 = rng.uniform(size=(pop, p))
+
+    def run(use_gpu_de):
+        random.seed(9)
+        np.random.seed(9)
+        ev = BlupParallelEvaluator(str(tmp_path / "g.npy"), str(tmp_path / "y.npy"), 0.4)
+        inds = [RandomKeyIndividual(keys0[i].copy(), k) for i in range(pop)]
+        fits, alive = [], []
+        with ev:
+            popn = Pop(inds, 0)
+            ev.evaluate(popn, popn, 0)
+            evo = _evolver("de_rand_1", p, 0.8, 0.5, False)
+            for g in range(1, gens + 1):
+                popn.generation = g
+                if use_gpu_de:
+                    kids = evo.evolve(popn)
+                    assert all(h is not None for h in DeviceKeyStore.get(0).rows(popn.population))
+                    alive.append(sum(r() is not None for r in EVM._BLOCKS._reg.values()))
+                else:
+                    DeviceKeyStore.get(0).clear()
+                    want = D.de_generation([x.get_internal_genome() for x in popn.population],
+                                           [x.fitness for x in popn.population], g, "de_rand_1", p, 0.8, 0.5, False)
+                    kids = [RandomKeyIndividual(w, k) for w in want]
+                ev.evaluate(popn, kids, g)
+                popn.population = [c if c.fitness > q.fitness else q for q, c in zip(popn.population, kids)]
+                fits.append([x.fitness for x in kids])
+            genomes = [x.get_internal_genome().copy() for x in popn.population]
+            if use_gpu_de:
+                a, b = popn.population[0], popn.population[1]
+                before = b.get_internal_genome().copy()
+                a.get_internal_genome()[0] = 0.123   # an in-place write, as Individual.__setitem__ does
+                assert np.array_equal(b.get_internal_genome(), before)
+        return fits, genomes, alive
+
+    f_gpu, g_gpu, alive = run(True)
+    f_ref, g_ref, _ = run(False)
+    assert f_gpu == f_ref
+    for x, y in zip(g_gpu, g_ref):
+        assert np.array_equal(x, y)
+    assert max(alive) <= EVM._BLOCKS.keep + 2, alive
