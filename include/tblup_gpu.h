@@ -230,6 +230,14 @@ int tblup_de_step_device(tblup_ctx* ctx, int strategy, const double* d_parents, 
                          const int32_t* donors, const int64_t* fixed, double F, double cr, int clip, double clip_hi,
                          uint32_t* mt_key, int32_t* mt_pos, double* d_children, int64_t ldc, void* stream);
 
+/* Enqueue dst row i (L doubles, row stride ldd) = the device row d_src_rows[i] (a host array of
+ * n device pointers, each to L doubles on this context's device) on `stream` (NULL = the
+ * context's stream): one launch per 128 rows.  The DE step's parents gathered from the rows
+ * where earlier generations' children still sit on the device (tblup_amd.keystore), as the
+ * reference's evolver reads population[i].get_internal_genome() (evolver.py:130-140). */
+int tblup_gather_rows(tblup_ctx* ctx, double* d_dst, int64_t n, int64_t L, int64_t ldd, const double* const* d_src_rows,
+                      void* stream);
+
 /* Host-only: advance numpy's MT19937 (key[624], pos) state by n_words 32-bit outputs
  * (GF(2) jump-ahead; used to check the DE step's stream arithmetic without a GPU). */
 int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint32_t* key_out, int32_t* pos_out);

@@ -988,6 +988,26 @@ int tblup_de_step(tblup_ctx* c, int strategy, const double* parents, int64_t pop
   return 0;
 }
 
+int tblup_gather_rows(tblup_ctx* c, double* d_dst, int64_t n, int64_t L, int64_t ldd, const double* const* d_src_rows,
+                      void* stream) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (n < 0 || L < 0 || ldd < L) return fail(TBLUP_ERR_ARG, "need n >= 0, 0 <= L <= ldd");
+  if (n == 0 || L == 0) return 0;
+  if (!d_dst || !d_src_rows) return fail(TBLUP_ERR_ARG, "null destination / source table");
+  for (int64_t i = 0; i < n; ++i)
+    if (!d_src_rows[i]) return fail(TBLUP_ERR_ARG, "null source row");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  for (int64_t r0 = 0; r0 < n; r0 += ROWPTRS) {
+    const int nr = (int)std::min<int64_t>(ROWPTRS, n - r0);
+    RowPtrs t{};
+    for (int k = 0; k < nr; ++k) t.p[k] = d_src_rows[r0 + k];
+    HIPCHK(launch_gather_rows(d_dst + r0 * ldd, ldd, L, t, nr, s));
+  }
+  return 0;
+}
+
 int tblup_get_wg_trace(tblup_ctx* c, uint64_t* out, int64_t cap, int64_t* n_records) {
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;

@@ -249,4 +249,33 @@ hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, 
   return hipGetLastError();
 }
 
+namespace {
+// dst row r (L doubles) = the device row src.p[r]; 16-B loads and stores when L is even and
+// the rows are 16-B aligned, else 8-B
+__global__ __launch_bounds__(256) void k_gather_rows(double* __restrict__ dst, int64_t ldd, int64_t L, RowPtrs src,
+                                                     int vec2) {
+  const int64_t r = blockIdx.y;
+  const double* sr = src.p[r];
+  double* dr = dst + r * ldd;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  if (vec2) {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; 2 * j < L; j += stride)
+      reinterpret_cast<v2d*>(dr)[j] = reinterpret_cast<const v2d*>(sr)[j];
+  } else {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < L; j += stride) dr[j] = sr[j];
+  }
+}
+}  // namespace
+
+hipError_t launch_gather_rows(double* dst, int64_t ldd, int64_t L, const RowPtrs& src, int nr, hipStream_t s) {
+  if (nr <= 0 || L <= 0) return hipSuccess;
+  bool vec2 = (L % 2 == 0) && (ldd % 2 == 0) && ((uintptr_t)dst % 16 == 0);
+  for (int r = 0; r < nr; ++r) vec2 = vec2 && ((uintptr_t)src.p[r] % 16 == 0);
+  const int64_t per = vec2 ? L / 2 : L;
+  const int64_t nb = (per + 256 * 4 - 1) / (256 * 4);   // ~4 elements per thread
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)(nb < 256 ? nb : 256), (unsigned)nr), dim3(256), 0, s, dst, ldd, L,
+                     src, vec2 ? 1 : 0);
+  return hipGetLastError();
+}
+
 }  // namespace tblup

@@ -193,6 +193,14 @@ hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, 
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
                           uint32_t* key_out, int32_t* pos_out, hipStream_t s);
 
+// ---- launcher (k_de.hip): rows from scattered device rows into one matrix (up to ROWPTRS rows
+//      per launch, source pointers in the kernel arguments) ----
+constexpr int ROWPTRS = 128;
+struct RowPtrs {
+  const double* p[ROWPTRS];
+};
+hipError_t launch_gather_rows(double* dst, int64_t ldd, int64_t L, const RowPtrs& src, int nr, hipStream_t s);
+
 // ---- launcher (k_scan.hip): per-SNP sums over a set of animals (seeder GWAS metric) ----
 hipError_t launch_snp_scan(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rows, int64_t nr,
                            const double* yc, int64_t* sx, int64_t* sxx, double* sxy, hipStream_t s);

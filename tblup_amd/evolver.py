@@ -125,6 +125,15 @@ class GpuDEStep:
         cur.wait_stream(ws)   # (the call synchronised ws already; keeps later caller work ordered)
         return children
 
+    def gather_rows(self, out, ptrs):
+        """out[i] = the device row at address ptrs[i] (this device), on torch's current stream."""
+        import torch
+        n, L = out.shape
+        tab = (ctypes.c_void_p * n)(*ptrs)
+        _native.check("tblup_gather_rows", self._lib.tblup_gather_rows(
+            self._ctx, ctypes.c_void_p(out.data_ptr()), n, L, out.stride(0), tab,
+            ctypes.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)))
+
     def close(self):
         if self._ctx:
             self._lib.tblup_ctx_destroy(self._ctx)
@@ -336,7 +345,8 @@ class _GpuDEEvolver(Evolver):
         store = DeviceKeyStore.get(step.device)
         inds = [population[i] for i in range(n)]
         with torch.cuda.device(step.device), torch.cuda.stream(work_stream(step.device)):
-            parents = store.gather(inds, L, host_rows=lambda i: genomes[i])   # device-resident parents
+            parents = store.gather(inds, L, host_rows=lambda i: genomes[i],
+                                   copy_rows=step.gather_rows)   # device-resident parents
             t = _mark(t, "ev_gather")
             children = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate, clip,
                                         self.dimensionality - 1)

@@ -149,10 +149,11 @@ class DeviceKeyStore:
         """(tensor, row) per individual (None where absent)."""
         return [self.lookup(i) for i in individuals]
 
-    def gather(self, individuals, L, host_rows=None):
+    def gather(self, individuals, L, host_rows=None, copy_rows=None):
         """A contiguous (len(individuals) x L) float64 device tensor of their internal genomes;
         rows not in the store come from host_rows(i) (None -> return None if any is missing).
-        No copy when the individuals are exactly one recorded block in order."""
+        No copy when the individuals are exactly one recorded block in order.  copy_rows(out,
+        pointers): one native gather of the recorded rows (pointer 0 = row to skip)."""
         import torch
         hits = self.rows(individuals)
         n = len(individuals)
@@ -163,6 +164,16 @@ class DeviceKeyStore:
         if host_rows is None and any(h is None for h in hits):
             return None
         out = torch.empty((n, L), dtype=torch.float64, device="cuda:%d" % self.device)
+        if copy_rows is not None and all(h is None or (h[0].dim() == 2 and h[0].shape[1] == L and h[0].stride(1) == 1)
+                                         for h in hits):
+            ptrs = [0 if h is None else h[0].data_ptr() + 8 * h[1] * h[0].stride(0) for h in hits]
+            missing = [i for i, q in enumerate(ptrs) if not q]
+            if len(missing) < n:
+                any_row = next(q for q in ptrs if q)
+                copy_rows(out, [q if q else any_row for q in ptrs])   # missing slots overwritten below
+            if missing:
+                self._fill_missing(out, missing, host_rows)
+            return out
         by_tensor = {}
         missing = []
         for i, h in enumerate(hits):

@@ -266,3 +266,20 @@ def test_gpu_block_rows_many_generations(gpu, tmp_path):
     for x, y in zip(g_gpu, g_ref):
         assert np.array_equal(x, y)
     assert max(alive) <= EVM._BLOCKS.keep + 2, alive
+
+
+@pytest.mark.parametrize("n,L,shift", [(1, 1, 0), (5, 7, 1), (130, 1000, 0), (300, 50_000, 0), (129, 33, 1)])
+def test_gather_rows(gpu, n, L, shift):
+    """tblup_gather_rows: rows scattered over several device tensors (odd L, rows starting
+    8 B off 16-B alignment, > 128 rows in several launches) gathered exactly."""
+    import torch
+    from tblup_amd.evolver import GpuDEStep
+    step = GpuDEStep.get(0)
+    srcs = [torch.rand(n, L + shift, dtype=torch.float64, device="cuda") for _ in range(3)]
+    rng = np.random.default_rng(n + L)
+    pick = [(int(rng.integers(3)), int(rng.integers(n))) for _ in range(n)]
+    ptrs = [srcs[s].data_ptr() + 8 * (r * (L + shift) + shift) for s, r in pick]
+    out = torch.full((n, L), -1.0, dtype=torch.float64, device="cuda")
+    step.gather_rows(out, ptrs)
+    want = torch.stack([srcs[s][r, shift:] for s, r in pick])
+    assert torch.equal(out, want)
