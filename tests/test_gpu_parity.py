@@ -464,3 +464,23 @@ def test_knockout_local_search_gpu(golden_dir, gpu, tmp_path):
             mask[i] = True
     np.testing.assert_array_equal(genome, full[mask])
     assert abs(fit - bf) <= FIT_ATOL
+
+
+def test_primal_counts_near_int16_limit(gpu):
+    """SNP-space form at n_T = 8000 (the system-tile counts reach ~3.5 n_T = 28k, just under the
+    int16 `kc` store and far inside fp32's exact integers on the FP4 MFMA path): fitness and
+    EBVs vs the oracle's restatement of snp_blup (evaluator.py:288-314) on the same panel."""
+    from tblup_amd.engine import GpuBlupEngine
+    rng = np.random.default_rng(33)
+    n, p, k = 9000, 1200, 400
+    geno = O.synth_geno(rng, n, p, maf_lo=0.6, maf_hi=0.95)
+    pheno = rng.standard_normal(n)
+    perm = rng.permutation(n)
+    T, V = np.sort(perm[:8000]), np.sort(perm[8000:])
+    genomes = [rng.choice(p, size=k, replace=False) for _ in range(3)]
+    with GpuBlupEngine(geno, pheno) as eng:
+        fit, ebv = eng.evaluate(genomes, T, V, 0.4, return_ebv=True)
+    for i, g in enumerate(genomes):
+        f_ref, e_ref = O.snp_blup(g, T, V, geno, pheno, 0.4, return_ebv=True)
+        assert abs(fit[i] - f_ref) <= FIT_ATOL
+        assert _relmax(ebv[i], e_ref) <= EBV_RTOL
