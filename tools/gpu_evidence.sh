@@ -22,7 +22,7 @@ python3 tools/pmc_mfma.py $M --out $O/pmc_mfma_$TAG.json || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o trace --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --pmc-json $O/pmc_traffic_$TAG.json --pmc-mfma-json $O/pmc_mfma_$TAG.json > $O/prof_bench_$TAG.log 2>&1 || { echo "kernel-trace failed"; tail -20 $O/prof_bench_$TAG.log; exit 1; }
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --pmc-json $O/pmc_traffic_$TAG.json --pmc-mfma-json $O/pmc_mfma_$TAG.json > $O/bench_$TAG.log 2> $O/bench_$TAG.err || { tail -20 $O/bench_$TAG.err; exit 1; }
 tail -1 $O/bench_$TAG.log | cut -c1-300
-timeout -k 10 200 python tools/generation_bench.py 12 > $O/generation_$TAG.log 2>&1 || { tail -20 $O/generation_$TAG.log; exit 1; }
+timeout -k 10 300 python tools/generation_bench.py 24 > $O/generation_$TAG.log 2>&1 || { tail -20 $O/generation_$TAG.log; exit 1; }
 tail -1 $O/generation_$TAG.log
 timeout -k 10 300 python tools/intracv_bench.py > $O/intracv_$TAG.log 2>&1 || { tail -20 $O/intracv_$TAG.log; exit 1; }
 grep config $O/intracv_$TAG.log
