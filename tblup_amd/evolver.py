@@ -219,10 +219,10 @@ class _RowBlocks:
     over older blocks: when more than `keep` older blocks are still referenced by the
     population, the least-referenced ones are compacted -- those individuals' genomes are
     replaced by equal own copies (set_internal_genome, individual.py:100-101) -- so at most
-    keep + 1 generations stay page-locked.  Freed blocks go back to torch's caching host
+    keep + 1 generations (about 2 GiB) stay page-locked.  Freed blocks go back to torch's caching host
     allocator and are reused without new page-locking."""
 
-    def __init__(self, keep=8):
+    def __init__(self, keep=12):
         self.keep = keep
         self._reg = {}   # id(block) -> weakref(block)
 
@@ -263,17 +263,22 @@ class _RowBlocks:
         if not drop:
             return
         import torch
-        for k in drop:
-            for indv in users[k]:
-                old = indv._genome
-                if indv.get_internal_genome() is not old:   # RandomKey / Index semantics only
-                    continue
-                buf = torch.empty(old.shape[0], dtype=torch.float64, pin_memory=True).numpy()
-                np.copyto(buf, old)
-                new = track(buf)
-                indv.set_internal_genome(new)
-                if store is not None:
-                    store.rebind(indv, old, new)
+        moved = [indv for k in drop for indv in users[k]
+                 if indv.get_internal_genome() is indv._genome]   # RandomKey / Index semantics only
+        bufs = [torch.empty(indv._genome.shape[0], dtype=torch.float64, pin_memory=True).numpy() for indv in moved]
+
+        def copy(j):
+            np.copyto(bufs[j], moved[j]._genome)
+        if len(moved) > 4:
+            list(_pool().map(copy, range(len(moved))))
+        else:
+            for j in range(len(moved)):
+                copy(j)
+        for indv, buf in zip(moved, bufs):
+            old, new = indv._genome, track(buf)
+            indv.set_internal_genome(new)
+            if store is not None:
+                store.rebind(indv, old, new)
 
 
 _BLOCKS = _RowBlocks()
