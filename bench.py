@@ -55,8 +55,8 @@ PEAKS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
     ap.add_argument("--pop", type=int, default=None, help="individuals per GPU (default: the config's)")
     ap.add_argument("--seed", type=int, default=1234)
