@@ -242,6 +242,17 @@ int tblup_gather_rows(tblup_ctx* ctx, double* d_dst, int64_t n, int64_t L, int64
  * (GF(2) jump-ahead; used to check the DE step's stream arithmetic without a GPU). */
 int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint32_t* key_out, int32_t* pos_out);
 
+/* Host-only: one DE generation's python-`random` draws, the loops of DERandOneEvolver /
+ * DECurrentToBestOneEvolver.evolve that feed tblup_de_step: per individual i the donors
+ * (exclusive_randrange, utils.py:21-36; rand/1: a, b, c, evolver.py:118-121; current-to-best/1:
+ * a, b beside `best`, evolver.py:199-203, donors[i] = (best, a, b)) and then fixed[i] =
+ * random.randrange(0, L) (evolver.py:76).  py_mt / py_index hold CPython's MT19937 state
+ * (random.getstate()[1]: 624 words, then the index) and are advanced in place exactly as the
+ * python loop advances it (random.setstate continues the stream).  best = -1 for rand/1.
+ * Needs 4 <= pop (smaller populations raise the reference's assertion: keep those in python). */
+int tblup_de_donors(int strategy, int64_t pop, int64_t L, int32_t best, uint32_t* py_mt, int32_t* py_index,
+                    int32_t* donors, int64_t* fixed);
+
 /* Index-error flag of the device entry points: synchronises `stream` (NULL = the context's
  * stream), sets *flag = 1 if any individual evaluated since the last call had an index
  * outside [-n_snps, n_snps) (its fitness is NaN), and clears the flag. */

@@ -55,6 +55,7 @@ SIGNATURES = {
     "tblup_grm": (_c.c_int, [_P, _I64P, _c.c_int64, _DP]),
     "tblup_snp_scan": (_c.c_int, [_P, _I64P, _c.c_int64, _DP, _I64P, _I64P, _DP]),
     "tblup_mt19937_jump": (_c.c_int, [_U32P, _c.c_int32, _c.c_uint64, _U32P, _I32P]),
+    "tblup_de_donors": (_c.c_int, [_c.c_int, _c.c_int64, _c.c_int64, _c.c_int32, _U32P, _I32P, _I32P, _I64P]),
     "tblup_gather_rows": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p,
                                      _c.c_void_p]),
 }

@@ -908,6 +908,21 @@ int tblup_mt19937_jump(const uint32_t* key, int32_t pos, uint64_t n_words, uint3
   return 0;
 }
 
+int tblup_de_donors(int strategy, int64_t pop, int64_t L, int32_t best, uint32_t* py_mt, int32_t* py_index,
+                    int32_t* donors, int64_t* fixed) {
+  g_err.clear();
+  if (strategy != TBLUP_DE_RAND_1 && strategy != TBLUP_DE_CURRENT_TO_BEST_1)
+    return fail(TBLUP_ERR_ARG, "unknown DE strategy");
+  if (pop < 4 || pop > 65535 || L < 1 || L >= ((int64_t)1 << 32))
+    return fail(TBLUP_ERR_ARG, "need 4 <= pop <= 65535 and 1 <= L < 2^32");
+  if (!py_mt || !py_index || !donors || !fixed) return fail(TBLUP_ERR_ARG, "null py_mt/py_index/donors/fixed");
+  if (*py_index < 0 || *py_index > 624) return fail(TBLUP_ERR_ARG, "py_index must be in [0, 624]");
+  if (strategy == TBLUP_DE_CURRENT_TO_BEST_1 ? (best < 0 || best >= pop) : best != -1)
+    return fail(TBLUP_ERR_ARG, "best must be in [0, pop) for current-to-best/1 and -1 for rand/1");
+  tblup_mt::py_random_donors(py_mt, py_index, pop, L, best, donors, fixed);
+  return 0;
+}
+
 static int validate_de(int strategy, int64_t pop, int64_t L, const int32_t* donors, const int64_t* fixed, double cr,
                        const uint32_t* mt_key, const int32_t* mt_pos) {
   if (strategy != TBLUP_DE_RAND_1 && strategy != TBLUP_DE_CURRENT_TO_BEST_1)

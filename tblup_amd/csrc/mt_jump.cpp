@@ -335,4 +335,71 @@ void jump_state(const uint32_t* key, int pos, uint64_t n_words, uint32_t* key_ou
   *pos_out = e.pos;
 }
 
+// ---- CPython's `random` (Modules/_randommodule.c of CPython 3.10): the same MT19937
+// recurrence, consumed one tempered word at a time from (mt, index); randrange(0, n) is
+// _randbelow_with_getrandbits(n): k = n.bit_length(), draw getrandbits(k) = word >> (32 - k)
+// until it is < n.  The donor loops restate utils.py:21-36 (exclusive_randrange: first draw,
+// then redraw while excluded), evolver.py:118-121 (a, b, c) and :199-203 (a, b beside the
+// best), then evolver.py:76 (fixed = randrange(0, L)), in that order per individual.
+namespace {
+
+struct PyMT {
+  uint32_t* mt;
+  int idx;
+  uint32_t word() {
+    if (idx >= MT_N) {
+      for (int k = 0; k < MT_N; ++k) mt[k] = twist(mt[k], mt[(k + 1) % MT_N], mt[(k + 397) % MT_N]);
+      idx = 0;
+    }
+    uint32_t y = mt[idx++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+  uint32_t below(uint64_t n) {   // 1 <= n < 2^32
+    const int k = 64 - __builtin_clzll(n);
+    uint32_t r = word() >> (32 - k);
+    while (r >= n) r = word() >> (32 - k);
+    return r;
+  }
+  // exclusive_randrange(0, n, ex[0..ne))
+  uint32_t excluding(uint64_t n, const int64_t* ex, int ne) {
+    for (;;) {
+      const uint32_t r = below(n);
+      bool hit = false;
+      for (int j = 0; j < ne; ++j) hit |= (int64_t)r == ex[j];
+      if (!hit) return r;
+    }
+  }
+};
+
+}  // namespace
+
+void py_random_donors(uint32_t* mt, int32_t* index, int64_t pop, int64_t L, int32_t best, int32_t* donors,
+                      int64_t* fixed) {
+  PyMT g{mt, *index};
+  for (int64_t i = 0; i < pop; ++i) {
+    if (best < 0) {
+      int64_t ex[3] = {i, 0, 0};
+      ex[1] = g.excluding(pop, ex, 1);
+      ex[2] = g.excluding(pop, ex, 2);
+      const int64_t c = g.excluding(pop, ex, 3);
+      donors[3 * i] = (int32_t)ex[1];
+      donors[3 * i + 1] = (int32_t)ex[2];
+      donors[3 * i + 2] = (int32_t)c;
+    } else {
+      int64_t ex[3] = {i, best, 0};
+      ex[2] = g.excluding(pop, ex, 2);
+      const int64_t b = g.excluding(pop, ex, 3);
+      donors[3 * i] = best;
+      donors[3 * i + 1] = (int32_t)ex[2];
+      donors[3 * i + 2] = (int32_t)b;
+    }
+    fixed[i] = g.below((uint64_t)L);
+  }
+  *index = g.idx;
+}
+
 }  // namespace tblup_mt

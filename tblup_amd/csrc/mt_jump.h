@@ -34,4 +34,10 @@ EndState end_state(int pos0, uint64_t n_words);
 // host jump of a numpy MT19937 state by n_words 32-bit outputs (tests and small cases)
 void jump_state(const uint32_t* key, int pos, uint64_t n_words, uint32_t* key_out, int* pos_out);
 
+// One DE generation's python-`random` draws (donors + the crossover's fixed position) on
+// CPython's MT19937 state (random.getstate()[1]: mt[624], index); best < 0: DE/rand/1, else
+// DE/current-to-best/1 with that best index.  Needs pop >= 4 and 1 <= L < 2^32.
+void py_random_donors(uint32_t* mt, int32_t* index, int64_t pop, int64_t L, int32_t best, int32_t* donors,
+                      int64_t* fixed);
+
 }  // namespace tblup_mt

@@ -55,6 +55,27 @@ def exclusive_randrange(begin, end, exclude):
     return r
 
 
+def _native_donors(strategy, n, L, best=-1):
+    """One generation's donor / fixed-position draws (the python loops of _donors below) on
+    CPython's MT19937 state in native code (tblup_de_donors): the same draws and the same
+    `random` state afterwards, without 4n interpreted randrange calls.  None when the loop must
+    stay in python (n < 4 raises the reference's assertion there; L >= 2^32)."""
+    if n < 4 or L >= 1 << 32:
+        return None
+    version, internal, gauss = random.getstate()
+    mt = np.array(internal[:624], dtype=np.uint32)
+    idx = np.array([internal[624]], dtype=np.int32)
+    donors = np.empty((n, 3), dtype=np.int32)
+    fixed = np.empty(n, dtype=np.int64)
+    lib = _native.load()
+    _native.check("tblup_de_donors", lib.tblup_de_donors(
+        strategy, n, L, best, mt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+        idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+        fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+    random.setstate((version, tuple(mt.tolist()) + (int(idx[0]),), gauss))
+    return donors, fixed
+
+
 class GpuDEStep:
     """A panel-less GPU context running tblup_de_step (one per process and device)."""
 
@@ -411,6 +432,9 @@ class DERandOneEvolver(_GpuDEEvolver):
 
     def _donors(self, population, L):
         n = len(population)
+        drawn = _native_donors(self.strategy, n, L)
+        if drawn is not None:
+            return drawn
         donors = np.empty((n, 3), dtype=np.int32)
         fixed = np.empty(n, dtype=np.int64)
         for i in range(n):   # de_rand_one (evolver.py:118-121) then crossover (evolver.py:76)
@@ -434,6 +458,9 @@ class DECurrentToBestOneEvolver(_GpuDEEvolver):
         n = len(population)
         best = max(population, key=lambda individual: individual.fitness)   # evolver.py:235
         best_index = population.population.index(best)                      # evolver.py:194
+        drawn = _native_donors(self.strategy, n, L, best_index)
+        if drawn is not None:
+            return drawn
         donors = np.empty((n, 3), dtype=np.int32)
         fixed = np.empty(n, dtype=np.int64)
         for i in range(n):   # evolver.py:199-203, then crossover (evolver.py:76)

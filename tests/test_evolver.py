@@ -122,3 +122,62 @@ def test_exclusive_randrange_consumes_like_reference():
     random.seed(3)
     b = [D.exclusive_randrange(0, 5, [0, 1, 2]) for _ in range(20)]
     assert a == b and all(x in (3, 4) for x in a)
+
+
+def _python_donors(strategy, n, L, best):
+    """The reference's per-individual draws in order (evolver.py:118-121 / :199-203 through
+    utils.py:21-36, then evolver.py:76's fixed position), via the oracle's exclusive_randrange."""
+    donors, fixed = [], []
+    for i in range(n):
+        if strategy == "de_rand_1":
+            a = D.exclusive_randrange(0, n, [i])
+            b = D.exclusive_randrange(0, n, [i, a])
+            c = D.exclusive_randrange(0, n, [i, a, b])
+            donors.append((a, b, c))
+        else:
+            excl = [i, best]
+            a = D.exclusive_randrange(0, n, excl)
+            excl.append(a)
+            b = D.exclusive_randrange(0, n, excl)
+            donors.append((best, a, b))
+        fixed.append(random.randrange(0, L))
+    return np.array(donors, dtype=np.int32), np.array(fixed, dtype=np.int64)
+
+
+@pytest.mark.parametrize("strategy", ["de_rand_1", "de_currenttobest_1"])
+@pytest.mark.parametrize("n,L,pre", [(4, 1, 0), (5, 2, 3), (7, 3, 623), (64, 1000, 624), (256, 50000, 17),
+                                     (1000, 3_000_000_000, 5), (300, 1 << 31, 400)])
+def test_native_donors_equal_python_random(strategy, n, L, pre):
+    """tblup_de_donors (CPython's MT19937 restated in C) draws the same donors and fixed
+    positions as the python loops and leaves `random` in the same state."""
+    from tblup_amd.evolver import _native_donors
+    code = _native.DE_STRATEGY[strategy]
+    for rep in range(3):
+        random.seed(7 * n + rep)
+        for _ in range(pre):
+            random.random()
+        best = -1 if strategy == "de_rand_1" else (rep * 37) % n
+        st = random.getstate()
+        got = _native_donors(code, n, L, best)
+        after_native = random.getstate()
+        random.setstate(st)
+        want = _python_donors(strategy, n, L, best)
+        assert got is not None
+        np.testing.assert_array_equal(got[0], want[0])
+        np.testing.assert_array_equal(got[1], want[1])
+        assert after_native == random.getstate()
+
+
+def test_native_donors_small_population_stays_in_python():
+    from tblup_amd.evolver import _native_donors
+    assert _native_donors(_native.DE_STRATEGY["de_rand_1"], 3, 10) is None
+    lib = _native.load()
+    d = np.zeros((3, 3), np.int32)
+    f = np.zeros(3, np.int64)
+    mt = np.zeros(624, np.uint32)
+    idx = np.array([624], np.int32)
+    rc = lib.tblup_de_donors(0, 3, 10, -1, mt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                             idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                             d.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                             f.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    assert rc != 0 and b"pop" in lib.tblup_last_error()
