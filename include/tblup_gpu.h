@@ -230,6 +230,18 @@ int tblup_de_step_device(tblup_ctx* ctx, int strategy, const double* d_parents, 
                          const int32_t* donors, const int64_t* fixed, double F, double cr, int clip, double clip_hi,
                          uint32_t* mt_key, int32_t* mt_pos, double* d_children, int64_t ldc, void* stream);
 
+/* tblup_de_step_device in two halves: the step and the copy of the new MT state into a
+ * page-locked context buffer are enqueued on `stream` without waiting (mt_key is read before
+ * returning; mt_pos is passed by value), and tblup_de_state_wait waits for that copy only and
+ * writes the state out.  Between the two the caller may enqueue work on the children (the
+ * evaluator's decode and evaluation, their copy to the host); one step may be pending at a time.
+ * tblup_de_step_device is the two calls back to back. */
+int tblup_de_step_device_async(tblup_ctx* ctx, int strategy, const double* d_parents, int64_t pop, int64_t L,
+                               int64_t ld, const int32_t* donors, const int64_t* fixed, double F, double cr, int clip,
+                               double clip_hi, const uint32_t* mt_key, int32_t mt_pos, double* d_children,
+                               int64_t ldc, void* stream);
+int tblup_de_state_wait(tblup_ctx* ctx, uint32_t* mt_key, int32_t* mt_pos);
+
 /* Enqueue dst row i (L doubles, row stride ldd) = the device row d_src_rows[i] (a host array of
  * n device pointers, each to L doubles on this context's device) on `stream` (NULL = the
  * context's stream): one launch per 128 rows.  The DE step's parents gathered from the rows

@@ -75,6 +75,9 @@ struct tblup_ctx {
   DevBuf de_polys, de_small, de_par, de_chi;   // DE step: jump polynomials, per-call args, host-path staging
   int64_t de_L = -1, de_pop = -1;              // (L, pop) of the uploaded polynomials
   bool de_end_jump = false;
+  uint32_t* de_host = nullptr;   // page-locked: the MT state after the last step (624 words + pos)
+  hipEvent_t de_ev = nullptr;    // recorded behind that state's copy
+  bool de_pending = false;       // tblup_de_step_device_async issued, tblup_de_state_wait not yet called
   size_t budget = 0;
   // profiling
   bool profiling = false;
@@ -487,6 +490,8 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->de_small.release();
   c->de_par.release();
   c->de_chi.release();
+  if (c->de_ev) (void)hipEventDestroy(c->de_ev);
+  if (c->de_host) (void)hipHostFree(c->de_host);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -938,12 +943,15 @@ static int validate_de(int strategy, int64_t pop, int64_t L, const int32_t* dono
   return 0;
 }
 
-int tblup_de_step_device(tblup_ctx* c, int strategy, const double* d_parents, int64_t pop, int64_t L, int64_t ld,
-                         const int32_t* donors, const int64_t* fixed, double F, double cr, int clip, double clip_hi,
-                         uint32_t* mt_key, int32_t* mt_pos, double* d_children, int64_t ldc, void* stream) {
+int tblup_de_step_device_async(tblup_ctx* c, int strategy, const double* d_parents, int64_t pop, int64_t L,
+                               int64_t ld, const int32_t* donors, const int64_t* fixed, double F, double cr, int clip,
+                               double clip_hi, const uint32_t* mt_key, int32_t mt_pos, double* d_children,
+                               int64_t ldc, void* stream) {
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;
-  if (int rc = validate_de(strategy, pop, L, donors, fixed, cr, mt_key, mt_pos)) return rc;
+  if (c->de_pending) return fail(TBLUP_ERR_ARG, "the previous DE step's state was not fetched (tblup_de_state_wait)");
+  int32_t* const mt_pos_in = &mt_pos;
+  if (int rc = validate_de(strategy, pop, L, donors, fixed, cr, mt_key, mt_pos_in)) return rc;
   if (ld < L || ldc < L) return fail(TBLUP_ERR_ARG, "ld/ldc < L");
   if (!d_parents || !d_children) return fail(TBLUP_ERR_ARG, "null device pointers");
   HIPCHK(hipSetDevice(c->device));
@@ -971,16 +979,43 @@ int tblup_de_step_device(tblup_ctx* c, int strategy, const double* d_parents, in
   std::memcpy(stage.data() + o_don, donors, 12 * pop);
   std::memcpy(stage.data() + o_fix, fixed, 8 * pop);
   HIPCHK(hipMemcpyAsync(base, stage.data(), small, hipMemcpyHostToDevice, s));
-  const tblup_mt::EndState e = tblup_mt::end_state(*mt_pos, 2 * (uint64_t)L * (uint64_t)pop);
-  HIPCHK(launch_de_step((const uint32_t*)base, *mt_pos, (const uint32_t*)c->de_polys.p, c->de_end_jump ? 1 : 0, e.s,
+  const tblup_mt::EndState e = tblup_mt::end_state(mt_pos, 2 * (uint64_t)L * (uint64_t)pop);
+  HIPCHK(launch_de_step((const uint32_t*)base, mt_pos, (const uint32_t*)c->de_polys.p, c->de_end_jump ? 1 : 0, e.s,
                         e.pos, d_parents, ld, (const int32_t*)(base + o_don), (const int64_t*)(base + o_fix), strategy,
                         F, cr, clip ? 1 : 0, clip_hi, L, (int)pop, d_children, ldc, (uint32_t*)(base + o_keyo),
                         (int32_t*)(base + o_pos), s));
-  HIPCHK(hipMemcpyAsync(stage.data(), base + o_keyo, 624 * 4 + 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  std::memcpy(mt_key, stage.data(), 624 * 4);
-  std::memcpy(mt_pos, stage.data() + 624 * 4, 4);
+  if (!c->de_host) HIPCHK(hipHostMalloc((void**)&c->de_host, 625 * 4, hipHostMallocDefault));
+  if (!c->de_ev) HIPCHK(hipEventCreateWithFlags(&c->de_ev, hipEventDisableTiming));
+  HIPCHK(hipMemcpyAsync(c->de_host, base + o_keyo, 624 * 4 + 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(c->de_ev, s));
+  c->de_pending = true;
   return 0;
+}
+
+int tblup_de_state_wait(tblup_ctx* c, uint32_t* mt_key, int32_t* mt_pos) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (!mt_key || !mt_pos) return fail(TBLUP_ERR_ARG, "null mt_key/mt_pos");
+  if (!c->de_pending) return fail(TBLUP_ERR_ARG, "no DE step pending (tblup_de_step_device_async)");
+  HIPCHK(hipSetDevice(c->device));
+  c->de_pending = false;
+  HIPCHK(hipEventSynchronize(c->de_ev));
+  std::memcpy(mt_key, c->de_host, 624 * 4);
+  std::memcpy(mt_pos, c->de_host + 624, 4);
+  return 0;
+}
+
+int tblup_de_step_device(tblup_ctx* c, int strategy, const double* d_parents, int64_t pop, int64_t L, int64_t ld,
+                         const int32_t* donors, const int64_t* fixed, double F, double cr, int clip, double clip_hi,
+                         uint32_t* mt_key, int32_t* mt_pos, double* d_children, int64_t ldc, void* stream) {
+  if (!mt_key || !mt_pos) {
+    g_err.clear();
+    return fail(TBLUP_ERR_ARG, "null donors/fixed/mt_key/mt_pos");
+  }
+  if (int rc = tblup_de_step_device_async(c, strategy, d_parents, pop, L, ld, donors, fixed, F, cr, clip, clip_hi,
+                                          mt_key, *mt_pos, d_children, ldc, stream))
+    return rc;
+  return tblup_de_state_wait(c, mt_key, mt_pos);
 }
 
 int tblup_de_step(tblup_ctx* c, int strategy, const double* parents, int64_t pop, int64_t L, const int32_t* donors,

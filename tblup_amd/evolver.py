@@ -122,9 +122,12 @@ class GpuDEStep:
         np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
         return children
 
-    def step_device(self, strategy, parents, donors, fixed, F, cr, clip, clip_hi):
+    def step_device(self, strategy, parents, donors, fixed, F, cr, clip, clip_hi, defer=False):
         """Same on a device tensor of parents (pop x L float64, on this device); returns the
-        children as a device tensor.  Runs on torch's current stream."""
+        children as a device tensor.  Runs on torch's current stream.  defer: return
+        (children, finish) without waiting for the step; finish() waits for the new MT state
+        only (tblup_de_state_wait) and hands it to numpy -- call it before numpy's global RNG is
+        used again."""
         import torch
         pop, L = parents.shape
         donors = np.ascontiguousarray(donors, dtype=np.int32)
@@ -136,14 +139,22 @@ class GpuDEStep:
             children = torch.empty_like(parents)
         st, key, pos = self._rng_state()
         stream = ws.cuda_stream
-        _native.check("tblup_de_step_device", self._lib.tblup_de_step_device(
+        _native.check("tblup_de_step_device_async", self._lib.tblup_de_step_device_async(
             self._ctx, int(strategy), ctypes.c_void_p(parents.data_ptr()), pop, L, parents.stride(0),
             donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
             float(F), float(cr), 1 if clip else 0, float(clip_hi),
-            key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
+            key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), pos.value,
             ctypes.c_void_p(children.data_ptr()), children.stride(0), ctypes.c_void_p(stream)))
-        np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
-        cur.wait_stream(ws)   # (the call synchronised ws already; keeps later caller work ordered)
+        cur.wait_stream(ws)   # later caller work on the children is ordered behind the step
+
+        def finish():
+            _native.check("tblup_de_state_wait", self._lib.tblup_de_state_wait(
+                self._ctx, key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos)))
+            np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
+
+        if defer:
+            return children, finish
+        finish()
         return children
 
     def gather_rows(self, out, ptrs):
@@ -356,8 +367,6 @@ class _GpuDEEvolver(Evolver):
         mi = 5 if population.generation % 5 == 0 else self.mutation_intensity
         n = len(population)
         import torch
-        _BLOCKS.compact([population[i] for i in range(n)], DeviceKeyStore.get(GpuDEStep.get(self.device).device))
-        t = _mark(t, "ev_compact")
         genomes = [population[i].get_internal_genome() for i in range(n)]
         L = len(genomes[0])
         if any(len(g) != L for g in genomes):
@@ -374,30 +383,33 @@ class _GpuDEEvolver(Evolver):
             parents = store.gather(inds, L, host_rows=lambda i: genomes[i],
                                    copy_rows=step.gather_rows)   # device-resident parents
             t = _mark(t, "ev_gather")
-            children = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate, clip,
-                                        self.dimensionality - 1)
+            children, rng_done = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate,
+                                                  clip, self.dimensionality - 1, defer=True)
             t = _mark(t, "ev_prepare_step")
-            # the population's evaluator (tblup_amd) may start evaluating the children on the GPU
-            # now, while their genomes cross to the host (BlupParallelEvaluator._speculate)
-            evaluator = getattr(population, "evaluator", None)
-            spec = getattr(evaluator, "_speculate", None)
-            speculated = bool(spec is not None and dtypes is None and spec(inds, children, population.generation))
-            t = _mark(t, "ev_speculate")
-            # float64 children: one DMA into a page-locked block whose rows become the children's
-            # genomes (views: no host copy); otherwise chunks, each followed by an event, so the
-            # per-row copies of one chunk overlap the transfer of the next
-            block_rows = dtypes is None and n * L * 8 <= _BLOCK_MAX
-            host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
-            nchunk = 1 if block_rows else (8 if n >= 16 else 1)
-            rows = (n + nchunk - 1) // nchunk
-            events = []
-            for c in range(nchunk):
-                lo, hi = c * rows, min(n, (c + 1) * rows)
-                if lo < hi:
-                    host[lo:hi].copy_(children[lo:hi], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record()
-                events.append(ev)
+            try:
+                # the population's evaluator (tblup_amd) may start evaluating the children on the GPU
+                # now, while their genomes cross to the host (BlupParallelEvaluator._speculate)
+                evaluator = getattr(population, "evaluator", None)
+                spec = getattr(evaluator, "_speculate", None)
+                speculated = bool(spec is not None and dtypes is None and spec(inds, children, population.generation))
+                t = _mark(t, "ev_speculate")
+                # float64 children: one DMA into a page-locked block whose rows become the children's
+                # genomes (views: no host copy); otherwise chunks, each followed by an event, so the
+                # per-row copies of one chunk overlap the transfer of the next
+                block_rows = dtypes is None and n * L * 8 <= _BLOCK_MAX
+                host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
+                nchunk = 1 if block_rows else (8 if n >= 16 else 1)
+                rows = (n + nchunk - 1) // nchunk
+                events = []
+                for c in range(nchunk):
+                    lo, hi = c * rows, min(n, (c + 1) * rows)
+                    if lo < hi:
+                        host[lo:hi].copy_(children[lo:hi], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    events.append(ev)
+            finally:
+                rng_done()   # numpy's global state after the step's np.random.rand draws
         t = _mark(t, "ev_transfer_issue")
         # the candidates (new uids, the parent's other attributes) while the transfer runs
         next_pop = [_copy_individual(population[i]) for i in range(n)]
@@ -421,7 +433,10 @@ class _GpuDEEvolver(Evolver):
             store.record(children, next_pop, arrays)
             store.record(parents, inds, genomes, adopt=True)
         store.prune([x.uid for x in inds] + [x.uid for x in next_pop])
-        _mark(t, "ev_bind_record")
+        t = _mark(t, "ev_bind_record")
+        # older blocks the parents leave sparsely used, while the GPU still evaluates the children
+        _BLOCKS.compact(inds, store)
+        _mark(t, "ev_compact")
         return next_pop
 
 
