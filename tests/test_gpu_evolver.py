@@ -118,6 +118,36 @@ def test_gpu_de_bad_arguments_raise(gpu):
         step.step(0, par, np.array([[1, 2, 3]] * 4), np.full(4, 10), 0.5, 0.8, False, 9)   # fixed >= L
 
 
+def test_gpu_de_deferred_state(gpu):
+    """step_device(defer=True): children and numpy's state equal the synchronous step's; a
+    second step before the state is fetched, or a fetch with nothing pending, is refused."""
+    import torch
+    from tblup_amd import _native
+    from tblup_amd.evolver import GpuDEStep
+    step = GpuDEStep.get(0)
+    rng = np.random.default_rng(4)
+    par = torch.from_numpy(rng.uniform(size=(16, 301))).cuda()
+    donors = np.array([[(i + 1) % 16, (i + 2) % 16, (i + 3) % 16] for i in range(16)])
+    fixed = rng.integers(0, 301, 16)
+    np.random.seed(5)
+    want = step.step_device(0, par, donors, fixed, 0.5, 0.8, True, 1.0).cpu().numpy()
+    want_state = np.random.get_state()
+    np.random.seed(5)
+    kids, finish = step.step_device(0, par, donors, fixed, 0.5, 0.8, True, 1.0, defer=True)
+    with pytest.raises(_native.TblupError, match="not fetched"):
+        step.step_device(0, par, donors, fixed, 0.5, 0.8, True, 1.0)
+    finish()
+    assert np.array_equal(kids.cpu().numpy(), want)
+    got_state = np.random.get_state()
+    assert np.array_equal(got_state[1], want_state[1]) and got_state[2] == want_state[2]
+    key = np.zeros(624, np.uint32)
+    pos = np.zeros(1, np.int32)
+    import ctypes
+    rc = step._lib.tblup_de_state_wait(step._ctx, key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                       pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    assert rc != 0 and b"no DE step pending" in step._lib.tblup_last_error()
+
+
 def test_gpu_generations_with_device_keystore(gpu, tmp_path):
     """evolve -> evaluate -> select for 3 generations with the GPU evolver and evaluator (keys
     stay on the device between them) equals the same loop with the host oracle DE and a
