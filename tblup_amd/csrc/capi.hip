@@ -76,6 +76,8 @@ struct tblup_ctx {
   int64_t de_L = -1, de_pop = -1;              // (L, pop) of the uploaded polynomials
   bool de_end_jump = false;
   uint32_t* de_host = nullptr;   // page-locked: the MT state after the last step (624 words + pos)
+  char* de_stage = nullptr;      // page-locked: the per-call arguments on their way to de_small
+  size_t de_stage_bytes = 0;
   hipEvent_t de_ev = nullptr;    // recorded behind that state's copy
   bool de_pending = false;       // tblup_de_step_device_async issued, tblup_de_state_wait not yet called
   size_t budget = 0;
@@ -492,6 +494,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->de_chi.release();
   if (c->de_ev) (void)hipEventDestroy(c->de_ev);
   if (c->de_host) (void)hipHostFree(c->de_host);
+  if (c->de_stage) (void)hipHostFree(c->de_stage);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -974,11 +977,21 @@ int tblup_de_step_device_async(tblup_ctx* c, int strategy, const double* d_paren
     if (int rc = dev_alloc(c, c->de_small, small)) return rc;
   }
   char* base = (char*)c->de_small.p;
-  std::vector<char> stage(small);
-  std::memcpy(stage.data(), mt_key, 624 * 4);
-  std::memcpy(stage.data() + o_don, donors, 12 * pop);
-  std::memcpy(stage.data() + o_fix, fixed, 8 * pop);
-  HIPCHK(hipMemcpyAsync(base, stage.data(), small, hipMemcpyHostToDevice, s));
+  // page-locked staging that outlives this call (the copy is asynchronous); the previous call's
+  // copy from it finished before that call's state was fetched (one step pending at a time)
+  if (small > c->de_stage_bytes) {
+    HIPCHK(hipStreamSynchronize(s));
+    if (c->de_stage) HIPCHK(hipHostFree(c->de_stage));
+    c->de_stage = nullptr;
+    c->de_stage_bytes = 0;
+    HIPCHK(hipHostMalloc((void**)&c->de_stage, small, hipHostMallocDefault));
+    c->de_stage_bytes = small;
+  }
+  char* stage = c->de_stage;
+  std::memcpy(stage, mt_key, 624 * 4);
+  std::memcpy(stage + o_don, donors, 12 * pop);
+  std::memcpy(stage + o_fix, fixed, 8 * pop);
+  HIPCHK(hipMemcpyAsync(base, stage, small, hipMemcpyHostToDevice, s));
   const tblup_mt::EndState e = tblup_mt::end_state(mt_pos, 2 * (uint64_t)L * (uint64_t)pop);
   HIPCHK(launch_de_step((const uint32_t*)base, mt_pos, (const uint32_t*)c->de_polys.p, c->de_end_jump ? 1 : 0, e.s,
                         e.pos, d_parents, ld, (const int32_t*)(base + o_don), (const int64_t*)(base + o_fix), strategy,
