@@ -59,8 +59,8 @@ def _native_donors(strategy, n, L, best=-1):
     """One generation's donor / fixed-position draws (the python loops of _donors below) on
     CPython's MT19937 state in native code (tblup_de_donors): the same draws and the same
     `random` state afterwards, without 4n interpreted randrange calls.  None when the loop must
-    stay in python (n < 4 raises the reference's assertion there; L >= 2^32)."""
-    if n < 4 or L >= 1 << 32:
+    stay in python (n < 4 raises the reference's assertion there; n > 65535 or L >= 2^32)."""
+    if n < 4 or n > 65535 or L >= 1 << 32:
         return None
     version, internal, gauss = random.getstate()
     mt = np.array(internal[:624], dtype=np.uint32)
