@@ -164,9 +164,22 @@ class DeviceKeyStore:
         if host_rows is None and any(h is None for h in hits):
             return None
         out = torch.empty((n, L), dtype=torch.float64, device="cuda:%d" % self.device)
-        if copy_rows is not None and all(h is None or (h[0].dim() == 2 and h[0].shape[1] == L and h[0].stride(1) == 1)
-                                         for h in hits):
-            ptrs = [0 if h is None else h[0].data_ptr() + 8 * h[1] * h[0].stride(0) for h in hits]
+        # (base address, row pitch in bytes) per distinct device tensor, None if not a plain
+        # row-major (., L) float64 matrix: torch's accessors once per tensor, not per row
+        geo = {}
+        for h in hits:
+            if h is not None and id(h[0]) not in geo:
+                t = h[0]
+                geo[id(t)] = ((t.data_ptr(), 8 * t.stride(0))
+                              if t.dim() == 2 and t.shape[1] == L and t.stride(1) == 1 else None)
+        if copy_rows is not None and all(g is not None for g in geo.values()):
+            ptrs = []
+            for h in hits:
+                if h is None:
+                    ptrs.append(0)
+                else:
+                    base, pitch = geo[id(h[0])]
+                    ptrs.append(base + pitch * h[1])
             missing = [i for i, q in enumerate(ptrs) if not q]
             if len(missing) < n:
                 any_row = next(q for q in ptrs if q)
