@@ -39,6 +39,8 @@ SIGNATURES = {
     "tblup_eval_batch_device": (_c.c_int, [_P, _c.c_int, _P, _P, _I64P, _c.c_int64, _c.c_double, _c.c_int, _P, _P,
                                            _P]),
     "tblup_set_profiling": (_c.c_int, [_P, _c.c_int]),
+    "tblup_set_graph": (_c.c_int, [_P, _c.c_int]),
+    "tblup_graph_stats": (_c.c_int, [_P, _c.POINTER(_c.c_int64), _c.POINTER(_c.c_int64)]),
     "tblup_get_profile": (_c.c_int, [_P, _DP, _I64P, _DP, _DP]),
     "tblup_reset_profile": (_c.c_int, [_P]),
     "tblup_debug_grm": (_c.c_int, [_P, _c.c_int, _I64P, _c.c_int64, _c.c_double, _c.c_int, _c.c_int, _DP, _DP]),

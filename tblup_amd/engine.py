@@ -291,6 +291,18 @@ class GpuBlupEngine:
         self._pending = (ev, (keys, d_off, d_idx, d_fit, offsets))
         return ev, host
 
+    # --------------------------------------------------------------- graph replay
+    def set_graph(self, enable=True):
+        """Replay repeated evaluate_device calls (same arguments) from one captured hipGraph."""
+        _native.check("tblup_set_graph", self._lib.tblup_set_graph(self._ctx, 1 if enable else 0))
+
+    def graph_stats(self):
+        """(captures, replays) of the graph path since the context was created."""
+        cap, rep = ctypes.c_int64(0), ctypes.c_int64(0)
+        _native.check("tblup_graph_stats", self._lib.tblup_graph_stats(self._ctx, ctypes.byref(cap),
+                                                                        ctypes.byref(rep)))
+        return cap.value, rep.value
+
     # --------------------------------------------------------------- profiling
     def set_profiling(self, enable=True):
         _native.check("tblup_set_profiling", self._lib.tblup_set_profiling(self._ctx, 1 if enable else 0))

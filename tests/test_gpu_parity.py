@@ -204,6 +204,45 @@ def test_config2_properties(config2):
     np.testing.assert_allclose(f, c["fit"][:8], rtol=0, atol=1e-12)
 
 
+def test_config2_graph_replay(config2):
+    """tblup_set_graph: repeated device evaluations replayed from one captured hipGraph give
+    the direct launches' fitness bit for bit; a changed argument (h2, offsets) re-captures and
+    still matches the host path."""
+    import torch
+    from tblup_amd.engine import concat_genomes
+    c = config2
+    eng = c["eng"]
+    sid = eng.split_id(c["T"], c["V"])
+    idx, off = concat_genomes(c["genomes"])
+    d_idx = torch.from_numpy(idx).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    d_fit = torch.empty(len(c["genomes"]), dtype=torch.float64, device="cuda")
+    s = torch.cuda.Stream()
+    cap0, rep0 = eng.graph_stats()
+    eng.set_graph(True)
+    try:
+        for h2, want in ((0.4, c["fit"]), (0.4, c["fit"]), (0.4, c["fit"]), (0.7, None)):
+            d_fit.fill_(float("nan"))
+            eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, h2, d_fit.data_ptr(),
+                                stream_ptr=s.cuda_stream)
+            s.synchronize()
+            got = d_fit.cpu().numpy()
+            if want is None:
+                want = eng.evaluate(c["genomes"], c["T"], c["V"], h2)
+            np.testing.assert_array_equal(got, want)
+        cap, rep = eng.graph_stats()
+        assert (cap - cap0, rep - rep0) == (2, 4)      # 0.4 captured once, replayed 3x; 0.7 recaptured
+        # a shorter batch (different offsets) re-captures
+        d_fit.fill_(float("nan"))
+        eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off[:9], 0.4, d_fit.data_ptr(),
+                            stream_ptr=s.cuda_stream)
+        s.synchronize()
+        np.testing.assert_array_equal(d_fit.cpu().numpy()[:8], c["fit"][:8])
+        assert eng.graph_stats()[0] - cap0 == 3
+    finally:
+        eng.set_graph(False)
+
+
 def test_config2_gblup_branch_sample(config2):
     """k > n at config-2 size: the GBLUP branch (p over all n animals, no y centring)."""
     c = config2
