@@ -1,5 +1,6 @@
-"""Benchmark: GBLUP fitness evals/s on BASELINE config 2 (2000 animals x 50k SNPs,
-panel k = 1000, DE population 256 per GPU), one process per GPU.
+"""Benchmark: GBLUP fitness evals/s on BASELINE config 2 at N = 1 (2000 animals x 50k SNPs,
+panel k = 1000, DE population 256 on one GPU) and config 3 at N > 1 (the same panel, DE
+population 1024 sharded over the N GPUs: 128 per GPU at N = 8), one process per GPU.
 
 A "step" is one generation's fitness evaluation of the population: for every
 individual the exact-integer system tiles (SNP-space form at k < n_T, as sklearn's Ridge
@@ -9,9 +10,12 @@ Cholesky, back substitution, prediction and Pearson fitness, plus (N > 1) the RC
 all-gather of the fp64 fitness vector.  Inputs
 (genotypes, split, the population's decoded index sets) are resident in HBM
 before timing starts.  Weak scaling: every rank evaluates its own 256
-individuals.
+individuals per GPU: with --scaling strong (default) the configuration's population is the
+WHOLE job's and every rank evaluates its contiguous shard (tblup_amd.distributed.shard_range);
+with --scaling weak it is every rank's own.  Individual i's keys come from its own seed, so the
+population -- and the all-gathered fitness vector (`fitness_checksum`) -- is the same for any N.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W [--config auto|config2|config3|...] [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 """
 import argparse
@@ -26,8 +30,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (n animals, P SNPs, panel k, pop per GPU, n_train, n_valid)
+    # name: (n animals, P SNPs, panel k, DE population, n_train, n_valid)
     "config2": (2000, 50_000, 1000, 256, 1280, 320),
+    "config3": (2000, 50_000, 1000, 1024, 1280, 320),  # sharded over the node's GPUs (BASELINE config 3)
     "config1": (200, 1000, 100, 32, 128, 32),
     "config4": (5000, 600_000, 5000, 256, 3200, 800),
     "config5": (2000, 50_000, 1000, 256, 1280, 320),   # 3 traits (BASELINE config 5, build-defined)
@@ -57,8 +62,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
-    ap.add_argument("--pop", type=int, default=None, help="individuals per GPU (default: the config's)")
+    ap.add_argument("--config", default="auto", choices=["auto"] + sorted(CONFIGS),
+                    help="auto: config2 on one GPU, config3 (pop 1024 sharded) on N > 1")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the population is the whole job's, sharded over the ranks; weak: per rank")
+    ap.add_argument("--pop", type=int, default=None,
+                    help="population (whole job under --scaling strong, per rank under weak; default: the config's)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--h2", type=float, default=0.4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -71,7 +80,9 @@ def parse():
     return ap.parse_args()
 
 
-def make_workload(cfg, seed, rank, pop, traits=1):
+def make_workload(cfg, seed, lo, hi, traits=1):
+    """The panel, split and individuals lo..hi-1 of the population (individual i's RandomKey
+    keys from its own seed: the same individuals whatever the sharding)."""
     n, P, k, _, nT, nV = cfg
     rng = np.random.default_rng(seed)
     maf = rng.uniform(0.05, 0.5, size=P)                  # SURVEY.md section 8d synthetic panel
@@ -79,7 +90,7 @@ def make_workload(cfg, seed, rank, pop, traits=1):
     pheno = rng.standard_normal(n) if traits == 1 else rng.standard_normal((n, traits))
     perm = np.random.default_rng(seed + 1).permutation(n)
     T, V = perm[:nT], perm[nT:nT + nV]
-    keys = np.random.default_rng(seed + 100 + rank).uniform(size=(pop, P))
+    keys = np.stack([np.random.default_rng((seed, 100, i)).uniform(size=P) for i in range(lo, hi)])
     genomes = np.argsort(keys, axis=1)[:, -k:]            # RandomKeyIndividual decode (individual.py:154-156)
     return geno, pheno, T, V, genomes, keys
 
@@ -140,12 +151,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    cfg = CONFIGS[args.config]
+    from tblup_amd.distributed import shard_range
+    config = args.config if args.config != "auto" else ("config2" if world == 1 else "config3")
+    cfg = CONFIGS[config]
     n, P, k, pop_default, nT, nV = cfg
-    pop = args.pop or pop_default
+    if args.scaling == "strong":
+        total = args.pop or pop_default
+        lo, hi = shard_range(total, rank, world)
+    else:
+        per = args.pop or pop_default
+        total, lo, hi = per * world, per * rank, per * (rank + 1)
+    pop = hi - lo                                          # this rank's shard
+    shard_max = max(b - a for a, b in (shard_range(total, r, world) for r in range(world))) \
+        if args.scaling == "strong" else pop
 
-    traits = TRAITS.get(args.config, 1)
-    geno, pheno, T, V, genomes, keys = make_workload(cfg, args.seed, rank, pop, traits)
+    traits = TRAITS.get(config, 1)
+    geno, pheno, T, V, genomes, keys = make_workload(cfg, args.seed, lo, hi, traits)
     if k > 8192:
         keys = None
     cpu = None
@@ -155,20 +176,24 @@ def main():
     import torch
     import torch.distributed as dist
     from tblup_amd import distributed as tdist
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; more ranks than GPUs (a rehearsal of the N > 1 path on a smaller box,
+    # TBLUP_DIST_BACKEND=gloo) share them round-robin
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     # the same process-group set-up and all-gather the drop-in evaluator uses
     # (ParallelEvaluator.__enter__ -> init_from_env; _fitness -> allgather)
     os.environ.setdefault("TBLUP_DIST_BACKEND", "nccl")
-    owns_group = tdist.init_from_env(local_rank)
+    owns_group = tdist.init_from_env(device)
     from tblup_amd.engine import GpuBlupEngine, concat_genomes
 
-    eng = GpuBlupEngine(geno, pheno, device=local_rank)
+    eng = GpuBlupEngine(geno, pheno, device=device)
     sid = eng.split_id(T, V)
     idx, off = concat_genomes(list(genomes))
     d_idx = torch.from_numpy(idx).cuda()
     d_off = torch.from_numpy(off).cuda()
-    d_fit = torch.empty(pop, dtype=torch.float64, device="cuda")
-    full = torch.empty(pop * world, dtype=torch.float64, device="cuda")
+    # the all-gather moves equal blocks: shards padded to the largest one
+    d_fit = torch.full((shard_max,), float("nan"), dtype=torch.float64, device="cuda")
+    full = torch.empty(shard_max * world, dtype=torch.float64, device="cuda")
     stream = torch.cuda.current_stream()
 
     def step():
@@ -253,12 +278,18 @@ def main():
         host_ref = {"de_step_ms": round((t2 - t1) * 1e3, 2), "decode_ms": round((t3 - t2) * 1e3, 2), "cores": 1,
                     "kind": "port", "sample": f"one generation of {pop} x {P} keys (evolver.py:140-157, "
                                               "individual.py:154-156), numpy on one host core"}
-    fit = d_fit.cpu().numpy()
+    if world > 1:
+        fit_all = full.cpu().numpy().reshape(world, shard_max)
+        spans = [shard_range(total, r, world) if args.scaling == "strong" else (pop * r, pop * (r + 1))
+                 for r in range(world)]
+        fit = np.concatenate([fit_all[r, :b - a] for r, (a, b) in enumerate(spans)])
+    else:
+        fit = d_fit.cpu().numpy()[:pop]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_evals = pop * world * args.steps
+    total_evals = total * args.steps
     value = total_evals / elapsed
 
     # roofline of the dominant kernel class, from live HIP-event timing over the timed region.
@@ -286,7 +317,7 @@ def main():
     if os.path.isfile(args.pmc_json):
         try:
             pmc = json.load(open(args.pmc_json))
-            if pmc.get("config") == args.config and dom in pmc.get("per_launch_bytes", {}):
+            if pmc.get("config") == config and dom in pmc.get("per_launch_bytes", {}):
                 traffic = pmc["per_launch_bytes"][dom]
         except (ValueError, OSError):
             traffic = None
@@ -294,7 +325,7 @@ def main():
     if os.path.isfile(args.pmc_mfma_json):
         try:
             pm = json.load(open(args.pmc_mfma_json))
-            if pm.get("config") == args.config and dom in pm.get("per_class", {}):
+            if pm.get("config") == config and dom in pm.get("per_class", {}):
                 mfma_busy = pm["per_class"][dom]["mfma_busy"]
         except (ValueError, OSError, KeyError):
             mfma_busy = None
@@ -327,7 +358,7 @@ def main():
 
     if args.profile_json and rank == 0:
         with open(args.profile_json, "w") as f:
-            json.dump({"config": args.config, "steps": args.steps, "profile": prof, "per_step_ms": step_ms,
+            json.dump({"config": config, "steps": args.steps, "profile": prof, "per_step_ms": step_ms,
                        "elapsed_s": elapsed}, f, indent=1)
     roofline["step"]["frac"] = round(roofline["step"]["lower_bound_ms"] / (elapsed / args.steps * 1e3), 4)
     roofline["fp32_roofline_frac_canonical"] = round(f_canon * value / world / (PEAKS["fp32_mfma_tflops"] * 1e12), 4)
@@ -336,14 +367,16 @@ def main():
             "metric": METRIC,
             "value": round(value, 2), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": ("fp4 e2m1 system tiles (exact integer genotype products, fp32 accumulate)" if k < nT else
                       "int8 GRM (exact int32 accumulate)") + " + f64 Cholesky/solve",
             "data": "synthetic (Binomial(2, U(0.05,0.5)) genotypes, N(0,1) phenotype, RandomKey individuals)",
-            "config": {"workload": f"{args.config}: {n} animals x {P} SNPs, panel k={k}, pop {pop} per GPU, "
-                                   f"n_train={nT}, n_valid={nV}, h2={args.h2}"
+            "config": {"workload": f"{config}: {n} animals x {P} SNPs, panel k={k}, DE pop {total} "
+                                   f"({shard_max} per GPU), n_train={nT}, n_valid={nV}, h2={args.h2}"
                                    + (f", {traits} traits (one Cholesky, {traits} RHS)" if traits > 1 else ""),
-                       "parallelism": f"population sharded over {world} GPU(s), RCCL fitness all-gather"},
+                       "pop_total": total, "pop_per_gpu": shard_max,
+                       "parallelism": f"population sharded over {world} GPU(s) ({args.scaling} scaling)"
+                                      + (f", {tdist.backend_name()} fitness all-gather" if world > 1 else "")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": step_ms,

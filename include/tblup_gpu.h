@@ -131,18 +131,6 @@ int tblup_eval_batch_device(tblup_ctx* ctx, int split_id, const int64_t* d_idx,
                             double h2, int branch, double* d_fitness, double* d_ebv, void* stream);
 
 /*
- * Graph replay of tblup_eval_batch_device (also TBLUP_GRAPH=1 at tblup_ctx_create): the
- * evaluation's launches (statistics, system tiles, the column loop's diagonal / off-diagonal
- * launches, the solve) are captured once into a hipGraph and replayed by one hipGraphLaunch
- * while every launch argument -- split (and any tblup_set_split / set_traits / drop_split
- * since), device pointers, batch, offsets, h2, branch, stream, workspace -- equals the previous
- * call's; any change re-captures.  Same results bit for bit.  Off while profiling or tracing.
- * tblup_graph_stats: captures and replays since the context was created.
- */
-int tblup_set_graph(tblup_ctx* ctx, int enable);
-int tblup_graph_stats(tblup_ctx* ctx, int64_t* captures, int64_t* replays);
-
-/*
  * RandomKeyIndividual / CoevolutionIndividual genome decode
  * (tblup/individual.py:154-156, `np.argsort(keys)[-int(length):]`): for each of
  * `batch` key rows of length d, the indices of its k_b = offsets[b+1]-offsets[b]

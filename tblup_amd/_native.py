@@ -15,6 +15,7 @@ LAYOUT_ANIMAL_MAJOR = 0
 LAYOUT_SNP_MAJOR = 1
 N_KCLASS = 6
 MAX_TRAITS = 4
+ERR_STATE = -4   # TBLUP_ERR_STATE: call out of order
 ERR_INDEX = -5   # TBLUP_ERR_INDEX: numpy's IndexError for data[:, indices]
 KCLASS_NAMES = ("stats", "gather", "grm", "chol_diag", "chol_offdiag", "solve")
 
@@ -39,8 +40,6 @@ SIGNATURES = {
     "tblup_eval_batch_device": (_c.c_int, [_P, _c.c_int, _P, _P, _I64P, _c.c_int64, _c.c_double, _c.c_int, _P, _P,
                                            _P]),
     "tblup_set_profiling": (_c.c_int, [_P, _c.c_int]),
-    "tblup_set_graph": (_c.c_int, [_P, _c.c_int]),
-    "tblup_graph_stats": (_c.c_int, [_P, _c.POINTER(_c.c_int64), _c.POINTER(_c.c_int64)]),
     "tblup_get_profile": (_c.c_int, [_P, _DP, _I64P, _DP, _DP]),
     "tblup_reset_profile": (_c.c_int, [_P]),
     "tblup_debug_grm": (_c.c_int, [_P, _c.c_int, _I64P, _c.c_int64, _c.c_double, _c.c_int, _c.c_int, _DP, _DP]),

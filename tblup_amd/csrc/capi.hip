@@ -97,16 +97,6 @@ struct tblup_ctx {
   int64_t wgt_used = 0;
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
   int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
-  int64_t epoch = 0;  // bumped whenever a split or the traits change (invalidates the captured graph)
-
-  // tblup_set_graph / TBLUP_GRAPH: a device evaluation whose launch arguments all equal the
-  // previous call's is replayed from one captured hipGraph (the steady state of the bench and
-  // of a DE run over fixed device buffers); anything else is captured afresh
-  bool use_graph = false;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t gexec = nullptr;
-  std::vector<int64_t> gkey;
-  int64_t graph_captures = 0, graph_replays = 0;
 };
 
 namespace {
@@ -447,8 +437,6 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->dbg_skip = dbg ? atoi(dbg) : 0;
   const char* wt = getenv("TBLUP_WG_TRACE");
   c->wg_trace = wt && atoi(wt) != 0;
-  const char* gr = getenv("TBLUP_GRAPH");
-  c->use_graph = gr && atoi(gr) != 0;
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   if (!panel) {
@@ -507,8 +495,6 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   if (c->de_ev) (void)hipEventDestroy(c->de_ev);
   if (c->de_host) (void)hipHostFree(c->de_host);
   if (c->de_stage) (void)hipHostFree(c->de_stage);
-  if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
-  if (c->graph) (void)hipGraphDestroy(c->graph);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -569,7 +555,7 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   auto it = c->splits.find(split_id);
   if (it != c->splits.end()) {
     dev_free(c, it->second->geno);
-    dev_free(c, it->second->gpk);
+  dev_free(c, it->second->gpk);
     dev_free(c, it->second->colsumT);
     dev_free(c, it->second->xty);
     dev_free(c, it->second->yT);
@@ -577,7 +563,6 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
     dev_free(c, it->second->ymu);
   }
   c->splits[split_id] = std::move(sp);
-  ++c->epoch;
   return 0;
 }
 
@@ -588,7 +573,6 @@ int tblup_set_traits(tblup_ctx* c, const double* pheno, int64_t n_traits) {
   if (!pheno || n_traits < 1 || n_traits > MAXT) return fail(TBLUP_ERR_ARG, "need 1 <= n_traits <= 4 and phenotypes");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  ++c->epoch;
   for (auto& kv : c->splits) {   // splits hold per-trait phenotype vectors
     dev_free(c, kv.second->geno);
     dev_free(c, kv.second->gpk);
@@ -617,14 +601,13 @@ int tblup_drop_split(tblup_ctx* c, int split_id) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   dev_free(c, it->second->geno);
-    dev_free(c, it->second->gpk);
+  dev_free(c, it->second->gpk);
   dev_free(c, it->second->colsumT);
   dev_free(c, it->second->xty);
   dev_free(c, it->second->yT);
   dev_free(c, it->second->yV);
   dev_free(c, it->second->ymu);
   c->splits.erase(it);
-  ++c->epoch;
   return 0;
 }
 
@@ -725,59 +708,8 @@ int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, co
     if (int rc = dev_alloc(c, c->ws, need)) return rc;
   }
   Carve cv{(char*)c->ws.p};
-  if (!c->use_graph || c->profiling || c->wg_trace)
-    return run_chunk(c, *sp, d, sd, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness, d_ebv, 0,
-                     nullptr, nullptr);
-  // graph mode: every value a launch argument is derived from is part of the key
-  int64_t h2bits;
-  std::memcpy(&h2bits, &h2, 8);
-  std::vector<int64_t> key = {c->epoch, split_id, (int64_t)(intptr_t)d_idx, (int64_t)(intptr_t)d_offsets,
-                              batch, h2bits, branch, (int64_t)(intptr_t)d_fitness, (int64_t)(intptr_t)d_ebv,
-                              (int64_t)(intptr_t)s, (int64_t)(intptr_t)c->ws.p, c->form_pref, c->dbg_skip};
-  key.insert(key.end(), h_offsets, h_offsets + batch + 1);
-  if (!c->gexec || key != c->gkey) {
-    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
-    if (c->graph) (void)hipGraphDestroy(c->graph);
-    c->gexec = nullptr;
-    c->graph = nullptr;
-    c->gkey.clear();
-    HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = run_chunk(c, *sp, d, sd, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness,
-                             d_ebv, 0, nullptr, nullptr);
-    hipGraph_t g = nullptr;
-    const hipError_t ec = hipStreamEndCapture(s, &g);
-    if (rc || ec != hipSuccess) {
-      if (g) (void)hipGraphDestroy(g);
-      return rc ? rc : fail(TBLUP_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
-    }
-    const hipError_t ei = hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0);
-    if (ei != hipSuccess) {
-      (void)hipGraphDestroy(g);
-      c->gexec = nullptr;
-      return fail(TBLUP_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
-    }
-    c->graph = g;
-    c->gkey = std::move(key);
-    ++c->graph_captures;
-  }
-  HIPCHK(hipGraphLaunch(c->gexec, s));
-  ++c->graph_replays;
-  return 0;
-}
-
-int tblup_set_graph(tblup_ctx* c, int enable) {
-  g_err.clear();
-  if (int rc = check_ctx(c)) return rc;
-  c->use_graph = enable != 0;
-  return 0;
-}
-
-int tblup_graph_stats(tblup_ctx* c, int64_t* captures, int64_t* replays) {
-  g_err.clear();
-  if (int rc = check_ctx(c)) return rc;
-  if (captures) *captures = c->graph_captures;
-  if (replays) *replays = c->graph_replays;
-  return 0;
+  return run_chunk(c, *sp, d, sd, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness, d_ebv, 0, nullptr,
+                   nullptr);
 }
 
 static int validate_decode(int64_t batch, int64_t d, const int64_t* offsets) {
@@ -1020,7 +952,7 @@ int tblup_de_step_device_async(tblup_ctx* c, int strategy, const double* d_paren
                                int64_t ldc, void* stream) {
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;
-  if (c->de_pending) return fail(TBLUP_ERR_ARG, "the previous DE step's state was not fetched (tblup_de_state_wait)");
+  if (c->de_pending) return fail(TBLUP_ERR_STATE, "the previous DE step's state was not fetched (tblup_de_state_wait)");
   int32_t* const mt_pos_in = &mt_pos;
   if (int rc = validate_de(strategy, pop, L, donors, fixed, cr, mt_key, mt_pos_in)) return rc;
   if (ld < L || ldc < L) return fail(TBLUP_ERR_ARG, "ld/ldc < L");
@@ -1077,7 +1009,7 @@ int tblup_de_state_wait(tblup_ctx* c, uint32_t* mt_key, int32_t* mt_pos) {
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;
   if (!mt_key || !mt_pos) return fail(TBLUP_ERR_ARG, "null mt_key/mt_pos");
-  if (!c->de_pending) return fail(TBLUP_ERR_ARG, "no DE step pending (tblup_de_step_device_async)");
+  if (!c->de_pending) return fail(TBLUP_ERR_STATE, "no DE step pending (tblup_de_step_device_async)");
   HIPCHK(hipSetDevice(c->device));
   c->de_pending = false;
   HIPCHK(hipEventSynchronize(c->de_ev));

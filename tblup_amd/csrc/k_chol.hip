@@ -112,7 +112,9 @@ __device__ __forceinline__ double rdlane(double x, int lane) {
 // compiler does not see inside asm, so hazards are handled here: NOP = the DPP read-after-VALU-
 // write wait for a register the previous instruction may have written (the next pivot's
 // column); the others are volatile so they keep their order, in which no fmac reads a
-// register the one before it wrote.
+// register the one before it wrote.  That the compiler places no other VALU write of an fmac's
+// src0 within 2 wait states of it is checked on the built library by tools/check_dpp_hazards.py
+// (tests/test_abi.py); an s_nop on every fmac instead would lengthen factor16's pivot chain.
 template <int J, bool NOP>
 __device__ __forceinline__ void fmac_row(double& x, double m) {
   if constexpr (NOP)

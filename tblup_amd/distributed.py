@@ -53,6 +53,15 @@ def init_from_env(device=None):
     return True
 
 
+def backend_name():
+    """'RCCL' for the nccl backend on ROCm, else the backend's own name ('' without a group)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return ""
+    b = dist.get_backend()
+    return "RCCL" if b == "nccl" else b
+
+
 def destroy():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():

@@ -98,7 +98,8 @@ class GpuBlupEngine:
 
     def _settle(self):
         """Wait for asynchronous work (eval_keys_async) that uses the context's workspace; every
-        other entry point calls this first, so calls stay serialised on the context."""
+        other entry point (the device-pointer ones included) calls this first, so calls stay
+        serialised on the context whatever stream they are enqueued on."""
         p = self._pending
         if p is not None:
             self._pending = None
@@ -106,6 +107,7 @@ class GpuBlupEngine:
 
     # ------------------------------------------------------------------ splits
     def split_id(self, train, valid):
+        self._settle()
         t = _as_int64(train)
         v = _as_int64(valid)
         key = hashlib.sha1(t.tobytes() + b"|" + v.tobytes()).hexdigest()
@@ -145,6 +147,7 @@ class GpuBlupEngine:
     def evaluate_device(self, split_id, d_idx_ptr, d_off_ptr, h_offsets, h2, d_fit_ptr, d_ebv_ptr=None,
                         stream_ptr=None, branch="auto"):
         """Asynchronous evaluation on device-resident buffers (raw device pointers)."""
+        self._settle()
         h_off = _as_int64(h_offsets)
         B = len(h_off) - 1
         _native.check("tblup_eval_batch_device", self._lib.tblup_eval_batch_device(
@@ -156,6 +159,7 @@ class GpuBlupEngine:
     def index_error(self, stream_ptr=None):
         """True if an individual evaluated through evaluate_device since the last call had an
         index outside [-P, P) (its fitness is NaN); synchronises the stream, clears the flag."""
+        self._settle()
         flag = ctypes.c_int(0)
         _native.check("tblup_index_error", self._lib.tblup_index_error(
             self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(flag)))
@@ -181,6 +185,7 @@ class GpuBlupEngine:
 
     def decode_randkey_device(self, d_keys_ptr, B, d, ld, d_off_ptr, h_offsets, d_idx_ptr, stream_ptr=None):
         """Device-resident decode: keys (B x ld doubles) -> idx at offsets (device pointers)."""
+        self._settle()
         h_off = _as_int64(h_offsets)
         _native.check("tblup_decode_topk_device", self._lib.tblup_decode_topk_device(
             self._ctx, ctypes.c_void_p(d_keys_ptr), B, d, ld, ctypes.c_void_p(d_off_ptr), _ptr(h_off, ctypes.c_int64),
@@ -290,18 +295,6 @@ class GpuBlupEngine:
             ev.record(st)
         self._pending = (ev, (keys, d_off, d_idx, d_fit, offsets))
         return ev, host
-
-    # --------------------------------------------------------------- graph replay
-    def set_graph(self, enable=True):
-        """Replay repeated evaluate_device calls (same arguments) from one captured hipGraph."""
-        _native.check("tblup_set_graph", self._lib.tblup_set_graph(self._ctx, 1 if enable else 0))
-
-    def graph_stats(self):
-        """(captures, replays) of the graph path since the context was created."""
-        cap, rep = ctypes.c_int64(0), ctypes.c_int64(0)
-        _native.check("tblup_graph_stats", self._lib.tblup_graph_stats(self._ctx, ctypes.byref(cap),
-                                                                        ctypes.byref(rep)))
-        return cap.value, rep.value
 
     # --------------------------------------------------------------- profiling
     def set_profiling(self, enable=True):

@@ -247,7 +247,7 @@ class _RowBlocks:
 
     A row is a view, so a block stays allocated while any genome in it lives (the reference
     gives every child its own array, individual.py:110-118; a view is one as far as any
-    reader can tell: disjoint rows, float64, writable).  DE selection leaves survivors spread
+    reader can tell: disjoint rows, float64, written through the TrackedGenome paths).  DE selection leaves survivors spread
     over older blocks: when more than `keep` older blocks are still referenced by the
     population, the least-referenced ones are compacted -- those individuals' genomes are
     replaced by equal own copies (set_internal_genome, individual.py:100-101) -- so at most
@@ -261,7 +261,9 @@ class _RowBlocks:
     def rows(self, block):
         import weakref
         self._reg[id(block)] = weakref.ref(block)
-        return [track(block[i]) for i in range(block.shape[0])]
+        rows = [track(block[i], lock=False) for i in range(block.shape[0])]
+        block.flags.writeable = False   # the rows' private aliases are the only writable ones
+        return rows
 
     def _block_of(self, g):
         b = g

@@ -11,13 +11,20 @@ An entry is valid while the individual still holds the very numpy array the
 entry was recorded with (`indv._genome is <recorded array>`), that array has not
 been written since, and the individual has the same `length`.
 `set_internal_genome` and `fill` (individual.py:103-130, 187-208,
-scheduler.py:209-251) replace the array or change the length; an in-place write
-(`Individual.__setitem__`, individual.py:119-120, or any numpy write through the
-array or a view of it) marks the recorded array stale -- recorded arrays are
-`TrackedGenome` views (an ndarray subclass that notices item assignment and
-in-place ufuncs) and stay writable, as the reference allows.  A stale or replaced
-genome is read from the host.  Device memory is plumbing here: torch tensors on
-the context's device.
+scheduler.py:209-251) replace the array or change the length.  In-place writes
+are allowed, as the reference allows them (`Individual.__setitem__`,
+individual.py:119-120), but never silently: a recorded array is a `TrackedGenome`,
+a READ-ONLY view whose memory has no other writable numpy alias (the page-locked
+block it lives in, or an adopted initial genome, is made read-only too).  Every
+numpy write path it intercepts -- item assignment, in-place ufuncs and `out=`,
+`ufunc.at`, the writing methods (`fill`, `sort`, `put`, `partition`, `byteswap`,
+`setfield`, `itemset`) and the writing functions (`np.copyto`, `np.put`, `np.place`,
+`np.putmask`, `np.put_along_axis`, `np.fill_diagonal`, any `out=`) -- marks the
+array stale and then writes through a private writable alias; every other write
+(`np.random.shuffle`, writes through `np.asarray(g)` or `g.view(np.ndarray)`, the
+buffer protocol) meets a read-only array and raises.  A stale or replaced genome is
+read from the host.  Device memory is plumbing here: torch tensors on the context's
+device.
 """
 import weakref
 
@@ -25,35 +32,105 @@ import numpy as np
 
 
 class TrackedGenome(np.ndarray):
-    """A genome array the key store mirrors on the device.  Writes through it or through
-    any view of it (item assignment, in-place ufuncs / `out=`) mark the owning array
-    stale; values and semantics are otherwise those of the ndarray it views.  Results of
-    computations on it are plain ndarrays."""
+    """A genome array the key store mirrors on the device: read-only to numpy, written only
+    through the paths below, each of which first marks the owning array stale.  Views of it
+    are TrackedGenomes of the same owner; copies and results of computations are plain
+    (writable, untracked) arrays."""
 
-    _owner = None
+    _owner = None    # the recorded array this view belongs to (None: it is the owner)
     _stale = False
+    _w = None        # owner only: a writable plain alias of its memory, held by nobody else
 
     def __array_finalize__(self, obj):
-        if isinstance(obj, TrackedGenome):
+        if isinstance(obj, TrackedGenome) and obj._tracked() and not self.flags.owndata:
             self._owner = obj._owner if obj._owner is not None else obj
+        else:                      # a copy: behaves as a plain array
+            self._owner = None
+            self._w = None
+
+    def _tracked(self):
+        return self._owner is not None or self._w is not None
+
+    def _root(self):
+        return self._owner if self._owner is not None else self
+
+    def _writable(self):
+        """A writable plain view of exactly this array's elements (marks the owner stale)."""
+        root = self._root()
+        if root._w is None:        # untracked copy
+            return self.view(np.ndarray)
+        root._stale = True
+        base = root._w
+        off = self.__array_interface__["data"][0] - base.__array_interface__["data"][0]
+        return np.ndarray(self.shape, dtype=self.dtype, buffer=base, offset=off, strides=self.strides)
 
     def _touch(self):
-        (self._owner if self._owner is not None else self)._stale = True
+        if self._tracked():
+            self._root()._stale = True
 
+    # -- item assignment and the writing methods
     def __setitem__(self, key, value):
-        self._touch()
-        super().__setitem__(key, value)
+        if not self._tracked():
+            return super().__setitem__(key, value)
+        self._writable()[key] = value
 
+    def fill(self, value):
+        (self._writable() if self._tracked() else super()).fill(value)
+
+    def sort(self, *a, **k):
+        (self._writable() if self._tracked() else super()).sort(*a, **k)
+
+    def partition(self, *a, **k):
+        (self._writable() if self._tracked() else super()).partition(*a, **k)
+
+    def put(self, *a, **k):
+        (self._writable() if self._tracked() else super()).put(*a, **k)
+
+    def setfield(self, *a, **k):
+        (self._writable() if self._tracked() else super()).setfield(*a, **k)
+
+    def itemset(self, *a):
+        w = self._writable() if self._tracked() else self.view(np.ndarray)
+        w[a[:-1] if len(a) > 2 else a[0]] = a[-1]
+
+    def byteswap(self, inplace=False):
+        if inplace and self._tracked():
+            self._writable().byteswap(inplace=True)
+            return self
+        return super().byteswap(inplace).view(np.ndarray)
+
+    # -- ufuncs: in place (out=) and ufunc.at write; everything else computes plain arrays
     def __array_ufunc__(self, ufunc, method, *inputs, out=None, **kwargs):
-        plain = tuple(x.view(np.ndarray) if isinstance(x, TrackedGenome) else x for x in inputs)
+        def plain(x):
+            return x.view(np.ndarray) if isinstance(x, TrackedGenome) else x
+        if method == "at" and isinstance(inputs[0], TrackedGenome):
+            inputs = (inputs[0]._writable(),) + tuple(plain(x) for x in inputs[1:])
+        else:
+            inputs = tuple(plain(x) for x in inputs)
         if out is not None:
-            for o in out:
-                if isinstance(o, TrackedGenome):
-                    o._touch()
-            kwargs["out"] = tuple(o.view(np.ndarray) if isinstance(o, TrackedGenome) else o for o in out)
-        res = getattr(ufunc, method)(*plain, **kwargs)
+            kwargs["out"] = tuple(o._writable() if isinstance(o, TrackedGenome) else o for o in out)
+        res = getattr(ufunc, method)(*inputs, **kwargs)
         if out is not None:
             return out[0] if len(out) == 1 else out
+        return res
+
+    # -- numpy functions that write into an argument
+    _WRITERS = {np.copyto: 0, np.put: 0, np.place: 0, np.putmask: 0, np.put_along_axis: 0, np.fill_diagonal: 0}
+
+    def __array_function__(self, func, types, args, kwargs):
+        pos = TrackedGenome._WRITERS.get(func)
+        if pos is not None and len(args) > pos and isinstance(args[pos], TrackedGenome):
+            args = list(args)
+            args[pos] = args[pos]._writable()
+        o = kwargs.get("out")
+        if isinstance(o, TrackedGenome):
+            kwargs = dict(kwargs, out=o._writable())
+        elif isinstance(o, tuple) and any(isinstance(x, TrackedGenome) for x in o):
+            kwargs = dict(kwargs, out=tuple(x._writable() if isinstance(x, TrackedGenome) else x for x in o))
+        args = tuple(a.view(np.ndarray) if isinstance(a, TrackedGenome) else a for a in args)
+        res = super().__array_function__(func, types, args, kwargs)
+        if o is not None:
+            return o
         return res
 
     def __reduce__(self):   # pickles / deep-copies as a plain ndarray
@@ -66,9 +143,18 @@ class TrackedGenome(np.ndarray):
         return self.view(np.ndarray).copy()
 
 
-def track(a):
-    """A TrackedGenome view of the float64 array `a` (no copy)."""
-    return a.view(TrackedGenome)
+def track(a, lock=True):
+    """A TrackedGenome over the float64 array `a`'s memory (no copy).  `a` itself is made
+    read-only (lock=False: the caller locks the memory's owner, e.g. a whole block, after
+    tracking all of its rows), so the only writable alias left is the TrackedGenome's own."""
+    w = a.view(np.ndarray)
+    t = a.view(TrackedGenome)
+    t._w = w
+    t._owner = None
+    t.flags.writeable = False
+    if lock:
+        a.flags.writeable = False
+    return t
 
 
 _STREAMS = {}

@@ -125,3 +125,9 @@ class OracleEngine:
 
     def close(self):
         pass
+
+
+def shard_population(pop, n_snps, k, seed=11):
+    """A population of `pop` selected-index sets where individual i comes from its own seed:
+    the same individuals in every process, whatever the sharding (tests/test_gpu_shards.py)."""
+    return [np.random.default_rng((seed, i)).choice(n_snps, k, replace=False) for i in range(pop)]

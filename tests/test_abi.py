@@ -50,3 +50,23 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(ImportError):
         _native.load()
+
+
+def test_no_dpp_read_after_valu_write_hazard_in_shipped_code():
+    """factor16's v_fmac_f64_dpp pivot updates are inline asm the compiler's hazard recognizer
+    cannot see into: check the built gfx950 code objects themselves -- no VALU
+    write of a DPP instruction's src0 within the 2 wait states the ISA requires."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import check_dpp_hazards as C
+    if not os.path.isfile(C.OBJDUMP):
+        pytest.skip("llvm-objdump not available")
+    n_dpp, bad = C.check(_native.LIB_PATH)
+    assert n_dpp >= 500                     # factor16's broadcast-fmacs are in the library
+    assert not bad, bad[:3]
+    # the checker itself flags the pattern it guards against
+    listing = ("v_mov_b32_e32 v65, v34\n\ts_nop 0\n"
+               "v_fmac_f64_dpp v[64:65], v[64:65], v[34:35] row_newbcast:0 row_mask:0xf bank_mask:0xf\n")
+    assert len(C.check_disassembly(listing)) == 1
+    assert not C.check_disassembly(listing.replace("s_nop 0", "s_nop 1"))

@@ -134,8 +134,9 @@ def test_gpu_de_deferred_state(gpu):
     want_state = np.random.get_state()
     np.random.seed(5)
     kids, finish = step.step_device(0, par, donors, fixed, 0.5, 0.8, True, 1.0, defer=True)
-    with pytest.raises(_native.TblupError, match="not fetched"):
+    with pytest.raises(_native.TblupError, match="not fetched") as ei:
         step.step_device(0, par, donors, fixed, 0.5, 0.8, True, 1.0)
+    assert ei.value.code == _native.ERR_STATE
     finish()
     assert np.array_equal(kids.cpu().numpy(), want)
     got_state = np.random.get_state()
@@ -145,7 +146,7 @@ def test_gpu_de_deferred_state(gpu):
     import ctypes
     rc = step._lib.tblup_de_state_wait(step._ctx, key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
                                        pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
-    assert rc != 0 and b"no DE step pending" in step._lib.tblup_last_error()
+    assert rc == _native.ERR_STATE and b"no DE step pending" in step._lib.tblup_last_error()
 
 
 def test_gpu_generations_with_device_keystore(gpu, tmp_path):

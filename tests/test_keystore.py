@@ -1,5 +1,6 @@
-"""Device key store validity: recorded genomes stay writable (Individual.__setitem__,
-individual.py:119-120) and any in-place write drops the device copy."""
+"""Device key store validity: recorded genomes stay writable through numpy's write paths
+(Individual.__setitem__, individual.py:119-120, and the rest) and any in-place write drops the
+device copy; a write the store cannot see raises instead of leaving a stale device row."""
 import copy
 import pickle
 
@@ -32,6 +33,51 @@ def test_tracked_genome_notices_writes():
     assert not f._stale
 
 
+@pytest.mark.parametrize("write", [
+    lambda g: np.copyto(g, np.arange(g.size, dtype=np.float64)[::-1]),
+    lambda g: g.sort(),
+    lambda g: g.fill(0.5),
+    lambda g: g.put([0, 1], [2.0, 3.0]),
+    lambda g: g.partition(2),
+    lambda g: np.put(g, [2], [9.0]),
+    lambda g: np.place(g, g > 0.5, [0.25]),
+    lambda g: np.putmask(g, g > 0.5, 0.75),
+    lambda g: np.add.at(g, [0, 0, 3], 1.0),
+    lambda g: np.clip(g, 0.2, 0.6, out=g),
+    lambda g: np.negative(g[::-2], out=g[::-2]),
+    lambda g: g[1:4].__setitem__(slice(None), -1.0),
+    lambda g: g.byteswap(inplace=True),
+], ids=["copyto", "sort", "fill", "put", "partition", "np.put", "np.place", "np.putmask", "ufunc.at",
+        "clip-out", "reversed-view-out", "view-setitem", "byteswap"])
+def test_every_numpy_write_path_marks_stale(write):
+    """Each in-place write numpy offers either marks the recorded array stale (and writes, with
+    numpy's own result) or raises; none leaves it looking unchanged."""
+    rng = np.random.default_rng(2)
+    vals = rng.uniform(size=8)
+    g = track(vals.copy())
+    want = vals.copy()
+    write(want)                                          # numpy's result on a plain array
+    write(g)
+    assert g._stale
+    np.testing.assert_array_equal(g.view(np.ndarray), want)
+
+
+def test_unseen_write_paths_raise():
+    """Writes the store cannot intercept meet a read-only array: the recorded memory has no
+    other writable numpy alias (the owner / block is locked too)."""
+    owner = np.random.default_rng(1).uniform(size=6)
+    g = track(owner)
+    for write in (lambda: np.random.shuffle(g), lambda: np.asarray(g).__setitem__(0, 1.0),
+                  lambda: g.view(np.ndarray).__setitem__(0, 1.0), lambda: owner.__setitem__(0, 1.0),
+                  lambda: g.base.__setitem__(0, 1.0)):
+        with pytest.raises(ValueError):
+            write()
+    assert not g._stale
+    cp = g.copy()                                        # copies are plain, writable, untracked
+    cp[0] = 5.0
+    assert not g._stale and cp[0] == 5.0
+
+
 class _Ind:
     def __init__(self, uid, g):
         self.uid, self._genome, self.length = uid, g, 5
@@ -59,6 +105,10 @@ def test_store_drops_written_and_replaced_genomes():
     store.record(t, [ind], plain, adopt=True)
     assert isinstance(ind._genome, TrackedGenome) and np.shares_memory(ind._genome, plain[0])
     assert store.lookup(ind) is not None
+    with pytest.raises(ValueError):                      # an old plain reference cannot write behind
+        plain[0][0] = 1.0                                # the store's back (adopt=True)
+    ind._genome[0] = 1.0                                 # the individual's own writes still work
+    assert store.lookup(ind) is None and plain[0][0] == 1.0
 
 
 @pytest.mark.gpu
@@ -87,11 +137,15 @@ def test_gpu_write_after_evolve_is_seen(gpu, tmp_path):
         g = kids[2].get_internal_genome()
         top = np.argsort(g)[-k:]
         g[top[:10]] = -1.0                                # knock 10 selected SNPs out in place
-        assert DeviceKeyStore.get(0).lookup(kids[2]) is None
-        assert DeviceKeyStore.get(0).lookup(kids[3]) is not None
+        # writes that are neither item assignment nor ufuncs
+        np.copyto(kids[4].get_internal_genome(), rng.uniform(size=p))
+        kids[5].get_internal_genome().sort()
+        store = DeviceKeyStore.get(0)
+        assert store.lookup(kids[2]) is None and store.lookup(kids[4]) is None and store.lookup(kids[5]) is None
+        assert store.lookup(kids[3]) is not None
         ev.evaluate(popn, kids, 1)
         T, V = ev.training_indices, ev.validation_indices
-        for j in (2, 3):
+        for j in (2, 3, 4, 5):
             want = O.blup(O.decode_randkeys(kids[j].get_internal_genome(), k), T, V, geno.astype(np.float64),
                           pheno, 0.4)
             assert abs(kids[j].fitness - want) < 1e-9
