@@ -249,7 +249,7 @@ def main():
         # evolver.py:103-157): DE/rand/1 + binary crossover with numpy's MT19937 stream
         # jumped per individual; reported beside the metric, not part of it
         from tblup_amd.evolver import GpuDEStep
-        de = GpuDEStep.get(local_rank)
+        de = GpuDEStep.get(device)
         drng = np.random.default_rng(args.seed + 7)
         donors = np.stack([drng.choice(pop, 3, replace=False) for _ in range(pop)]).astype(np.int32)
         fixed = drng.integers(0, P, size=pop)
