@@ -97,6 +97,10 @@ struct tblup_ctx {
   int64_t wgt_used = 0;
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
   int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
+  // Cholesky schedule (results are bit-identical under every setting; see OffPlan):
+  int ahead = -1;     // TBLUP_AHEAD: -1 auto (B < AHEAD_B), 0 never, 1 always
+  int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
+  int qmode = 1;      // TBLUP_QMODE: tile (J+1, J) forms the next diagonal's last SYRK term
 };
 
 namespace {
@@ -189,7 +193,47 @@ bool sys_tiles(const EvalDims& d, const SysDims& sd) {
   return env != 0 && sd.form == FORM_PRIMAL && d.nT <= KC_MAX_NT && sd.NT >= 2;
 }
 
-size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k, bool with_ebv) {
+}  // namespace
+
+OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol) {
+  OffPlan p{};
+  p.nI = NT - J - 1;
+  if (p.nI <= 0) {
+    p.nI = 0;
+    return p;
+  }
+  // launch j computes the partial sums of column j + 1's tiles
+  auto ahead_at = [&](int j) {
+    const bool on = ahead == 1 || (ahead < 0 && B < AHEAD_B);
+    return on && j >= 1 && j + 2 <= NT - 1;
+  };
+  p.nP = ahead_at(J) ? NT - 2 - J : 0;
+  p.ahead_cur = (J >= 2 && ahead_at(J - 1)) ? 1 : 0;
+  const int dt = (J >= 1 && J + 1 < NT) ? 1 : 0;   // diagonal target J + 1 (its partial over L < J)
+  p.nrs = 1;
+  p.nds = dt;
+  if (p.nP > 0 && st) {   // row slices need k_sys_tiles' counts (the int8 K is a whole-tile product)
+    for (int r : {1, 2, 4}) {
+      if (nrs_pol > 0 && r != nrs_pol) continue;
+      p.nrs = r;
+      p.nds = dt * (r >= 2 ? 2 : 1);
+      if (nrs_pol > 0 || B * p.units() >= 512) break;
+    }
+  }
+  p.n_kd = (J == 0 && NT > 2 && !st) ? B * (NT - 2) : 0;
+  return p;
+}
+
+namespace {
+
+bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
+  for (int J = 0; J < NT; ++J)
+    if (off_plan(B, NT, J, st, c->ahead, c->nrs).nP > 0) return true;
+  return false;
+}
+
+size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k,
+                   bool with_ebv) {
   size_t s = 0;
   auto add = [&](size_t x) { s = (size_t)round_up((int64_t)(s + x), 256); };
   add(sd.form == FORM_DUAL ? (size_t)B * sd.cblk * sd.prow * KBLK : 0);   // panel (dual only)
@@ -203,6 +247,8 @@ size_t chunk_bytes(const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_
   add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // next diagonal tile (minus its last SYRK term)
   add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
+  add(any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
+  add(c->qmode ? (size_t)B * 36 * 256 * 8 : 0);                // next diagonal's last SYRK term
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nt * d.nV * 8 : 0);              // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
@@ -283,6 +329,10 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* Kdg = cv.take<double>((size_t)B * sd.NT * 36 * 256);
   const bool use_st = sys_tiles(d, sd) && stop_stage != 1;
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
+  double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
+  double* Qp = c->qmode ? cv.take<double>((size_t)B * 36 * 256) : nullptr;
+  std::vector<OffPlan> plan(sd.NT);
+  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
@@ -312,13 +362,13 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
                 (const double*)sp.ymu.p, panel, pstride, d_off,
                 (const int8_t*)sp.geno.p, d_idx, d.nRp, (const uint8_t*)sp.gpk.p, d.nRp / 4, u, scal,
-                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb};
+                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb, Pp, Qp, c->qmode};
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
   if (c->wg_trace) {
     int64_t nwg = 0;
-    for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(B, sd.NT, J, use_st);
+    for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
@@ -352,9 +402,12 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const double Bd = (double)B;
   for (int J = 0; J < sd.NT; ++J) {
     const double jt = (double)J;
-    // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
-    // forward-substitution GEMV (the int8 GRM tiles are counted under KC_GRM)
-    const double fd = Bd * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
+    const OffPlan& p = plan[J];
+    // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile (unless tile (J, J-1)
+    // formed it: qmode), potrf + trtri, forward-substitution GEMV (the exact system tiles are
+    // counted under KC_GRM)
+    const double syrk_last = c->qmode ? 0.0 : T3 * std::min(jt, 1.0);
+    const double fd = Bd * (syrk_last + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
     const double bd = Bd * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
@@ -362,17 +415,21 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     }
     rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, s); });
     if (rc) return rc;
-    const int nI = sd.NT - J - 1;
-    if (nI > 0) {
-      // per tile: GEMM update 2*128^3*J, triangular solve 128^3 (fused GRM tile int-ops excluded);
-      // plus the preparation of diagonal tile J+1: 128^3 per L < J (lower half stored)
-      const double fo = Bd * nI * (2.0 * T3 * jt + T3) + Bd * T3 * jt;
-      const double bo = Bd * nI * (TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) + 2.0 * Bd * TILE * TILE * jt * 8.0;
+    if (p.nI > 0) {
+      // T-units: GEMM1 over the L not summed ahead (2*128^3 each) + the triangular solve 128^3,
+      // and Q (128^3) in tile (J+1, J); P-units: 2*128^3 per L < J; D-unit: 128^3 per L < J
+      // (lower half); the fused int8 GRM tiles' int-ops are excluded
+      const double lt = p.ahead_cur ? 1.0 : jt;
+      const double fo = Bd * p.nI * (2.0 * T3 * lt + T3) + (c->qmode ? Bd * T3 : 0.0) +
+                        Bd * p.nP * 2.0 * T3 * jt + (p.nds ? Bd * T3 * jt : 0.0);
+      const double bo = Bd * p.nI * (TILE * TILE * lt * 8.0 + TILE * TILE * 8.0) +
+                        Bd * p.nP * (2.0 * TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) +
+                        (p.nds ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
       if (wgt) {
         cl.wgt = wgt + c->wgt_used * WGT_REC;
-        c->wgt_used += offdiag_grid(B, sd.NT, J, use_st);
+        c->wgt_used += offdiag_grid(p, B);
       }
-      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(cl, J, s); });
+      rc = timed(c, s, KC_OFFDIAG, fo, bo, [&] { return launch_chol_offdiag(cl, J, p, s); });
       if (rc) return rc;
     }
   }
@@ -439,6 +496,9 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->wg_trace = wt && atoi(wt) != 0;
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
+  if (const char* e = getenv("TBLUP_AHEAD")) c->ahead = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
+  if (const char* e = getenv("TBLUP_QMODE")) c->qmode = atoi(e) != 0;
   if (!panel) {
     *out = c.release();
     return 0;
@@ -653,13 +713,13 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
     int64_t b1 = b0, sum_k = 0;
     while (b1 < batch) {
       const int64_t k = offsets[b1 + 1] - offsets[b1];
-      if (b1 > b0 && chunk_bytes(d, sd, b1 + 1 - b0, sum_k + k, want_ebv) > c->budget) break;
+      if (b1 > b0 && chunk_bytes(c, d, sd, b1 + 1 - b0, sum_k + k, want_ebv) > c->budget) break;
       if (b1 - b0 >= 65535) break;
       sum_k += k;
       ++b1;
     }
     const int64_t B = b1 - b0;
-    const size_t need = chunk_bytes(d, sd, B, sum_k, want_ebv);
+    const size_t need = chunk_bytes(c, d, sd, B, sum_k, want_ebv);
     HIPCHK(hipStreamSynchronize(c->stream));
     if (int rc = dev_alloc(c, c->ws, need)) return rc;
     Carve cv{(char*)c->ws.p};
@@ -700,7 +760,7 @@ int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, co
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const EvalDims d = dims_of(c, *sp);
   const SysDims sd = choose_sys(c, d, h_offsets, batch, branch, c->form_pref);
-  const size_t need = chunk_bytes(d, sd, batch, 0, false);
+  const size_t need = chunk_bytes(c, d, sd, batch, 0, false);
   if (need > c->ws.bytes) {
     // the workspace may still be in use by earlier work on either stream
     HIPCHK(hipStreamSynchronize(s));
@@ -804,7 +864,7 @@ int tblup_debug_grm(tblup_ctx* c, int split_id, const int64_t* idx, int64_t k, d
   const EvalDims d = dims_of(c, *sp);
   const SysDims sd = choose_sys(c, d, offs, 1, branch, 1);   // readback is of the kernel (dual) form
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (int rc = dev_alloc(c, c->ws, chunk_bytes(d, sd, 1, k, false) + (size_t)d.nRp * d.nTp * 8 + 4096)) return rc;
+  if (int rc = dev_alloc(c, c->ws, chunk_bytes(c, d, sd, 1, k, false) + (size_t)d.nRp * d.nTp * 8 + 4096)) return rc;
   Carve cv{(char*)c->ws.p};
   int64_t* d_idx = cv.take<int64_t>((size_t)k);
   int64_t* d_off = cv.take<int64_t>(2);

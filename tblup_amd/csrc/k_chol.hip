@@ -241,7 +241,6 @@ struct CholArgs {
   double* w;                // [B][nt][ns] forward-substitution partial sums
   double* S;                // [B][2][36*256] K_JJ - sum_{L<J-1} L_JL L_JL^T, slot J&1
   double* Kd;               // [B][NT][36*256] GRM diagonal tiles (k_diag_grm)
-  int NSX;                  // off-diagonal launch: diagonal-preparation workgroups per individual (0 or 1)
   const double* yT;         // [nt][ytp] dual right-hand sides (y_T - mu, on the fly)
   const double* rhs;        // [B][nt][ns] primal right-hand sides
   const int8_t* panel;      // [B] x pstride
@@ -264,6 +263,10 @@ struct CholArgs {
   uint64_t* wgt;            // workgroup trace records (TBLUP_WG_TRACE), null in production
   uint64_t* dtr;            // diagonal launch: phase timestamps of workgroup 0 (TBLUP_WG_TRACE), else null
   const int16_t* kc;        // SNP form: off-diagonal system-tile counts (k_sys_tiles), else null
+  double* part;             // [2][B][NT][128*128] off-diagonal partial sums K - sum_{L<J-1} (acc layout), slot J&1
+  double* Q;                // [B][36*256] L_{J+1,J} L_{J+1,J}^T (packed blocks) for the next diagonal tile
+  int64_t B;                // individuals in the chunk
+  int qmode;                // diagonal J takes its last SYRK term from Q (made by tile (J, J-1))
 };
 
 // st: profiling only (phase stamps of one factorisation in diagonal workgroup 0), else null
@@ -529,15 +532,19 @@ __device__ __forceinline__ void i8_tt2d_pk64(const uint8_t* sa, const uint8_t* s
   __syncthreads();
 }
 
-// GEMM1: acc[cb] -= sum_{k < 128J} L_J[c][k] L_I[i][k] for the wave's 16 columns i, on 32-row
-// stages: only A (the Lt_J stage every wave reads) goes through the LDS ring (2 x 32 KiB);
-// each wave's B operand (its own 16 columns of Lt_I) is loaded straight into registers one
-// stage ahead.  (A 16-row A+B ring has twice the barriers and measured 2% slower.)
-__device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const double* __restrict__ ltI, int J,
-                                          double* lds, v4d (&acc)[8]) {
+// GEMM1: acc[cb] -= sum_k L_J[c][k] L_I[i][k] over the nL Lt tiles starting at ltJ / ltI (k < 128 nL)
+// for the wave's 16 columns i and the NCB row blocks cb0 .. cb0+NCB-1, on 32-row stages: only A
+// (the Lt_J stage every wave reads) goes through the LDS ring (2 x 32 KiB); each wave's B operand
+// (its own 16 columns of Lt_I) is loaded straight into registers one stage ahead.  (A 16-row A+B
+// ring has twice the barriers and measured 2% slower.)  Every accumulator element's chain of MFMAs
+// is the same whatever NCB / cb0 and wherever the L range is split, so partial sums handed from
+// one launch to the next reproduce the one-workgroup result bit for bit.
+template <int NCB>
+__device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const double* __restrict__ ltI, int nL,
+                                          int cb0, double* lds, v4d (&acc)[NCB]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   constexpr int AS = 32 * TILE;   // doubles per 32-row stage
-  const int nst = 4 * J;
+  const int nst = 4 * nL;
   if (nst == 0) return;
   auto src_of = [&](int s) { return (int64_t)(s >> 2) * TT + (s & 3) * AS; };
   auto issue_a = [&](int s) {
@@ -566,7 +573,8 @@ __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const 
     for (int kk = 0; kk < 8; ++kk) {
       const int k = 4 * kk + (l >> 4);
 #pragma unroll
-      for (int cb = 0; cb < 8; ++cb) acc[cb] = mfma64_nega(As[lt_off(k, 16 * cb + (l & 15))], bc[kk], acc[cb]);
+      for (int cb = 0; cb < NCB; ++cb)
+        acc[cb] = mfma64_nega(As[lt_off(k, 16 * (cb0 + cb) + (l & 15))], bc[kk], acc[cb]);
       // B of the next stage into the register this k-step has consumed
       if (more) bc[kk] = bs[4 * kk * TILE];
     }
@@ -576,8 +584,8 @@ __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const 
 }
 
 // SYRK of Lt stages restricted to the 36 lower blocks, 8 waves: wave W takes blocks
-// W + 8i (5 blocks for W < 4, 4 for W >= 4).
-template <int W>
+// W + 8i (5 blocks for W < 4, 4 for W >= 4); only the i in MASK (a diagonal-target slice).
+template <int W, int MASK>
 __device__ __forceinline__ void syrk_stage8(const double* As, v4d (&acc)[5], int l) {
   constexpr int NBW = (W < 4) ? 5 : 4;
 #pragma unroll
@@ -587,13 +595,18 @@ __device__ __forceinline__ void syrk_stage8(const double* As, v4d (&acc)[5], int
 #pragma unroll
     for (int q = 0; q < 8; ++q) a8[q] = As[lt_off(k, 16 * q + (l & 15))];
 #pragma unroll
-    for (int i = 0; i < NBW; ++i) acc[i] = mfma64(a8[tri_q(W + 8 * i)], a8[tri_s(W + 8 * i)], acc[i]);
+    for (int i = 0; i < NBW; ++i)
+      if ((MASK >> i) & 1) acc[i] = mfma64(a8[tri_q(W + 8 * i)], a8[tri_s(W + 8 * i)], acc[i]);
   }
 }
 
-// SYRK of Lt rows restricted to the 36 lower blocks, 8 waves (wave W takes blocks W + 8i),
-// on 32-row stages through a 2 x 32 KiB LDS-DMA ring: one barrier per 32 k rows.
-__device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, int nst16, double* lds, v4d (&acc)[5]) {
+// block masks of the diagonal-target slices: all blocks; even i; odd i
+__host__ __device__ constexpr int slice_mask(int sl) { return sl == 0 ? 0x1F : sl == 1 ? 0x15 : 0x0A; }
+
+// SYRK of Lt rows restricted to the 36 lower blocks, 8 waves (wave W takes blocks W + 8i, i in
+// slice_mask(sl)), on 32-row stages through a 2 x 32 KiB LDS-DMA ring: one barrier per 32 k rows.
+__device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, int nst16, double* lds, v4d (&acc)[5],
+                                               int sl = 0) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (nst16 <= 0) return;
   constexpr int AS = 32 * TILE;
@@ -608,47 +621,59 @@ __device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, i
     }
   };
   issue(0);
+  const int ws = w + 8 * sl;   // wave-uniform (wave, slice) instantiation
   for (int s = 0; s < nst; ++s) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (s + 1 < nst) issue(s + 1);
     const double* As = lds + (s & 1) * AS;
-    switch (w) {
-      case 0: syrk_stage8<0>(As, acc, l); syrk_stage8<0>(As + LTS, acc, l); break;
-      case 1: syrk_stage8<1>(As, acc, l); syrk_stage8<1>(As + LTS, acc, l); break;
-      case 2: syrk_stage8<2>(As, acc, l); syrk_stage8<2>(As + LTS, acc, l); break;
-      case 3: syrk_stage8<3>(As, acc, l); syrk_stage8<3>(As + LTS, acc, l); break;
-      case 4: syrk_stage8<4>(As, acc, l); syrk_stage8<4>(As + LTS, acc, l); break;
-      case 5: syrk_stage8<5>(As, acc, l); syrk_stage8<5>(As + LTS, acc, l); break;
-      case 6: syrk_stage8<6>(As, acc, l); syrk_stage8<6>(As + LTS, acc, l); break;
-      default: syrk_stage8<7>(As, acc, l); syrk_stage8<7>(As + LTS, acc, l); break;
+#define SYRK_CASE(W, SL)                                    \
+  case W + 8 * SL:                                          \
+    syrk_stage8<W, slice_mask(SL)>(As, acc, l);             \
+    syrk_stage8<W, slice_mask(SL)>(As + LTS, acc, l);       \
+    break;
+#define SYRK_CASES(SL) SYRK_CASE(0, SL) SYRK_CASE(1, SL) SYRK_CASE(2, SL) SYRK_CASE(3, SL) \
+                       SYRK_CASE(4, SL) SYRK_CASE(5, SL) SYRK_CASE(6, SL) SYRK_CASE(7, SL)
+    switch (ws) {
+      SYRK_CASES(0)
+      SYRK_CASES(1)
+      SYRK_CASES(2)
+      default: break;
     }
+#undef SYRK_CASES
+#undef SYRK_CASE
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 }
 
-// S[b][Jt&1] = K_{Jt,Jt} - sum_{L < nterm} L_{Jt,L} L_{Jt,L}^T (packed blocks), 8 waves.
-__device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int Jt, int nterm, double* lds) {
+// Packed-block store of a wave's SYRK accumulators (blocks W + 8i, i in the slice):
+// dst[o] = base[o] - acc (base null: dst[o] = acc).
+__device__ __forceinline__ void store_syrk_blocks(double* dst, const double* base, const v4d (&acc)[5], int sl) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  v4d acc[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-  if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc);
-  const double* Kb = a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD;
-  double* Pd = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
     const int e = w + 8 * i;
-    if (e < NPACK) {
+    if (e < NPACK && ((slice_mask(sl) >> i) & 1)) {
       const int q = tri_q_rt(e), sb = e - q * (q + 1) / 2;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = pk(q, sb) + bo((l >> 4) + 4 * r, l & 15);
-        Pd[o] = Kb[o] - acc[i][r];
+        dst[o] = base ? base[o] - acc[i][r] : acc[i][r];
       }
     }
   }
+}
+
+// S[b][Jt&1] = K_{Jt,Jt} - sum_{L < nterm} L_{Jt,L} L_{Jt,L}^T (packed blocks; the blocks of slice
+// sl only), 8 waves: the diagonal target's partial sum.
+__device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int Jt, int nterm, double* lds, int sl) {
+  v4d acc[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
+  if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc, sl);
+  store_syrk_blocks(a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD,
+                    a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD, acc, sl);
 }
 
 // ---------------------------------------------------------------------------
@@ -762,7 +787,24 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   // launch's loads are HBM-bound and the SYRK at 2 waves per SIMD then runs after them.)
   const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
                                 : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
-  {
+  if (a.qmode && J > 0) {
+    // the last SYRK term was formed by the workgroup of tile (J, J-1) in the previous launch (Q):
+    // every lane subtracts it from exactly the 16-B pieces its own LDS-DMA brought in
+    const double* q = a.Q + b * (int64_t)NPACK * BLKD;
+    v2d qv[NPACK * BLKD / 2 / DTHR];
+#pragma unroll
+    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
+      const int chunk = (e * DW + w) * 64;
+      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
+      qv[e] = *reinterpret_cast<const v2d*>(q + 2 * (chunk + l));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {
+      v2d* tv = reinterpret_cast<v2d*>(Tp + 2 * ((e * DW + w) * 64 + l));
+      *tv = *tv - qv[e];
+    }
+  } else {
 #pragma unroll
     for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
       const int chunk = (e * DW + w) * 64;
@@ -932,78 +974,74 @@ __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// off-diagonal tiles of column J (one WG per individual x tile row I > J)
-//   0. cnt = A_J A_I^T on int8 MFMA, landing in the f64 layout; acc = K_JI = K_IJ^T
-//   1. acc -= sum_{L<J} L_JL L_IL^T          (acc = T^T, wave w holds all c x its 32 i)
-//   2. out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb]   (X = inv(L_JJ); acc is the B operand)
-//      -> Lt tile (I, J); w_I += L_IJ z_J
-// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
-
+// Off-diagonal launch of column J: one 8-wave workgroup per unit, two per CU (LDS <= 72 KiB).
+//   T-unit, tile (I, J), I > J:
+//     0. acc = K_JI in the f64 accumulator layout: from k_sys_tiles' counts (SNP form) or int8
+//        MFMA here (rows permuted so the counts land in the f64 layout) -- or, when launch J-1 ran
+//        ahead, its partial sum K_JI - sum_{L<J-1} L_JL L_IL^T
+//     1. acc -= sum_{L} L_JL L_IL^T over the L < J not summed yet   (acc = T^T, wave w: its 16 i)
+//     2. out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb]   (X = inv(L_JJ); acc is the B operand)
+//        -> Lt tile (I, J); w_I += L_IJ z_J
+//     3. (qmode, I = J+1) Q = L_{J+1,J} L_{J+1,J}^T on the 36 lower blocks: the next diagonal
+//        kernel's last SYRK term, off its chain
+//   P-unit (ahead), tile (I, J+1), I >= J+2, row blocks of slice rs: acc = K - sum_{L<J} (steps 0-1
+//     of launch J+1's T-unit, which continues the same MFMA chains: bit-identical results)
+//   D-unit, diagonal tile J+1, block slice: S = K - sum_{L<J} L_{J+1,L} L_{J+1,L}^T (packed blocks)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I, double* lds, double* uj_sh,
-                                             double* ui_sh, double (*zj_sh)[TILE]) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int J = a.J, NT = a.NT;
-  const int64_t ns = a.ns;
-  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
-  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+
+// K_{I,Jt} (the T^T layout of tile (I, Jt)) for the NCB row blocks from cb0: exact counts of
+// k_sys_tiles (loads issued by kc_issue) or, NCB = 8 only, the int8 tile here.
+template <int NCB>
+__device__ __forceinline__ void kc_issue(const CholArgs& a, int64_t b, int I, int Jt, int cb0, int2 (&kcv)[NCB]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int NT = a.NT;
+  const int16_t* kt = a.kc + ((b * (NT * (NT - 1) / 2)) + I * (I - 1) / 2 + Jt) * KC_TILE + w * 8 * 64 * 4;
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) kcv[cb] = *reinterpret_cast<const int2*>(kt + ((cb0 + cb) * 64 + l) * 4);
+}
+
+template <int NCB>
+__device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int Jt, int cb0, const int2 (&kcv)[NCB],
+                                      uint8_t* lds8, const double* uj_sh, const double* ui_sh, v4d (&acc)[NCB]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)Jt * TILE;
   const double* sc = a.scal + b * SCAL;
   const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], sm = sc[SC_SM];
   const int64_t nrow = (int64_t)sc[SC_NROW];
-  int2 kcv[8];
+  const int il = 16 * w + (l & 15);
+  const bool ireal = i0 + il < nrow;
   if (a.kc) {
-    const int16_t* kt = a.kc + ((b * (NT * (NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE + w * 8 * 64 * 4;
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) kcv[cb] = *reinterpret_cast<const int2*>(kt + (cb * 64 + l) * 4);
-  }
-  if (t < TILE) {
-    uj_sh[t] = a.u[b * a.prow + j0 + t];
-    ui_sh[t] = a.u[b * a.prow + i0 + t];
-#pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr)
-      zj_sh[tr][t] = (tr < a.nt) ? a.z[(b * a.nt + tr) * ns + j0 + t] : 0.0;
-  }
-  __syncthreads();
-
-  // 0. K_JI: from k_sys_tiles' counts (SNP form; loads issued now, applied after GEMM1), or on
-  //    int8 MFMA here (16x16x64, rows permuted so the counts land in the f64 layout)
-  v4d acc[8];
-  if (a.kc) {
-    // counts issued before the u / z loads above landed; exact ints -> fp64 K (same epilogue as
-    // the in-tile path below)
+    // counts issued before the u / z loads landed; exact ints -> fp64 K
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int il = 16 * w + (l & 15);
-    const bool ireal = i0 + il < nrow;
 #pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
+    for (int cb = 0; cb < NCB; ++cb) {
       const int32_t c4[4] = {(int32_t)(int16_t)(kcv[cb].x & 0xffff), (int32_t)(int16_t)(kcv[cb].x >> 16),
                              (int32_t)(int16_t)(kcv[cb].y & 0xffff), (int32_t)(int16_t)(kcv[cb].y >> 16)};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int cl = 16 * cb + (l >> 4) + 4 * r;
+        const int cl = 16 * (cb0 + cb) + (l >> 4) + 4 * r;
         const double v = grm_value(c4[r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
         acc[cb][r] = (ireal && j0 + cl < nrow) ? v : 0.0;
       }
     }
-  } else {
+    return;
+  }
+  if constexpr (NCB == 8) {
     v4i cnt[8];
     const int64_t nblk = (int64_t)sc[SC_CBLK];
     if (!(a.skip & 32) && a.form == FORM_PRIMAL) {
       const int row = 16 * w + (l >> 2), pos = l & 3;
       i8_tt2d_pk64<4>(row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
-                      row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk,
-                      reinterpret_cast<uint8_t*>(lds), cnt);
+                      row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, lds8, cnt);
     } else if (!(a.skip & 32)) {
       const int row = 16 * w + (l >> 2), pos = l & 3;
       i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
                 row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, a.prow * KBLK,
-                reinterpret_cast<int8_t*>(lds), cnt);
+                reinterpret_cast<int8_t*>(lds8), cnt);
     } else {
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
     }
-    const int il = 16 * w + (l & 15);
-    const bool ireal = i0 + il < nrow;
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb) {
 #pragma unroll
@@ -1014,9 +1052,76 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
       }
     }
   }
+}
 
-  // 1. T^T = K_JI - sum_L L_JL L_IL^T
-  if (J > 0 && !(a.skip & 64)) gemm1_a32(Lb + (int64_t)J * NT * TT, Lb + (int64_t)I * NT * TT, J, lds, acc);
+// Partial sums of launch J+1's tiles, acc layout: [slot Jt&1][b][I][wave][cb][lane][4]
+__device__ __forceinline__ double* part_ptr(const CholArgs& a, int64_t b, int I, int Jt) {
+  return a.part + (((int64_t)(Jt & 1) * a.B + b) * a.NT + I) * TT + (threadIdx.x >> 6) * 8 * 64 * 4;
+}
+
+// P-unit: acc = K_{I,J+1} - sum_{L<J} L_{J+1,L} L_{I,L}^T for row blocks [cb0, cb0 + NCB).
+template <int NCB>
+__device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, int rs, double* lds, double* uj_sh,
+                                          double* ui_sh) {
+  const int t = threadIdx.x, l = t & 63;
+  const int J = a.J, Jt = J + 1, NT = a.NT, cb0 = rs * NCB;
+  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)Jt * TILE;
+  int2 kcv[NCB];
+  if (a.kc) kc_issue<NCB>(a, b, I, Jt, cb0, kcv);
+  if (t < TILE) {
+    uj_sh[t] = a.u[b * a.prow + j0 + t];
+    ui_sh[t] = a.u[b * a.prow + i0 + t];
+  }
+  __syncthreads();
+  v4d acc[NCB];
+  k_acc<NCB>(a, b, I, Jt, cb0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
+  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+  if (!(a.skip & 64)) gemm1_a32<NCB>(Lb + (int64_t)Jt * NT * TT, Lb + (int64_t)I * NT * TT, J, cb0, lds, acc);
+  double* pd = part_ptr(a, b, I, Jt);
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    v2d* d = reinterpret_cast<v2d*>(pd + ((cb0 + cb) * 64 + l) * 4);
+    d[0] = v2d{acc[cb][0], acc[cb][1]};
+    d[1] = v2d{acc[cb][2], acc[cb][3]};
+  }
+}
+
+// T-unit: tile (I, J).
+__device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, int ahead_cur, double* lds,
+                                          double* uj_sh, double* ui_sh, double (*zj_sh)[TILE]) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int J = a.J, NT = a.NT;
+  const int64_t ns = a.ns;
+  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
+  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+  v4d acc[8];
+  int2 kcv[8];
+  if (ahead_cur) {
+    const double* pd = part_ptr(a, b, I, J);
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const v2d* s2 = reinterpret_cast<const v2d*>(pd + (cb * 64 + l) * 4);
+      const v2d lo = s2[0], hi = s2[1];
+      acc[cb] = v4d{lo[0], lo[1], hi[0], hi[1]};
+    }
+  } else if (a.kc) {
+    kc_issue<8>(a, b, I, J, 0, kcv);
+  }
+  if (t < TILE) {
+    uj_sh[t] = a.u[b * a.prow + j0 + t];
+    ui_sh[t] = a.u[b * a.prow + i0 + t];
+#pragma unroll
+    for (int tr = 0; tr < MAXT; ++tr)
+      zj_sh[tr][t] = (tr < a.nt) ? a.z[(b * a.nt + tr) * ns + j0 + t] : 0.0;
+  }
+  __syncthreads();
+  if (!ahead_cur) k_acc<8>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
+
+  // 1. T^T = K_JI - sum_L L_JL L_IL^T over the L not summed by launch J-1
+  const int Ls = ahead_cur ? J - 1 : 0;
+  if (J > Ls && !(a.skip & 64))
+    gemm1_a32<8>(Lb + (int64_t)J * NT * TT + (int64_t)Ls * TT, Lb + (int64_t)I * NT * TT + (int64_t)Ls * TT, J - Ls, 0,
+                 lds, acc);
 
   // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X in the
   //    packed block layout (blocks transposed): all 36 blocks (72 KiB) land in LDS in one
@@ -1067,6 +1172,19 @@ __device__ __forceinline__ void offdiag_tile(const CholArgs& a, int64_t b, int I
         a.w[gi] = (J == 0) ? v : a.w[gi] + v;
       }
     }
+  }
+
+
+  // 3. Q = L_{J+1,J} L_{J+1,J}^T (36 lower blocks) from the Lt tile just stored: this workgroup's
+  //    own stores, complete (vmcnt) and ordered before the reads by the barrier
+  if (a.qmode && I == J + 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    v4d q5[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) q5[i] = v4d{0.0, 0.0, 0.0, 0.0};
+    if (!(a.skip & 2)) syrk_lower8_32(Lout, 8, lds, q5);
+    store_syrk_blocks(a.Q + b * (int64_t)NPACK * BLKD, nullptr, q5, 0);
   }
 }
 
@@ -1144,32 +1262,48 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
   }
 }
 
-// Off-diagonal tiles (I, J) for I0 <= I < I0 + nI, plus (first in the grid, so they
-// overlap the tiles) one workgroup per individual preparing diagonal tile J+1 except its
-// L = J term: S[(J+1)&1] = K - sum_{L<J} (those tiles are final already).
-// LDS: ring / stages <= 64 KiB, so two workgroups share a CU.
-__global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, int I0, int nI, int64_t n_tiles, int64_t n_kd) {
+// Off-diagonal launch of column J (see OffPlan): per individual, its P-units (longest first),
+// D-units, then its T-units -- all of them contiguous in the XCD-remapped order, so one XCD's L2
+// serves the individual's Lt block rows -- and, column 0 of the kernel form only, the K_JJ
+// workgroups for J >= 2 at the end of the grid.
+__global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) {
   __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
   __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
-  const int64_t n_extra = (int64_t)gridDim.x - n_tiles - n_kd;
+  const int64_t U = p.units();
+  const int64_t n_units = a.B * U;
   const int64_t bid = blockIdx.x;
   WgTrace tr(a.wgt);
-  if (bid < n_extra) {
-    const int64_t b = xcd_remap(bid, n_extra);
-    syrk_partial8(a, b, a.J + 1, a.J, lds);
-    tr.done(WGT_PREP, a.J, a.J + 1, b);
-    return;
-  }
-  if (bid >= n_extra + n_tiles) {   // column 0 only: K_JJ for J >= 2
-    const int64_t lg = xcd_remap(bid - n_extra - n_tiles, n_kd);
+  if (bid >= n_units) {   // column 0, kernel form: K_JJ for J >= 2
+    const int64_t lg = xcd_remap(bid - n_units, p.n_kd);
     const int nJ = a.NT - 2;
     diag_grm_tile(a, lg / nJ, 2 + (int)(lg % nJ), reinterpret_cast<uint8_t*>(lds), uj_sh);
     tr.done(WGT_KJJ, a.J, 2 + (int)(lg % nJ), lg / nJ);
     return;
   }
-  const int64_t logical = xcd_remap(bid - n_extra, n_tiles);
-  offdiag_tile(a, logical / nI, I0 + (int)(logical % nI), lds, uj_sh, ui_sh, zj_sh);
-  tr.done(WGT_TILE, a.J, I0 + (int)(logical % nI), logical / nI);
+  const int64_t logical = xcd_remap(bid, n_units);
+  const int64_t b = logical / U;
+  int u = (int)(logical % U);
+  const int npu = p.nP * p.nrs;
+  if (u < npu) {
+    const int I = a.J + 2 + u / p.nrs, rs = u % p.nrs;
+    switch (p.nrs) {
+      case 1: part_unit<8>(a, b, I, rs, lds, uj_sh, ui_sh); break;
+      case 2: part_unit<4>(a, b, I, rs, lds, uj_sh, ui_sh); break;
+      default: part_unit<2>(a, b, I, rs, lds, uj_sh, ui_sh); break;
+    }
+    tr.done(WGT_PART, a.J, I, b);
+    return;
+  }
+  u -= npu;
+  if (u < p.nds) {
+    syrk_partial8(a, b, a.J + 1, a.J, lds, p.nds == 1 ? 0 : 1 + u);
+    tr.done(WGT_PREP, a.J, a.J + 1, b);
+    return;
+  }
+  u -= p.nds;
+  const int I = a.J + 1 + u;
+  tile_unit(a, b, I, p.ahead_cur, lds, uj_sh, ui_sh, zj_sh);
+  tr.done(WGT_TILE, a.J, I, b);
 }
 
 // ===========================================================================
@@ -1323,10 +1457,15 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
     }
 }
 
+static CholArgs make_args(const CholLaunch& c, int J) {
+  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
+             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
+             c.wgt, nullptr, c.kc, c.part, c.Q, c.B, c.qmode};
+  return a;
+}
+
 hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
-  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip,
-             c.wgt, nullptr, c.kc};
+  CholArgs a = make_args(c, 0);
   const int ntri = c.sd.NT * (c.sd.NT + 1) / 2;
   hipLaunchKernelGGL(k_sys_tiles, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
   return hipGetLastError();
@@ -1340,32 +1479,25 @@ __global__ __launch_bounds__(OTH, 2) void k_diag_grm8(CholArgs a, int nJ) {
 }
 
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
-  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, 0, c.skip, nullptr, nullptr, c.kc};
+  CholArgs a = make_args(c, 0);
+  a.wgt = nullptr;
   const int nJ = std::min(c.sd.NT, 2);
   hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * nJ)), dim3(OTH), 0, s, a, nJ);
   return hipGetLastError();
 }
 
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
-  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr, c.kc};
+  CholArgs a = make_args(c, J);
   // profiling: the phase stamps of this launch follow its B workgroup records
   if (c.wgt) a.dtr = c.wgt + c.B * WGT_REC;
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s) {
-  CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, 0, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip, c.wgt, nullptr, c.kc};
-  const int I0 = J + 1, nI = c.sd.NT - I0;
-  if (nI <= 0) return hipSuccess;
-  a.NSX = (J >= 1 && J + 1 < c.sd.NT) ? 1 : 0;
-  const int64_t n_tiles = c.B * nI;
-  const int64_t n_kd = (J == 0 && c.sd.NT > 2 && !c.kc) ? c.B * (c.sd.NT - 2) : 0;
-  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)offdiag_grid(c.B, c.sd.NT, J, c.kc != nullptr)), dim3(OTH), 0, s,
-                     a, I0, nI, n_tiles, n_kd);
+hipError_t launch_chol_offdiag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s) {
+  if (p.nI <= 0) return hipSuccess;
+  CholArgs a = make_args(c, J);
+  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)offdiag_grid(p, c.B)), dim3(OTH), 0, s, a, p);
   return hipGetLastError();
 }
 

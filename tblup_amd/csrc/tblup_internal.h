@@ -150,6 +150,9 @@ struct CholLaunch {
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
   uint64_t* wgt;         // per-workgroup timestamp records of this launch (env TBLUP_WG_TRACE), else null
   int16_t* kc;           // SNP form: exact off-diagonal system-tile counts from k_sys_tiles, else null
+  double* part;          // [2][B][NT][128*128] partial sums of the next column's tiles (ahead schedule)
+  double* Q;             // [B][36*256] last SYRK term of the next diagonal tile (qmode)
+  int qmode;             // tile (J+1, J) forms Q; the diagonal kernel subtracts it instead of a SYRK
 };
 // k_sys_tiles output: per individual NT(NT-1)/2 off-diagonal tiles (I > J, t = I(I-1)/2 + J) of
 // 128 x 128 int16 counts, in the order the off-diagonal kernel's lanes read them:
@@ -162,19 +165,29 @@ constexpr int WGT_REC = 4;
 // a diagonal launch's records are followed by DTR_RECS records holding the phase stamps of
 // its workgroup 0 (8 waves x 64 uint64), written as kind-0 records
 constexpr int DTR_RECS = 8 * 64 / WGT_REC;
-enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5 };
-// workgroups launched by launch_chol_offdiag for column J (also the trace stride)
-inline int64_t offdiag_grid(int64_t B, int NT, int J, bool sys_tiles) {
-  const int nI = NT - J - 1;
-  if (nI <= 0) return 0;
-  const int nsx = (J >= 1 && J + 1 < NT) ? 1 : 0;
-  const int64_t n_kd = (J == 0 && NT > 2 && !sys_tiles) ? B * (NT - 2) : 0;
-  return B * nI + B * nsx + n_kd;
-}
+enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_PART = 6 };
+// Work units of the off-diagonal launch of column J, per individual (k_chol.hip):
+//   nI  T-units: tiles (I, J), I > J
+//   nP  x nrs P-units (ahead schedule): partial sums K - sum_{L<J} of tiles (I, J+1), I >= J+2, in
+//       nrs row slices -- launch J+1's T-units then start from them (ahead_cur) and sum one L
+//   nds D-units: the diagonal tile J+1's partial sum over L < J (1 or 2 block slices)
+//   n_kd K_JJ workgroups (column 0 of the kernel form only)
+struct OffPlan {
+  int nI, nP, nrs, nds, ahead_cur;
+  int64_t n_kd;
+  __host__ __device__ int64_t units() const { return (int64_t)nP * nrs + nds + nI; }
+};
+// Schedule policy (host, per chunk: a function of B and the system shape only, so the results
+// are bit-identical for any policy -- every accumulator keeps its MFMA chain):
+//   ahead: -1 auto (ahead when B < AHEAD_B), 0 never, 1 always; nrs: 0 auto (fill >= 2 units per CU
+//   slot pair), else fixed 1 / 2 / 4; dual: no k_sys_tiles counts (int8 K in-tile: nrs = 1)
+constexpr int64_t AHEAD_B = 192;
+OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs);
+inline int64_t offdiag_grid(const OffPlan& p, int64_t B) { return p.nI > 0 ? B * p.units() + p.n_kd : 0; }
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
 // then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.
 hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s);
-hipError_t launch_chol_offdiag(const CholLaunch& c, int J, hipStream_t s);
+hipError_t launch_chol_offdiag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s);
 // all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 // SNP form: every (I >= J) system tile of the batch on int8 MFMA in one launch -- off-diagonal

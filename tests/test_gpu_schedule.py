@@ -1,0 +1,88 @@
+"""Cholesky schedule invariance: the classic column schedule, the ahead schedule (partial sums of
+the next column's tiles computed one launch early, in 1 / 2 / 4 row slices) and Q (the next
+diagonal's last SYRK term formed by tile (J+1, J)) redistribute the same MFMA chains over
+workgroups and launches, so fitness and EBVs must be bit-identical under every setting, for
+both system forms and for system sizes from 1 to 8+ tile columns; and equal to the oracle.
+(TBLUP_AHEAD / TBLUP_NRS / TBLUP_QMODE are read when a context is created.)"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import blup_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SETTINGS = [
+    {"TBLUP_AHEAD": "0", "TBLUP_QMODE": "0"},       # round-2 schedule
+    {"TBLUP_AHEAD": "0", "TBLUP_QMODE": "1"},
+    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "1", "TBLUP_QMODE": "1"},
+    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "2", "TBLUP_QMODE": "0"},
+    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "4", "TBLUP_QMODE": "1"},
+    {"TBLUP_AHEAD": "-1", "TBLUP_NRS": "0", "TBLUP_QMODE": "1"},   # the defaults
+]
+
+
+def _evaluate(geno, pheno, genomes, T, V, env, form=None, multi=None):
+    from tblup_amd.engine import GpuBlupEngine
+    keys = list(env) + ["TBLUP_FORM"]
+    old = {k: os.environ.get(k) for k in keys}
+    try:
+        os.environ.update(env)
+        if form is not None:
+            os.environ["TBLUP_FORM"] = str(form)
+        with GpuBlupEngine(geno, pheno if multi is None else multi, device=0) as eng:
+            groups = genomes if isinstance(genomes[0], list) else [genomes]
+            out = [eng.evaluate(g, T, V, 0.4, return_ebv=True) for g in groups]
+            return np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out])
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def panel():
+    rng = np.random.default_rng(21)
+    n, p = 2000, 20_000
+    geno = O.synth_geno(rng, n, p)
+    pheno = rng.standard_normal(n)
+    perm = rng.permutation(n)
+    return {"geno": geno, "pheno": pheno, "T": perm[:1280], "V": perm[1280:1600], "rng": rng}
+
+
+@pytest.mark.parametrize("form", [None, 1])
+def test_schedules_are_bit_identical(panel, gpu, form):
+    """k from 100 (1 tile column) to 1100 (9): SNP form (default) and kernel form (TBLUP_FORM=1:
+    int8 K inside the units, whole-tile partials) -- every setting gives the same bits."""
+    rng = np.random.default_rng(5)
+    # one batch per system size (the batch's largest k sets the tile columns) and a mixed one
+    groups = [[rng.choice(20_000, k, replace=False) for _ in range(6)] for k in (100, 250, 640, 1000, 1100)]
+    groups.append([rng.choice(20_000, k, replace=False) for k in (383, 1000, 777, 900, 128, 1024)])
+    genomes = [g for grp in groups for g in grp]
+    ref = None
+    for env in SETTINGS:
+        fit, ebv = _evaluate(panel["geno"], panel["pheno"], groups, panel["T"], panel["V"], env, form)
+        if ref is None:
+            ref = (fit, ebv)
+            continue
+        np.testing.assert_array_equal(fit, ref[0], err_msg=str(env))
+        np.testing.assert_array_equal(ebv, ref[1], err_msg=str(env))
+    for i in (0, 14, 25, 31):
+        f, e = O.blup_grm_form(genomes[i], panel["T"], panel["V"], panel["geno"], panel["pheno"], 0.4)
+        assert abs(ref[0][i] - f) <= 1e-9
+
+
+def test_schedules_small_batches_and_traits(panel, gpu):
+    """Batches of 1, 3 and 40 individuals (the ahead schedule's auto row slicing changes with B),
+    3 traits: identical to the round-2 schedule."""
+    rng = np.random.default_rng(6)
+    multi = np.stack([panel["pheno"], rng.standard_normal(2000), rng.standard_normal(2000)], axis=1)
+    for B in (1, 3, 40):
+        genomes = [rng.choice(20_000, 1000, replace=False) for _ in range(B)]
+        a = _evaluate(panel["geno"], None, genomes, panel["T"], panel["V"], SETTINGS[0], multi=multi)
+        b = _evaluate(panel["geno"], None, genomes, panel["T"], panel["V"], SETTINGS[-1], multi=multi)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])

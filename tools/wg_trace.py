@@ -17,7 +17,7 @@ os.environ["TBLUP_WG_TRACE"] = "1"
 
 import bench  # noqa: E402
 
-KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys"}
+KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part"}
 
 
 def main():
