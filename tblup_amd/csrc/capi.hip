@@ -100,7 +100,6 @@ struct tblup_ctx {
   // Cholesky schedule (results are bit-identical under every setting; see OffPlan):
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (B < AHEAD_B), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
-  int qmode = 1;      // TBLUP_QMODE: tile (J+1, J) forms the next diagonal's last SYRK term
 };
 
 namespace {
@@ -213,12 +212,13 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   p.nrs = 1;
   p.nds = dt;
   if (p.nP > 0 && st) {   // row slices need k_sys_tiles' counts (the int8 K is a whole-tile product)
-    for (int r : {1, 2, 4}) {
-      if (nrs_pol > 0 && r != nrs_pol) continue;
-      p.nrs = r;
-      p.nds = dt * (r >= 2 ? 2 : 1);
-      if (nrs_pol > 0 || B * p.units() >= 512) break;
-    }
+    // unit work in 2*128^3-flop GEMM units: T-unit 1 + 0.5 (GEMM2), P-unit J / nrs, D-unit J / 2 / nds;
+    // slice until no P- or D-unit is longer than a T-unit or the launch's work per slot (two per CU)
+    const double jt = J, tw = 1.5;
+    const double per_slot = (double)B * (p.nI * tw + p.nP * jt + 0.5 * jt) / 512.0;
+    const double cap = std::max(per_slot, tw);
+    p.nrs = nrs_pol > 0 ? nrs_pol : (jt <= cap ? 1 : jt / 2.0 <= cap ? 2 : 4);
+    p.nds = dt * ((0.5 * jt <= cap && nrs_pol <= 1) ? 1 : 2);
   }
   p.n_kd = (J == 0 && NT > 2 && !st) ? B * (NT - 2) : 0;
   return p;
@@ -248,7 +248,6 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
   add(any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
-  add(c->qmode ? (size_t)B * 36 * 256 * 8 : 0);                // next diagonal's last SYRK term
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nt * d.nV * 8 : 0);              // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
@@ -330,7 +329,6 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const bool use_st = sys_tiles(d, sd) && stop_stage != 1;
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
   double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
-  double* Qp = c->qmode ? cv.take<double>((size_t)B * 36 * 256) : nullptr;
   std::vector<OffPlan> plan(sd.NT);
   for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
@@ -362,7 +360,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
                 (const double*)sp.ymu.p, panel, pstride, d_off,
                 (const int8_t*)sp.geno.p, d_idx, d.nRp, (const uint8_t*)sp.gpk.p, d.nRp / 4, u, scal,
-                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb, Pp, Qp, c->qmode};
+                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb, Pp};
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
@@ -403,11 +401,9 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   for (int J = 0; J < sd.NT; ++J) {
     const double jt = (double)J;
     const OffPlan& p = plan[J];
-    // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile (unless tile (J, J-1)
-    // formed it: qmode), potrf + trtri, forward-substitution GEMV (the exact system tiles are
-    // counted under KC_GRM)
-    const double syrk_last = c->qmode ? 0.0 : T3 * std::min(jt, 1.0);
-    const double fd = Bd * (syrk_last + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
+    // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
+    // forward-substitution GEMV (the exact system tiles are counted under KC_GRM)
+    const double fd = Bd * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
     const double bd = Bd * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
@@ -416,12 +412,11 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, s); });
     if (rc) return rc;
     if (p.nI > 0) {
-      // T-units: GEMM1 over the L not summed ahead (2*128^3 each) + the triangular solve 128^3,
-      // and Q (128^3) in tile (J+1, J); P-units: 2*128^3 per L < J; D-unit: 128^3 per L < J
-      // (lower half); the fused int8 GRM tiles' int-ops are excluded
+      // T-units: GEMM1 over the L not summed ahead (2*128^3 each) + the triangular solve 128^3;
+      // P-units: 2*128^3 per L < J; D-unit: 128^3 per L < J (lower half); the fused int8 GRM
+      // tiles' int-ops are excluded
       const double lt = p.ahead_cur ? 1.0 : jt;
-      const double fo = Bd * p.nI * (2.0 * T3 * lt + T3) + (c->qmode ? Bd * T3 : 0.0) +
-                        Bd * p.nP * 2.0 * T3 * jt + (p.nds ? Bd * T3 * jt : 0.0);
+      const double fo = Bd * p.nI * (2.0 * T3 * lt + T3) + Bd * p.nP * 2.0 * T3 * jt + (p.nds ? Bd * T3 * jt : 0.0);
       const double bo = Bd * p.nI * (TILE * TILE * lt * 8.0 + TILE * TILE * 8.0) +
                         Bd * p.nP * (2.0 * TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) +
                         (p.nds ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
@@ -498,7 +493,6 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   if (const char* e = getenv("TBLUP_AHEAD")) c->ahead = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
-  if (const char* e = getenv("TBLUP_QMODE")) c->qmode = atoi(e) != 0;
   if (!panel) {
     *out = c.release();
     return 0;

@@ -264,9 +264,7 @@ struct CholArgs {
   uint64_t* dtr;            // diagonal launch: phase timestamps of workgroup 0 (TBLUP_WG_TRACE), else null
   const int16_t* kc;        // SNP form: off-diagonal system-tile counts (k_sys_tiles), else null
   double* part;             // [2][B][NT][128*128] off-diagonal partial sums K - sum_{L<J-1} (acc layout), slot J&1
-  double* Q;                // [B][36*256] L_{J+1,J} L_{J+1,J}^T (packed blocks) for the next diagonal tile
   int64_t B;                // individuals in the chunk
-  int qmode;                // diagonal J takes its last SYRK term from Q (made by tile (J, J-1))
 };
 
 // st: profiling only (phase stamps of one factorisation in diagonal workgroup 0), else null
@@ -787,24 +785,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   // launch's loads are HBM-bound and the SYRK at 2 waves per SIMD then runs after them.)
   const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
                                 : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
-  if (a.qmode && J > 0) {
-    // the last SYRK term was formed by the workgroup of tile (J, J-1) in the previous launch (Q):
-    // every lane subtracts it from exactly the 16-B pieces its own LDS-DMA brought in
-    const double* q = a.Q + b * (int64_t)NPACK * BLKD;
-    v2d qv[NPACK * BLKD / 2 / DTHR];
-#pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
-      const int chunk = (e * DW + w) * 64;
-      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
-      qv[e] = *reinterpret_cast<const v2d*>(q + 2 * (chunk + l));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {
-      v2d* tv = reinterpret_cast<v2d*>(Tp + 2 * ((e * DW + w) * 64 + l));
-      *tv = *tv - qv[e];
-    }
-  } else {
+  {
 #pragma unroll
     for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
       const int chunk = (e * DW + w) * 64;
@@ -982,8 +963,6 @@ __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
 //     1. acc -= sum_{L} L_JL L_IL^T over the L < J not summed yet   (acc = T^T, wave w: its 16 i)
 //     2. out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb]   (X = inv(L_JJ); acc is the B operand)
 //        -> Lt tile (I, J); w_I += L_IJ z_J
-//     3. (qmode, I = J+1) Q = L_{J+1,J} L_{J+1,J}^T on the 36 lower blocks: the next diagonal
-//        kernel's last SYRK term, off its chain
 //   P-unit (ahead), tile (I, J+1), I >= J+2, row blocks of slice rs: acc = K - sum_{L<J} (steps 0-1
 //     of launch J+1's T-unit, which continues the same MFMA chains: bit-identical results)
 //   D-unit, diagonal tile J+1, block slice: S = K - sum_{L<J} L_{J+1,L} L_{J+1,L}^T (packed blocks)
@@ -1173,19 +1152,6 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
       }
     }
   }
-
-
-  // 3. Q = L_{J+1,J} L_{J+1,J}^T (36 lower blocks) from the Lt tile just stored: this workgroup's
-  //    own stores, complete (vmcnt) and ordered before the reads by the barrier
-  if (a.qmode && I == J + 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    v4d q5[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) q5[i] = v4d{0.0, 0.0, 0.0, 0.0};
-    if (!(a.skip & 2)) syrk_lower8_32(Lout, 8, lds, q5);
-    store_syrk_blocks(a.Q + b * (int64_t)NPACK * BLKD, nullptr, q5, 0);
-  }
 }
 
 // K_JJ for every (individual, J) with the off-diagonal kernel's 8-wave int8 tile (A = B =
@@ -1262,29 +1228,23 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
   }
 }
 
-// Off-diagonal launch of column J (see OffPlan): per individual, its P-units (longest first),
-// D-units, then its T-units -- all of them contiguous in the XCD-remapped order, so one XCD's L2
-// serves the individual's Lt block rows -- and, column 0 of the kernel form only, the K_JJ
-// workgroups for J >= 2 at the end of the grid.
+// Off-diagonal launch of column J (see OffPlan).  The grid holds the unit classes longest first
+// -- every P-unit, then every D-unit, then every T-unit (a class's units dispatched after
+// another class's have started cannot hide behind them: with the D-units after the T-units of
+// their own individual, as one list per individual, the launches ran 9% longer) -- each class
+// XCD-remapped so that one XCD's L2 serves an individual's Lt block rows; and, column 0 of the
+// kernel form only, the K_JJ workgroups for J >= 2 at the end.
 __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) {
   __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
   __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
-  const int64_t U = p.units();
-  const int64_t n_units = a.B * U;
-  const int64_t bid = blockIdx.x;
+  const int64_t npu = (int64_t)p.nP * p.nrs;
+  const int64_t n_p = a.B * npu, n_d = a.B * p.nds, n_t = a.B * p.nI;
+  int64_t bid = blockIdx.x;
   WgTrace tr(a.wgt);
-  if (bid >= n_units) {   // column 0, kernel form: K_JJ for J >= 2
-    const int64_t lg = xcd_remap(bid - n_units, p.n_kd);
-    const int nJ = a.NT - 2;
-    diag_grm_tile(a, lg / nJ, 2 + (int)(lg % nJ), reinterpret_cast<uint8_t*>(lds), uj_sh);
-    tr.done(WGT_KJJ, a.J, 2 + (int)(lg % nJ), lg / nJ);
-    return;
-  }
-  const int64_t logical = xcd_remap(bid, n_units);
-  const int64_t b = logical / U;
-  int u = (int)(logical % U);
-  const int npu = p.nP * p.nrs;
-  if (u < npu) {
+  if (bid < n_p) {
+    const int64_t lg = xcd_remap(bid, n_p);
+    const int64_t b = lg / npu;
+    const int u = (int)(lg % npu);
     const int I = a.J + 2 + u / p.nrs, rs = u % p.nrs;
     switch (p.nrs) {
       case 1: part_unit<8>(a, b, I, rs, lds, uj_sh, ui_sh); break;
@@ -1294,16 +1254,29 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
     tr.done(WGT_PART, a.J, I, b);
     return;
   }
-  u -= npu;
-  if (u < p.nds) {
+  bid -= n_p;
+  if (bid < n_d) {
+    const int64_t lg = xcd_remap(bid, n_d);
+    const int64_t b = lg / p.nds;
+    const int u = (int)(lg % p.nds);
     syrk_partial8(a, b, a.J + 1, a.J, lds, p.nds == 1 ? 0 : 1 + u);
     tr.done(WGT_PREP, a.J, a.J + 1, b);
     return;
   }
-  u -= p.nds;
-  const int I = a.J + 1 + u;
-  tile_unit(a, b, I, p.ahead_cur, lds, uj_sh, ui_sh, zj_sh);
-  tr.done(WGT_TILE, a.J, I, b);
+  bid -= n_d;
+  if (bid < n_t) {
+    const int64_t lg = xcd_remap(bid, n_t);
+    const int64_t b = lg / p.nI;
+    const int I = a.J + 1 + (int)(lg % p.nI);
+    tile_unit(a, b, I, p.ahead_cur, lds, uj_sh, ui_sh, zj_sh);
+    tr.done(WGT_TILE, a.J, I, b);
+    return;
+  }
+  // column 0, kernel form: K_JJ for J >= 2
+  const int64_t lg = xcd_remap(bid - n_t, p.n_kd);
+  const int nJ = a.NT - 2;
+  diag_grm_tile(a, lg / nJ, 2 + (int)(lg % nJ), reinterpret_cast<uint8_t*>(lds), uj_sh);
+  tr.done(WGT_KJJ, a.J, 2 + (int)(lg % nJ), lg / nJ);
 }
 
 // ===========================================================================
@@ -1460,7 +1433,7 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
-             c.wgt, nullptr, c.kc, c.part, c.Q, c.B, c.qmode};
+             c.wgt, nullptr, c.kc, c.part, c.B};
   return a;
 }
 

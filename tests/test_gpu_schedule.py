@@ -1,9 +1,9 @@
-"""Cholesky schedule invariance: the classic column schedule, the ahead schedule (partial sums of
-the next column's tiles computed one launch early, in 1 / 2 / 4 row slices) and Q (the next
-diagonal's last SYRK term formed by tile (J+1, J)) redistribute the same MFMA chains over
-workgroups and launches, so fitness and EBVs must be bit-identical under every setting, for
-both system forms and for system sizes from 1 to 8+ tile columns; and equal to the oracle.
-(TBLUP_AHEAD / TBLUP_NRS / TBLUP_QMODE are read when a context is created.)"""
+"""Cholesky schedule invariance: the classic column schedule and the ahead schedule (partial sums
+of the next column's tiles computed one launch early, in 1 / 2 / 4 row slices, the diagonal
+target's in 1 / 2 block slices) redistribute the same MFMA chains over workgroups and launches,
+so fitness and EBVs must be bit-identical under every setting, for both system forms and for
+system sizes from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS are
+read when a context is created.)"""
 import os
 
 import numpy as np
@@ -14,12 +14,12 @@ from oracle import blup_oracle as O
 pytestmark = pytest.mark.gpu
 
 SETTINGS = [
-    {"TBLUP_AHEAD": "0", "TBLUP_QMODE": "0"},       # round-2 schedule
-    {"TBLUP_AHEAD": "0", "TBLUP_QMODE": "1"},
-    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "1", "TBLUP_QMODE": "1"},
-    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "2", "TBLUP_QMODE": "0"},
-    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "4", "TBLUP_QMODE": "1"},
-    {"TBLUP_AHEAD": "-1", "TBLUP_NRS": "0", "TBLUP_QMODE": "1"},   # the defaults
+    {"TBLUP_AHEAD": "0"},                           # the classic (round-2) schedule
+    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "1"},
+    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "2"},
+    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "4"},
+    {"TBLUP_AHEAD": "1", "TBLUP_NRS": "0"},
+    {"TBLUP_AHEAD": "-1", "TBLUP_NRS": "0"},        # the defaults
 ]
 
 

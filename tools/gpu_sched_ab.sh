@@ -14,10 +14,10 @@ run() {  # name pop env...
   tail -1 $O/ab_${name}_$TAG.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$name', d['value'], d['ms_per_step'], d['kernel_ms_per_step'], d['fitness_checksum'])"
 }
 for pop in 256 128 64 32; do
-  run p${pop}_classic $pop TBLUP_AHEAD=0 TBLUP_QMODE=0
-  run p${pop}_q $pop TBLUP_AHEAD=0 TBLUP_QMODE=1
-  run p${pop}_ahead_q $pop TBLUP_AHEAD=1 TBLUP_QMODE=1
+  run p${pop}_classic $pop TBLUP_AHEAD=0
+  run p${pop}_q $pop TBLUP_AHEAD=0
+  run p${pop}_ahead_q $pop TBLUP_AHEAD=1
 done
-run p256_ahead_q_nrs2 256 TBLUP_AHEAD=1 TBLUP_QMODE=1 TBLUP_NRS=2
-run p32_ahead_q_nrs2 32 TBLUP_AHEAD=1 TBLUP_QMODE=1 TBLUP_NRS=2
+run p256_ahead_q_nrs2 256 TBLUP_AHEAD=1 TBLUP_NRS=2
+run p32_ahead_q_nrs2 32 TBLUP_AHEAD=1 TBLUP_NRS=2
 echo ab done
