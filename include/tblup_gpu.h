@@ -131,6 +131,23 @@ int tblup_eval_batch_device(tblup_ctx* ctx, int split_id, const int64_t* d_idx,
                             double h2, int branch, double* d_fitness, double* d_ebv, void* stream);
 
 /*
+ * Every individual against each of n_splits registered splits (IntraGCVBlupParallelEvaluator's
+ * k folds, tblup/evaluator.py:509-537, whose fitness is the mean over folds; or any split set):
+ * fitness is n_splits x batch row-major (row f = split_ids[f]).  The splits' evaluations are
+ * enqueued back to back on one stream with one upload of the index lists and one
+ * synchronisation, instead of one tblup_eval_batch round trip per fold.  Same numbers as
+ * tblup_eval_batch per split, bit for bit.  Host pointers, synchronous.
+ */
+int tblup_eval_folds(tblup_ctx* ctx, const int* split_ids, int n_splits, const int64_t* idx, const int64_t* offsets,
+                     int64_t batch, double h2, int branch, double* fitness);
+
+/* Same on device-resident inputs / outputs (d_fitness: n_splits x batch), enqueued on `stream`
+ * (NULL = the context's stream) without synchronising; h_offsets as in tblup_eval_batch_device. */
+int tblup_eval_folds_device(tblup_ctx* ctx, const int* split_ids, int n_splits, const int64_t* d_idx,
+                            const int64_t* d_offsets, const int64_t* h_offsets, int64_t batch, double h2, int branch,
+                            double* d_fitness, void* stream);
+
+/*
  * RandomKeyIndividual / CoevolutionIndividual genome decode
  * (tblup/individual.py:154-156, `np.argsort(keys)[-int(length):]`): for each of
  * `batch` key rows of length d, the indices of its k_b = offsets[b+1]-offsets[b]

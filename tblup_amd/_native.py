@@ -39,6 +39,9 @@ SIGNATURES = {
     "tblup_eval_batch": (_c.c_int, [_P, _c.c_int, _I64P, _I64P, _c.c_int64, _c.c_double, _c.c_int, _DP, _DP]),
     "tblup_eval_batch_device": (_c.c_int, [_P, _c.c_int, _P, _P, _I64P, _c.c_int64, _c.c_double, _c.c_int, _P, _P,
                                            _P]),
+    "tblup_eval_folds": (_c.c_int, [_P, _I32P, _c.c_int, _I64P, _I64P, _c.c_int64, _c.c_double, _c.c_int, _DP]),
+    "tblup_eval_folds_device": (_c.c_int, [_P, _I32P, _c.c_int, _P, _P, _I64P, _c.c_int64, _c.c_double, _c.c_int,
+                                           _P, _P]),
     "tblup_set_profiling": (_c.c_int, [_P, _c.c_int]),
     "tblup_get_profile": (_c.c_int, [_P, _DP, _I64P, _DP, _DP]),
     "tblup_reset_profile": (_c.c_int, [_P]),

@@ -766,6 +766,116 @@ int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, co
                    nullptr);
 }
 
+// IntraGCV's k folds (evaluator.py:509-537) or any set of splits: every individual against every
+// split, enqueued back to back on one stream (the folds reuse one workspace in stream order), one
+// host round trip for the whole set instead of one per fold.
+static int validate_splits(tblup_ctx* c, const int* split_ids, int n_splits, std::vector<Split*>& sps) {
+  if (!split_ids || n_splits < 1) return fail(TBLUP_ERR_ARG, "need n_splits >= 1 split ids");
+  sps.resize(n_splits);
+  for (int f = 0; f < n_splits; ++f) {
+    sps[f] = find_split(c, split_ids[f]);
+    if (!sps[f]) return fail(TBLUP_ERR_ARG, "unknown split id " + std::to_string(split_ids[f]));
+  }
+  return 0;
+}
+
+int tblup_eval_folds_device(tblup_ctx* c, const int* split_ids, int n_splits, const int64_t* d_idx,
+                            const int64_t* d_offsets, const int64_t* h_offsets, int64_t batch, double h2, int branch,
+                            double* d_fitness, void* stream) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_batch(c, branch, h2, h_offsets, batch)) return rc;
+  std::vector<Split*> sps;
+  if (int rc = validate_splits(c, split_ids, n_splits, sps)) return rc;
+  if (batch == 0) return 0;
+  if (!d_idx || !d_offsets || !d_fitness) return fail(TBLUP_ERR_ARG, "null device pointers");
+  if (batch > 65535) return fail(TBLUP_ERR_ARG, "device batch limited to 65535 individuals per call");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  size_t need = 0;
+  for (int f = 0; f < n_splits; ++f) {
+    const EvalDims d = dims_of(c, *sps[f]);
+    need = std::max(need, chunk_bytes(c, d, choose_sys(c, d, h_offsets, batch, branch, c->form_pref), batch, 0, false));
+  }
+  if (need > c->ws.bytes) {
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (int rc = dev_alloc(c, c->ws, need)) return rc;
+  }
+  for (int f = 0; f < n_splits; ++f) {
+    const EvalDims d = dims_of(c, *sps[f]);
+    const SysDims sd = choose_sys(c, d, h_offsets, batch, branch, c->form_pref);
+    Carve cv{(char*)c->ws.p};
+    if (int rc = run_chunk(c, *sps[f], d, sd, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv,
+                           d_fitness + (int64_t)f * batch, nullptr, 0, nullptr, nullptr))
+      return rc;
+  }
+  return 0;
+}
+
+int tblup_eval_folds(tblup_ctx* c, const int* split_ids, int n_splits, const int64_t* idx, const int64_t* offsets,
+                     int64_t batch, double h2, int branch, double* fitness) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (int rc = validate_batch(c, branch, h2, offsets, batch)) return rc;
+  std::vector<Split*> sps;
+  if (int rc = validate_splits(c, split_ids, n_splits, sps)) return rc;
+  if (batch == 0) return 0;
+  if (!idx || !fitness) return fail(TBLUP_ERR_ARG, "null idx/fitness");
+  if (int rc = check_indices(c, idx, offsets[batch])) return rc;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<EvalDims> ds(n_splits);
+  for (int f = 0; f < n_splits; ++f) ds[f] = dims_of(c, *sps[f]);
+  auto fold_bytes = [&](const int64_t* off, int64_t B, int64_t sum_k) {
+    size_t m = 0;
+    for (int f = 0; f < n_splits; ++f)
+      m = std::max(m, chunk_bytes(c, ds[f], choose_sys(c, ds[f], off, B, branch, c->form_pref), B, sum_k, false));
+    return m + (size_t)n_splits * B * 8 + 256;
+  };
+  int64_t b0 = 0;
+  while (b0 < batch) {
+    int64_t b1 = b0, sum_k = 0;
+    std::vector<int64_t> hoff(1, 0);
+    while (b1 < batch) {
+      const int64_t k = offsets[b1 + 1] - offsets[b1];
+      hoff.push_back(hoff.back() + k);
+      if (b1 > b0 && fold_bytes(hoff.data(), b1 + 1 - b0, sum_k + k) > c->budget) {
+        hoff.pop_back();
+        break;
+      }
+      if (b1 - b0 >= 65535) {
+        hoff.pop_back();
+        break;
+      }
+      sum_k += k;
+      ++b1;
+    }
+    const int64_t B = b1 - b0;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (int rc = dev_alloc(c, c->ws, fold_bytes(hoff.data(), B, sum_k))) return rc;
+    Carve head{(char*)c->ws.p};
+    int64_t* d_idx = head.take<int64_t>((size_t)sum_k);
+    int64_t* d_off = head.take<int64_t>((size_t)B + 1);
+    double* d_fit = head.take<double>((size_t)n_splits * B);
+    HIPCHK(hipMemcpyAsync(d_idx, idx + offsets[b0], (size_t)sum_k * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_off, hoff.data(), (size_t)(B + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    for (int f = 0; f < n_splits; ++f) {
+      Carve cv = head;   // every fold reuses the same workspace after the inputs, in stream order
+      const SysDims sd = choose_sys(c, ds[f], hoff.data(), B, branch, c->form_pref);
+      if (int rc = run_chunk(c, *sps[f], ds[f], sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv,
+                             d_fit + (int64_t)f * B, nullptr, 0, nullptr, nullptr))
+        return rc;
+    }
+    for (int f = 0; f < n_splits; ++f)
+      HIPCHK(hipMemcpyAsync(fitness + (int64_t)f * batch + b0, d_fit + (int64_t)f * B, (size_t)B * 8,
+                            hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    b0 = b1;
+  }
+  if (c->profiling) return drain_events(c);
+  return 0;
+}
+
 static int validate_decode(int64_t batch, int64_t d, const int64_t* offsets) {
   if (batch < 0 || d < 1 || d > 0x7fffffff) return fail(TBLUP_ERR_ARG, "decode needs batch >= 0, 1 <= d < 2^31");
   if (batch > 0 && (!offsets || offsets[0] != 0)) return fail(TBLUP_ERR_ARG, "offsets must start at 0");

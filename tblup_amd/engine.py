@@ -59,7 +59,7 @@ def concat_genomes(genomes):
 class GpuBlupEngine:
     """Genotypes + phenotypes resident on one GPU; batched BLUP fitness."""
 
-    MAX_SPLITS = 16
+    MAX_SPLITS = 16   # a cached split is ~100 MB at config 2; IntraGCV holds k of them
 
     def __init__(self, data, labels, device=0, snp_major=False):
         """labels: (n,) phenotypes, or (n, t) for multi-trait evaluation (t <= 4, BASELINE
@@ -143,6 +143,32 @@ class GpuBlupEngine:
                 _native.BRANCH[branch], _ptr(fit, ctypes.c_double),
                 _ptr(ebv, ctypes.c_double) if return_ebv else None))
         return (fit, ebv) if return_ebv else fit
+
+    def evaluate_folds(self, genomes, splits, h2, branch="auto"):
+        """Every genome against each (train, valid) split in one call (tblup_eval_folds: the
+        splits' evaluations back to back on the GPU, one round trip): (n_splits, B) fitness, row f
+        bit-identical to evaluate(genomes, *splits[f]).  IntraGCV's k folds (evaluator.py:509-537)."""
+        self._settle()
+        sids = np.array([self.split_id(t, v) for t, v in splits], dtype=np.int32)
+        idx, offsets = concat_genomes(genomes)
+        B = len(genomes)
+        fit = np.empty((len(sids), B), dtype=np.float64)
+        if B:
+            _native.check("tblup_eval_folds", self._lib.tblup_eval_folds(
+                self._ctx, _ptr(sids, ctypes.c_int32), len(sids), _ptr(idx, ctypes.c_int64),
+                _ptr(offsets, ctypes.c_int64), B, float(h2), _native.BRANCH[branch], _ptr(fit, ctypes.c_double)))
+        return fit
+
+    def evaluate_folds_device(self, split_ids, d_idx_ptr, d_off_ptr, h_offsets, h2, d_fit_ptr, stream_ptr=None,
+                              branch="auto"):
+        """Asynchronous evaluate_folds on device-resident buffers (d_fit: n_splits x B)."""
+        self._settle()
+        sids = np.ascontiguousarray(split_ids, dtype=np.int32)
+        h_off = _as_int64(h_offsets)
+        _native.check("tblup_eval_folds_device", self._lib.tblup_eval_folds_device(
+            self._ctx, _ptr(sids, ctypes.c_int32), len(sids), ctypes.c_void_p(d_idx_ptr), ctypes.c_void_p(d_off_ptr),
+            _ptr(h_off, ctypes.c_int64), len(h_off) - 1, float(h2), _native.BRANCH[branch],
+            ctypes.c_void_p(d_fit_ptr), ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def evaluate_device(self, split_id, d_idx_ptr, d_off_ptr, h_offsets, h2, d_fit_ptr, d_ebv_ptr=None,
                         stream_ptr=None, branch="auto"):

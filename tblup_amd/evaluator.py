@@ -366,14 +366,28 @@ class InterGCVBlupParallelEvaluator(BlupParallelEvaluator):
 
 
 class IntraGCVBlupParallelEvaluator(InterGCVBlupParallelEvaluator):
-    """k-fold CV inside every fitness evaluation; fitness = mean over folds (evaluator.py:494-537)."""
+    """k-fold CV inside every fitness evaluation; fitness = mean over folds (evaluator.py:494-537).
+    The k folds' evaluations go to the GPU as one batch (GpuBlupEngine.evaluate_folds)."""
+
+    def _fold_fitness(self, genomes):
+        """(n_folds, len(genomes)) fitness; sharded across ranks like _fitness."""
+        splits = [self.train_validation_indices(k) for k in range(self.n_folds)]
+        folds = getattr(self.engine, "evaluate_folds", None)
+        if folds is None:   # engines without the batched entry (test stand-ins): one call per fold
+            return np.array([self._fitness(genomes, t, v) for t, v in splits])
+        rank, ws = world()
+        if ws == 1:
+            return folds(genomes, splits, self.h2)
+        lo, hi = shard_range(len(genomes), rank, ws)
+        local = folds(genomes[lo:hi], splits, self.h2)
+        dev = getattr(self.engine, "device", None)
+        return np.array([allgather_fitness(local[k], len(genomes), dev) for k in range(self.n_folds)])
 
     def _evaluate(self, population, to_evaluate, indices, generation):
         sums = {i: 0 for i in indices}
+        per_fold = self._fold_fitness(list(to_evaluate)) if to_evaluate else [[] for _ in range(self.n_folds)]
         for k in range(self.n_folds):
-            train, valid = self.train_validation_indices(k)
-            fits = self._fitness(list(to_evaluate), train, valid) if to_evaluate else []
-            for i, f in zip(indices, fits):
+            for i, f in zip(indices, per_fold[k]):
                 sums[i] += f
         for i, s in sums.items():
             population[i].set_fitness(s / self.n_folds)

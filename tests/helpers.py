@@ -123,6 +123,10 @@ class OracleEngine:
                 out.append(O.snp_blup(g, train, valid, self.data, self.labels, h2))
         return np.array(out, dtype=np.float64)
 
+    def evaluate_folds(self, genomes, splits, h2, branch="auto"):
+        """GpuBlupEngine.evaluate_folds: (n_splits, B), row f = evaluate(genomes, *splits[f])."""
+        return np.array([self.evaluate(genomes, t, v, h2, branch) for t, v in splits]).reshape(len(splits), -1)
+
     def close(self):
         pass
 

@@ -233,6 +233,35 @@ def test_config2_device_entry_repeats(config2):
     np.testing.assert_array_equal(d_fit.cpu().numpy()[:8], c["fit"][:8])
 
 
+def test_config2_folds_batched_equal_per_split(config2):
+    """tblup_eval_folds (IntraGCV's k folds, evaluator.py:509-537, in one call): each row equals
+    that split's own evaluation bit for bit, at config-2 size, host and device entries; an unknown
+    split id is an argument error."""
+    import torch
+    from tblup_amd import _native
+    from tblup_amd.engine import concat_genomes
+    from tblup_amd.evaluator import InterGCVBlupParallelEvaluator
+    c = config2
+    eng = c["eng"]
+    folds = InterGCVBlupParallelEvaluator.make_fold_indices(np.asarray(c["T"]), 5)
+    genomes = c["genomes"][:96]
+    got = eng.evaluate_folds(genomes, folds, 0.4)
+    assert got.shape == (5, 96)
+    for k, (t, v) in enumerate(folds):
+        np.testing.assert_array_equal(got[k], eng.evaluate(genomes, t, v, 0.4))
+    sids = [eng.split_id(t, v) for t, v in folds]
+    idx, off = concat_genomes(genomes)
+    d_idx, d_off = torch.from_numpy(idx).cuda(), torch.from_numpy(off).cuda()
+    d_fit = torch.full((5, 96), float("nan"), dtype=torch.float64, device="cuda")
+    s = torch.cuda.Stream()
+    eng.evaluate_folds_device(sids, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(),
+                              stream_ptr=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(d_fit.cpu().numpy(), got)
+    with pytest.raises(_native.TblupError, match="unknown split"):
+        eng.evaluate_folds_device([sids[0], 12345], d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr())
+
+
 def test_config2_gblup_branch_sample(config2):
     """k > n at config-2 size: the GBLUP branch (p over all n animals, no y centring)."""
     c = config2

@@ -1,10 +1,13 @@
 """IntraGCV (k = 5 folds inside every fitness evaluation, evaluator.py:494-537) against one
-fold's evaluation, through the drop-in classes on the GPU: config 1 (200 x 1000, k = 100,
-pop 32) and config 2 (2000 x 50k, k = 1000, pop 256).  Prints one JSON line per config with
-the median time of a fresh population's evaluate() for the plain evaluator (one split) and
-for IntraGCV (its k folds one after another on the evaluator's context).  A variant with the
-folds on k contexts driven from k host threads measured slower (config 1: 1.54 vs 0.91 ms,
-config 2: 35.8 vs 32.3 ms) and was dropped."""
+fold's evaluation on the GPU: config 1 (200 x 1000, k = 100, pop 32) and config 2 (2000 x 50k,
+k = 1000, pop 256).  Per config one JSON line with
+  * device-resident genomes (no host decode in the ratio): one fold's evaluate_device and the
+    k folds' evaluate_folds_device (tblup_eval_folds_device: the folds back to back on one
+    stream), medians over repeats, and their ratio;
+  * end to end through the drop-in classes: the median time of a fresh population's evaluate()
+    for the plain evaluator (one split) and for IntraGCV (one evaluate_folds call).
+(A variant with the folds on k contexts driven from k host threads measured slower in round 2:
+config 1 1.54 vs 0.91 ms, config 2 35.8 vs 32.3 ms.)"""
 import json
 import os
 import random
@@ -45,13 +48,50 @@ def main():
 
         def make_pop():
             return [RandomKeyIndividual(k, p, genome=rng.uniform(size=p)) for _ in range(pop)]
+        # device-resident genomes: one fold vs the k folds
+        import torch
+        from tblup_amd.engine import GpuBlupEngine, concat_genomes
+        eng = GpuBlupEngine(geno, np.load(pp), device=0)
+        random.seed(1)
+        np.random.seed(1)
+        ev0 = E.IntraGCVBlupParallelEvaluator(gp, pp, 0.4, n_folds=5)
+        splits = [ev0.train_validation_indices(f) for f in range(5)]
+        sids = [eng.split_id(t, v) for t, v in splits]
+        genomes = [np.argsort(rng.uniform(size=p))[-k:] for _ in range(pop)]
+        idx, off = concat_genomes(genomes)
+        d_idx, d_off = torch.from_numpy(idx).cuda(), torch.from_numpy(off).cuda()
+        d_fit = torch.empty((5, pop), dtype=torch.float64, device="cuda")
+        st = torch.cuda.current_stream()
+
+        def dev_ms(fn, reps=20):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            return float(np.median(ts)) * 1e3
+        one_dev = dev_ms(lambda: eng.evaluate_device(sids[0], d_idx.data_ptr(), d_off.data_ptr(), off, 0.4,
+                                                     d_fit.data_ptr(), stream_ptr=st.cuda_stream))
+        folds_dev = dev_ms(lambda: eng.evaluate_folds_device(sids, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4,
+                                                             d_fit.data_ptr(), stream_ptr=st.cuda_stream))
+        got = d_fit.cpu().numpy()
+        for f in (0, 4):   # the batched folds are each split's own evaluation
+            assert np.array_equal(got[f], eng.evaluate(genomes, *splits[f], 0.4))
+        eng.close()
         random.seed(1)
         np.random.seed(1)
         one = timed_evals(E.BlupParallelEvaluator(gp, pp, 0.4), make_pop, 5)
         random.seed(1)
         np.random.seed(1)
         intra = timed_evals(E.IntraGCVBlupParallelEvaluator(gp, pp, 0.4, n_folds=5), make_pop, 5)
-        print(json.dumps({"config": name, "pop": pop, "one_split_ms": round(one, 3), "intragcv_ms": round(intra, 3),
+        print(json.dumps({"config": name, "pop": pop,
+                          "device_one_fold_ms": round(one_dev, 3), "device_k_folds_ms": round(folds_dev, 3),
+                          "device_ratio": round(folds_dev / one_dev, 2),
+                          "one_split_ms": round(one, 3), "intragcv_ms": round(intra, 3),
                           "ratio": round(intra / one, 2)}), flush=True)
 
 
