@@ -256,7 +256,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
 
 // Form of the per-individual system for a batch.  The SNP-space (primal) form is what
 // sklearn's Ridge solves when k <= n_T (_ridge.py _solve_cholesky: X^T X + alpha I); it is
-// used when every individual takes the snp branch and it gives fewer 128-row tiles than the
+// used when every individual takes the snp branch and it gives no more 128-row tiles than the
 // kernel form.  pref: 0 auto, 1 force dual, 2 force primal (snp batches only).
 SysDims choose_sys(const tblup_ctx* c, const EvalDims& d, const int64_t* h_off, int64_t B, int branch, int pref);
 
@@ -285,7 +285,9 @@ SysDims choose_sys(const tblup_ctx* c, const EvalDims& d, const int64_t* h_off, 
     if (mode != 2) all_snp = false;
   }
   const int64_t kp = round_up(max_k, TILE);
-  const bool primal = all_snp && pref != 1 && (pref == 2 || kp < d.nTp);
+  // equal tile counts (kp == nTp, e.g. k = 1000 against a 1024-animal CV fold) also take the SNP
+  // form: its system tiles come from k_sys_tiles' FP4 counts instead of the in-tile int8 products
+  const bool primal = all_snp && pref != 1 && (pref == 2 || kp <= d.nTp);
   SysDims sd;
   if (primal) {
     sd.form = FORM_PRIMAL;

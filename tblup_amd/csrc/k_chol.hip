@@ -1241,9 +1241,6 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
   const int64_t n_p = a.B * npu, n_d = a.B * p.nds, n_t = a.B * p.nI;
   int64_t bid = blockIdx.x;
   WgTrace tr(a.wgt);
-  // experiment bits (TBLUP_DBG_SKIP): static priority for one half of the workgroup
-  if (((a.skip >> 20) & 1) && (threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
-  if (((a.skip >> 21) & 1) && (threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(1);
   if (bid < n_p) {
     const int64_t lg = xcd_remap(bid, n_p);
     const int64_t b = lg / npu;
