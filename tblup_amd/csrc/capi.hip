@@ -98,7 +98,7 @@ struct tblup_ctx {
   int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
   int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
   // Cholesky schedule (results are bit-identical under every setting; see OffPlan):
-  int ahead = -1;     // TBLUP_AHEAD: -1 auto (B < AHEAD_B), 0 never, 1 always
+  int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
 };
 
@@ -201,9 +201,10 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
     p.nI = 0;
     return p;
   }
-  // launch j computes the partial sums of column j + 1's tiles
+  // launch j computes the partial sums of column j + 1's tiles; auto: when the launch's P-units
+  // (B x (NT - 2 - j)) fit in AHEAD_SLOTS workgroup slots, i.e. run beside its T-units in one wave
   auto ahead_at = [&](int j) {
-    const bool on = ahead == 1 || (ahead < 0 && B < AHEAD_B);
+    const bool on = ahead == 1 || (ahead < 0 && B * (NT - 2 - j) < AHEAD_SLOTS);
     return on && j >= 1 && j + 2 <= NT - 1;
   };
   p.nP = ahead_at(J) ? NT - 2 - J : 0;

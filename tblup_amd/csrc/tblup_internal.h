@@ -177,10 +177,11 @@ struct OffPlan {
 };
 // Schedule policy (host, per chunk: a function of B and the system shape only, so the results
 // are bit-identical for any policy -- every accumulator keeps its MFMA chain):
-//   ahead: -1 auto (ahead when B < AHEAD_B: measured +14% at B = 32, even at 64-192, -5% at 256),
-//   0 never, 1 always; nrs: 0 auto (fill >= 2 units per CU
+//   ahead: -1 auto (launch j ahead when B * (NT - 2 - j) < AHEAD_SLOTS; measured at config 2 against
+//   the classic schedule: +14% at B = 32, +2.3% at B = 128, even at 256; a whole-chunk B < 64 rule
+//   and thresholds 512 / 1024 were slower at 128), 0 never, 1 always; nrs: 0 auto (fill >= 2 units per CU
 //   slot pair), else fixed 1 / 2 / 4; dual: no k_sys_tiles counts (int8 K in-tile: nrs = 1)
-constexpr int64_t AHEAD_B = 64;
+constexpr int64_t AHEAD_SLOTS = 256;
 OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs);
 inline int64_t offdiag_grid(const OffPlan& p, int64_t B) { return p.nI > 0 ? B * p.units() + p.n_kd : 0; }
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
