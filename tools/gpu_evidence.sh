@@ -7,8 +7,10 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-dev}
 O=gpurun_out
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/gputest_$TAG.log 2>&1
+if [ -z "$SKIP_TESTS" ]; then
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/gputest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/gputest_$TAG.log; tail -3 $O/gputest_$TAG.log; [ $rc -eq 0 ] || exit 1
+fi
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmcf_$TAG -o pmc --output-format csv -- $B > $O/pmcf_$TAG.log 2>&1 || { echo "pmc fetch failed"; tail -5 $O/pmcf_$TAG.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmcw_$TAG -o pmc --output-format csv -- $B > $O/pmcw_$TAG.log 2>&1 || { echo "pmc write failed"; tail -5 $O/pmcw_$TAG.log; exit 1; }
@@ -26,12 +28,17 @@ timeout -k 10 300 python tools/generation_bench.py 24 > $O/generation_$TAG.log 2
 tail -1 $O/generation_$TAG.log
 timeout -k 10 300 python tools/intracv_bench.py > $O/intracv_$TAG.log 2>&1 || { tail -20 $O/intracv_$TAG.log; exit 1; }
 grep config $O/intracv_$TAG.log
+timeout -k 10 300 python tools/knockout_bench.py > $O/knockout_$TAG.log 2>&1 || { tail -20 $O/knockout_$TAG.log; exit 1; }
+tail -1 $O/knockout_$TAG.log
 timeout -k 10 200 python tools/wg_trace.py $O/wg_trace_$TAG.npy > $O/wg_trace_$TAG.txt 2>&1 || { tail -20 $O/wg_trace_$TAG.txt; exit 1; }
 timeout -k 10 200 python tools/wg_trace.py $O/wg_trace128_$TAG.npy --pop 128 > $O/wg_trace128_$TAG.txt 2>&1 || { tail -20 $O/wg_trace128_$TAG.txt; exit 1; }
 timeout -k 10 400 python bench.py --config config4 --steps 5 --warmup 2 > $O/bench_config4_$TAG.log 2> $O/bench_config4_$TAG.err || { tail -20 $O/bench_config4_$TAG.err; exit 1; }
 timeout -k 10 300 python bench.py --config config5 --steps 10 --warmup 3 > $O/bench_config5_$TAG.log 2> $O/bench_config5_$TAG.err || { tail -20 $O/bench_config5_$TAG.err; exit 1; }
-timeout -k 10 300 python bench.py --pop 128 --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_pop128_$TAG.log 2> $O/bench_pop128_$TAG.err || { tail -20 $O/bench_pop128_$TAG.err; exit 1; }
-for c in config4 config5 pop128; do tail -1 $O/bench_${c}_$TAG.log | cut -c1-200; done
+for P in 32 64 128; do
+timeout -k 10 300 python bench.py --pop $P --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_pop${P}_$TAG.log 2> $O/bench_pop${P}_$TAG.err || { tail -20 $O/bench_pop${P}_$TAG.err; exit 1; }
+done
+timeout -k 10 300 python bench.py --config config3 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_config3_$TAG.log 2> $O/bench_config3_$TAG.err || { tail -20 $O/bench_config3_$TAG.err; exit 1; }
+for c in config3 config4 config5 pop32 pop64 pop128; do tail -1 $O/bench_${c}_$TAG.log | cut -c1-200; done
 timeout -k 10 100 ./tools/mfma_peak > $O/mfma_peak_$TAG.json 2>&1 || exit 1
 timeout -k 10 100 ./tools/fp4_probe > $O/fp4_probe_$TAG.json 2>&1 || exit 1
 echo evidence done
