@@ -8,11 +8,14 @@ all relative to the current mask: every candidate before the first accepted one
 was evaluated against exactly the mask the sequential walk would have used, so
 those decisions stand; the first acceptance changes the mask, and the walk
 resumes after it with a fresh batch.  Decisions are therefore identical to the
-sequential walk on the same fitness values (acceptances are rare, so a k = 1000
-walk costs ~k/window + #accepted batched calls instead of k).
+sequential walk on the same fitness values.  Acceptances are NOT rare (about half of
+the knock-outs from a config-2 population's best, `profiles/r03a_knockout.json`), so
+the default speculates over a decision tree instead of a line (knockout_walk).
 """
-import numpy as np
+import heapq
 from copy import deepcopy
+
+import numpy as np
 
 from .evaluator import BlupParallelEvaluator
 
@@ -32,31 +35,85 @@ class LocalSearch:
         raise NotImplementedError()
 
 
-def knockout_walk(genome, best_fitness, evaluate_batch, window=256):
+def knockout_walk(genome, best_fitness, evaluate_batch, window=256, tree=True, latency=130.0):
     """The greedy knockout walk of local.py:62-76 with speculative batches.
 
     evaluate_batch(list of index arrays) -> fitness array.  Returns (mask, best_fitness,
-    n_batches)."""
+    n_batches).
+
+    tree=False: linear windows -- the next `window` knock-outs against the current mask; the
+    walk resumes after the first acceptance.
+    tree=True (default): decision-tree speculation.  A node is a path of decisions for the next
+    positions (each knock-out accepted or rejected) plus the candidate after it; the batch holds
+    the most probable nodes (acceptance rate p estimated from the walk so far, node probability
+    p^accepted (1-p)^rejected along its path), and the walk then follows the actual decisions
+    through the evaluated tree -- every node on the followed path was evaluated against exactly
+    the mask and best fitness the sequential walk has there, so the decisions are the
+    sequential walk's.  The batch size B <= window maximises the expected decisions resolved
+    (the sum of the selected nodes' probabilities) per batch cost `latency + B` (a batch costs a
+    fixed latency of about `latency` individuals' throughput: config 2 on one MI355X, B = 1
+    0.86 ms, B = 256 2.5 ms).  With p = 0.5 a batch of 32-64 resolves 5-6 decisions where a
+    linear window resolves 2."""
     genome = np.asarray(genome)
-    mask = np.ones(len(genome), dtype=bool)
+    n = len(genome)
+    mask = np.ones(n, dtype=bool)
     i, n_batches = 0, 0
-    while i < len(genome):
-        cand = list(range(i, min(len(genome), i + window)))
+    if not tree:
+        while i < n:
+            cand = list(range(i, min(n, i + window)))
+            subsets = []
+            for j in cand:
+                m = mask.copy()
+                m[j] = False
+                subsets.append(genome[m])
+            fits = np.asarray(evaluate_batch(subsets), dtype=np.float64)
+            n_batches += 1
+            nxt = cand[-1] + 1
+            for j, f in zip(cand, fits):
+                if f > best_fitness:        # local.py:69-71: keep the index masked
+                    best_fitness = f
+                    mask[j] = False
+                    nxt = j + 1             # later candidates assumed the old mask: re-evaluate them
+                    break
+            i = nxt
+        return mask, best_fitness, n_batches
+    accepted = decided = 0
+    while i < n:
+        p = (accepted + 1.0) / (decided + 2.0)
+        # best-first expansion of the decision tree rooted at position i
+        heap, order, tick = [(-1.0, 0, ())], [], 1
+        while heap and len(order) < window:
+            negp, _, path = heapq.heappop(heap)
+            order.append((path, -negp))
+            if i + len(path) + 1 < n:
+                heapq.heappush(heap, (negp * p, tick, path + (True,)))
+                heapq.heappush(heap, (negp * (1.0 - p), tick + 1, path + (False,)))
+                tick += 2
+        gain = np.cumsum([q for _, q in order])
+        B = int(np.argmax(gain / (latency + np.arange(1, len(order) + 1)))) + 1
+        nodes = {}
         subsets = []
-        for j in cand:
+        for path, _ in order[:B]:
             m = mask.copy()
-            m[j] = False
+            for d, acc in enumerate(path):
+                if acc:
+                    m[i + d] = False
+            m[i + len(path)] = False
+            nodes[path] = len(subsets)
             subsets.append(genome[m])
         fits = np.asarray(evaluate_batch(subsets), dtype=np.float64)
         n_batches += 1
-        nxt = cand[-1] + 1
-        for j, f in zip(cand, fits):
-            if f > best_fitness:        # local.py:69-71: keep the index masked
+        path = ()
+        while i < n and path in nodes:
+            f = fits[nodes[path]]
+            acc = bool(f > best_fitness)    # local.py:69-71
+            if acc:
                 best_fitness = f
-                mask[j] = False
-                nxt = j + 1             # later candidates assumed the old mask: re-evaluate them
-                break
-        i = nxt
+                mask[i] = False
+                accepted += 1
+            decided += 1
+            path += (acc,)
+            i += 1
     return mask, best_fitness, n_batches
 
 

@@ -2,8 +2,8 @@
 eigendecomposition / Schur-complement downdate route it could be replaced by.
 
 The walk starts from the best of a pop-256 population (bench.py's synthetic workload) and runs
-`tblup_amd.local.knockout_walk` with speculative windows of 64 / 128 / 256 candidates (the
-decisions are identical for every window).  Printed as one JSON line:
+`tblup_amd.local.knockout_walk` with decision-tree speculation (the default) and with linear
+windows of 64 / 256 candidates (the decisions are identical for every mode).  Printed as one JSON line:
   * per window: wall ms of the whole walk, batches, accepted knock-outs;
   * one B = 1 evaluation (the sequential walk's per-candidate cost: k of them);
   * the downdate route's fixed costs for ONE base system (k x k, fp64): the eigendecomposition
@@ -43,15 +43,20 @@ def main():
         out["one_eval_b1_ms"] = round(float(np.median(ts)) * 1e3, 3)
         out["sequential_walk_est_ms"] = round(out["one_eval_b1_ms"] * len(best), 1)
         ref = None
-        for w in (64, 128, 256):
-            knockout_walk(best, best_fit, lambda s: eng.evaluate(s, T, V, h2), w)   # warm
+        for name, w, tree in (("tree_w256", 256, True), ("linear_w64", 64, False), ("linear_w256", 256, False)):
+            sizes = []
+
+            def batch(s):
+                sizes.append(len(s))
+                return eng.evaluate(s, T, V, h2)
             t0 = time.perf_counter()
-            mask, bf, nb = knockout_walk(best, best_fit, lambda s: eng.evaluate(s, T, V, h2), w)
+            mask, bf, nb = knockout_walk(best, best_fit, batch, w, tree=tree)
             dt = time.perf_counter() - t0
             if ref is None:
                 ref = (mask, bf)
             assert np.array_equal(mask, ref[0]) and bf == ref[1]
-            out[f"walk_w{w}"] = {"ms": round(dt * 1e3, 1), "batches": nb, "accepted": int((~mask).sum())}
+            out[f"walk_{name}"] = {"ms": round(dt * 1e3, 1), "batches": nb, "accepted": int((~mask).sum()),
+                                   "mean_batch": round(float(np.mean(sizes)), 1)}
         out["fitness_before_after"] = [best_fit, float(ref[1])]
     # downdate route: one eigendecomposition of the k x k system (SNP form, train-centred)
     Xc = geno[np.ix_(T, best)].astype(np.float64)
