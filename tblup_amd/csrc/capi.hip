@@ -100,6 +100,10 @@ struct tblup_ctx {
   // Cholesky schedule (results are bit-identical under every setting; see OffPlan):
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
+  int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
+  int solve_chain = 0;   // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain)
+  DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
+  int32_t chain_seq = 0; // flag value of the last chained solve
 };
 
 namespace {
@@ -249,6 +253,12 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
   add(any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
+  if (sd.form == FORM_PRIMAL && c->solve_chain) {               // chained solve: beta, c_{J->I}, EBV shares
+    add((size_t)B * d.nt * sd.ns * 8);
+    add((size_t)B * sd.NT * sd.NT * d.nt * TILE * 8);
+    add((size_t)B * sd.NT * d.nt * d.nV * 8);
+    add((size_t)B * sd.NT * d.nt * 8);
+  }
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nt * d.nV * 8 : 0);              // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
@@ -371,6 +381,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     int64_t nwg = 0;
     for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
+    if (sd.form == FORM_PRIMAL && c->solve_chain) nwg += B * sd.NT * (sd.NT + 1) / 2;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
     wgt = (uint64_t*)c->wgt.p;
@@ -435,7 +446,31 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const double fs = (double)B * (2.0 * (double)sd.ns * sd.ns / 2.0 + 2.0 * kbar * (double)(d.nT + d.nV) + 10.0 * d.nV);
   const double bs = (double)B * (((double)sd.ns * sd.ns / 2.0 + (double)sd.NT * TILE * TILE) * 8.0 +
                                  kbar * (double)(d.nT + d.nV));
-  rc = timed(c, s, KC_SOLVE, fs, bs, [&] { return launch_solve(cl, d_fit, d_ebv, s); });
+  SolveChain ch{};
+  const SolveChain* chp = nullptr;
+  if (sd.form == FORM_PRIMAL && c->solve_chain) {
+    const size_t fbytes = ((size_t)B * chain_flags(sd.NT) + 1) * 4;
+    if (c->chain.bytes < fbytes || c->chain_seq >= INT32_MAX - 1) {
+      HIPCHK(hipStreamSynchronize(s));   // the flags may still be read by an earlier chained solve
+      if (int rc2 = dev_alloc(c, c->chain, fbytes)) return rc2;
+      HIPCHK(hipMemsetAsync(c->chain.p, 0, c->chain.bytes, s));
+      c->chain_seq = 0;
+    }
+    ch.flags = (int32_t*)c->chain.p;
+    ch.err = ch.flags + (c->chain.bytes / 4 - 1);
+    ch.beta = cv.take<double>((size_t)B * d.nt * sd.ns);
+    ch.cpart = cv.take<double>((size_t)B * sd.NT * sd.NT * d.nt * TILE);
+    ch.epart = cv.take<double>((size_t)B * sd.NT * d.nt * d.nV);
+    ch.mbpart = cv.take<double>((size_t)B * sd.NT * d.nt);
+    ch.seq = ++c->chain_seq;
+    ch.mode = c->chain_sync;
+    chp = &ch;
+    if (wgt) {
+      cl.wgt = wgt + c->wgt_used * WGT_REC;
+      c->wgt_used += B * sd.NT * (sd.NT + 1) / 2;
+    }
+  }
+  rc = timed(c, s, KC_SOLVE, fs, bs, [&] { return launch_solve(cl, chp, d_fit, d_ebv, s); });
   return rc;
 }
 
@@ -495,6 +530,8 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   if (const char* e = getenv("TBLUP_AHEAD")) c->ahead = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_SOLVE_CHAIN")) c->solve_chain = atoi(e) != 0;
+  if (const char* e = getenv("TBLUP_CHAIN_SYNC")) c->chain_sync = atoi(e);
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
   if (!panel) {
     *out = c.release();
@@ -543,6 +580,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   c->scratch.release();
   c->ws.release();
   c->wgt.release();
+  c->chain.release();
   c->dec_keys.release();
   c->dec_idx.release();
   c->de_polys.release();

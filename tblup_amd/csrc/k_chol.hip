@@ -1282,11 +1282,11 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
 // ===========================================================================
 // SNP form: every system tile (I >= J) of the batch in one launch, before the column loop:
 // C = A B^T over the n_T train animals on FP4 MFMA (16x16x128, e2m1 operands, fp32 accumulate),
-// 2-bit packed split rows read in place.  Genotype g is the e2m1 nibble 2g (0, 1.0, 2.0), so a
-// packed dword's even fields become nibbles by (x << 1) & 0x66666666 and its odd fields by
-// (x >> 1) & 0x66666666 -- 4 VALU ops per 16 animals into 4 operand dwords (the int8 form spent 7
-// per 16 animals) -- and the counts (<= 4 n_T < 2^24) accumulate exactly in fp32 at twice the
-// int8 rate.  The animals' order inside k is the same for A and B, so A B^T is unchanged.
+// 2-bit packed split rows read in place.  Genotype code g read as an e2m1 nibble is g / 2 (0, 0.5,
+// 1.0), so a packed dword's even fields become nibbles by x & 0x33333333 and its odd fields by
+// (x >> 2) & 0x33333333 -- 3 VALU ops per 16 animals into 2 operand dwords (the int8 form spent 7
+// per 16 animals) -- and both operands carry the E8M0 scale 2.0; the counts (<= 4 n_T < 2^24)
+// accumulate exactly in fp32 at twice the int8 rate.  The animals' order inside k is the same for A and B, so A B^T is unchanged.
 // 4 waves per workgroup; wave (qr, qc) computes a 64 x 64 quadrant = 4 x 4 blocks; 256-animal
 // stages through a 3-deep LDS-DMA ring (48 KiB, three workgroups per CU).  A rows are read
 // through pi(rho) so the counts land in the f64 accumulator layout.  Off-diagonal tiles store
@@ -1300,11 +1300,17 @@ constexpr int STW = 4;   // waves per system-tile workgroup
 __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
                                        int l);
 
-// two packed dwords (32 animals) -> one fp4 MFMA operand (even fields, odd fields of each)
-__device__ __forceinline__ v8i fp4_operand(uint32_t x0, uint32_t x1) {
-  constexpr uint32_t M = 0x66666666u;
-  return v8i{(int)((x0 << 1) & M), (int)((x0 >> 1) & M), (int)((x1 << 1) & M), (int)((x1 >> 1) & M), 0, 0, 0, 0};
+// two packed dwords (32 animals) -> one fp4 MFMA operand (even fields, odd fields of each): the
+// 2-bit code g lands in the low half of a nibble, e2m1 value g / 2 (0, 0.5 subnormal, 1.0), and
+// the E8M0 operand scales 2.0 (128) restore g -- 3 VALU ops per packed dword instead of 4
+__device__ __forceinline__ v4i fp4_operand(uint32_t x0, uint32_t x1) {
+  constexpr uint32_t M = 0x33333333u;
+  return v4i{(int)(x0 & M), (int)((x0 >> 2) & M), (int)(x1 & M), (int)((x1 >> 2) & M)};
 }
+// the scaled f8f6f4 MFMA with fp4 operands in 4 VGPRs each (the clang builtin types them as 8 VGPRs,
+// the upper half unused by fp4 -- 32 more VGPRs and a zeroing move per operand)
+__device__ v4f mfma_fp4_16x16x128(v4i a, v4i b, v4f c, int cbsz, int blgp, int opsel_a, int scale_a, int opsel_b,
+                                  int scale_b) __asm("llvm.amdgcn.mfma.scale.f32.16x16x128.f8f6f4.v4i32.v4i32");
 #define sys_diag_epilogue sys_diag_epilogue_impl
 
 __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* kc, int ntri) {
@@ -1357,7 +1363,7 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
     }
     __builtin_amdgcn_s_barrier();
     if (st + D - 1 < nst) issue(st + D - 1);
-    if (compute) {
+    if (compute && !(a.skip & (1 << 18))) {
       const uint8_t* As = lds + (int)(st % D) * 2 * TB;
       const uint8_t* Bs = As + TB;
       const bool ztail = (st == nst - 1 && tail_ch != 0 && ch >= tail_ch);   // past the training animals
@@ -1370,7 +1376,7 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        v8i av[4], bv[4];
+        v4i av[4], bv[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           av[m] = s2 == 0 ? fp4_operand(aq[m].x, aq[m].y) : fp4_operand(aq[m].z, aq[m].w);
@@ -1379,12 +1385,12 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int n = 0; n < 4; ++n)   // cbsz = blgp = 4: A, B in fp4; E8M0 scales 127 = 1.0
-            cnt[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av[m], bv[n], cnt[m][n], 4, 4, 0, 127, 0, 127);
+          for (int n = 0; n < 4; ++n)   // cbsz = blgp = 4: A, B in fp4; E8M0 scales 128 = 2.0
+            cnt[m][n] = mfma_fp4_16x16x128(av[m], bv[n], cnt[m][n], 4, 4, 0, 128, 0, 128);
       }
     }
   }
-  if (compute && I != J) {
+  if (compute && I != J && !(a.skip & (1 << 16))) {
     int16_t* kt = kc + ((b * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE;
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -1396,7 +1402,7 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
                              (int)((uint32_t)((int)c[2] & 0xffff) | ((uint32_t)(int)c[3] << 16))};
         *reinterpret_cast<int2*>(kt + ((ib * 8 + cb) * 64 + l) * 4) = packed;
       }
-  } else if (compute) {
+  } else if (compute && I == J && !(a.skip & (1 << 17))) {
     sys_diag_epilogue(a, cnt, b, J, qr, qc, l);
   }
   tr.done(WGT_SYS, J, I, b);
@@ -1410,6 +1416,15 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
   const int64_t nrow = (int64_t)sc[SC_NROW];
   const double* ub = a.u + b * a.prow + j0;
   double* Kd = a.Kd + (b * a.NT + J) * (int64_t)NPACK * BLKD;
+  // every centring sum this lane needs, loaded before the first store (Kd and u are both double
+  // pointers: loads interleaved with the stores were issued one after another, ~47 us a launch)
+  double ur[4][4], uc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ur[m][r] = ub[16 * (4 * qr + m) + (l >> 4) + 4 * r];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) uc[n] = ub[16 * (4 * qc + n) + (l & 15)];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -1418,12 +1433,11 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
       if (cb < ib) continue;
       const int il = 16 * ib + (l & 15);
       const int64_t gj = j0 + il;
-      const double uj = ub[il];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * cb + (l >> 4) + 4 * r;
         const int64_t gi = j0 + cl;
-        const double kv = grm_value((int32_t)cnt[m][n][r], ub[cl], uj, sa_, cN, invd, sm);
+        const double kv = grm_value((int32_t)cnt[m][n][r], ur[m][r], uc[n], sa_, cN, invd, sm);
         const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
         Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
       }

@@ -17,6 +17,7 @@ namespace {
 
 constexpr int NTH = 1024;
 
+template <int NTH_ = NTH>
 __device__ __forceinline__ double block_sum(double v, double* red) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
 #pragma unroll
@@ -26,10 +27,11 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   __syncthreads();
   double s = 0.0;
 #pragma unroll
-  for (int i = 0; i < NTH / 64; ++i) s += red[i];
+  for (int i = 0; i < NTH_ / 64; ++i) s += red[i];
   return s;
 }
 
+template <int NTH_ = NTH>
 __device__ __forceinline__ double block_max(double v, double* red) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
 #pragma unroll
@@ -39,44 +41,45 @@ __device__ __forceinline__ double block_max(double v, double* red) {
   __syncthreads();
   double s = red[0];
 #pragma unroll
-  for (int i = 1; i < NTH / 64; ++i) s = fmax(s, red[i]);
+  for (int i = 1; i < NTH_ / 64; ++i) s = fmax(s, red[i]);
   return s;
 }
 
 }  // namespace
 
+template <int NTH_ = NTH>
 __device__ __forceinline__ double pearson_abs(const double* e, const double* yV, int64_t nV, double* red) {
   const int t = threadIdx.x;
   const double yb = yV[0], eb = e[0];
   double sx = 0.0, sy = 0.0, ncx = 0.0, ncy = 0.0;
-  for (int64_t v = t; v < nV; v += NTH) {
+  for (int64_t v = t; v < nV; v += NTH_) {
     sx += e[v];
     sy += yV[v];
     ncx += (e[v] != eb) ? 1.0 : 0.0;
     ncy += (yV[v] != yb) ? 1.0 : 0.0;
   }
-  const double mx = block_sum(sx, red) / (double)nV;
-  const double my = block_sum(sy, red) / (double)nV;
-  const double nonconst_x = block_sum(ncx, red);
-  const double nonconst_y = block_sum(ncy, red);
+  const double mx = block_sum<NTH_>(sx, red) / (double)nV;
+  const double my = block_sum<NTH_>(sy, red) / (double)nV;
+  const double nonconst_x = block_sum<NTH_>(ncx, red);
+  const double nonconst_y = block_sum<NTH_>(ncy, red);
   double ax = 0.0, ay = 0.0;
-  for (int64_t v = t; v < nV; v += NTH) {
+  for (int64_t v = t; v < nV; v += NTH_) {
     ax = fmax(ax, fabs(e[v] - mx));
     ay = fmax(ay, fabs(yV[v] - my));
   }
-  const double xmax = block_max(ax, red);
-  const double ymax = block_max(ay, red);
+  const double xmax = block_max<NTH_>(ax, red);
+  const double ymax = block_max<NTH_>(ay, red);
   double qx = 0.0, qy = 0.0;
-  for (int64_t v = t; v < nV; v += NTH) {
+  for (int64_t v = t; v < nV; v += NTH_) {
     const double a = (e[v] - mx) / xmax, c = (yV[v] - my) / ymax;
     qx += a * a;
     qy += c * c;
   }
-  const double nx = xmax * sqrt(block_sum(qx, red));
-  const double ny = ymax * sqrt(block_sum(qy, red));
+  const double nx = xmax * sqrt(block_sum<NTH_>(qx, red));
+  const double ny = ymax * sqrt(block_sum<NTH_>(qy, red));
   double rr = 0.0;
-  for (int64_t v = t; v < nV; v += NTH) rr += ((e[v] - mx) / nx) * ((yV[v] - my) / ny);
-  double r = block_sum(rr, red);
+  for (int64_t v = t; v < nV; v += NTH_) rr += ((e[v] - mx) / nx) * ((yV[v] - my) / ny);
+  double r = block_sum<NTH_>(rr, red);
   if (r == r) r = fmin(fmax(r, -1.0), 1.0);  // np.clip keeps NaN (fmin/fmax would drop it)
   if (nonconst_x == 0.0 || nonconst_y == 0.0) r = __builtin_nan("");
   if (nV == 2) r = rint(r);
@@ -309,7 +312,316 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   if (t == 0) fit[b] = sc[SC_BAD] != 0.0 ? __builtin_nan("") : (nt == 1) ? fsum : fsum / (double)nt;
 }
 
-hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s) {
+
+// ===========================================================================
+// Chained back substitution (SNP form): an individual's solve spread over the chip.
+//   F(b, J)     block row J: v = z_J - sum_{K > J} c_{K->J} (K ascending), beta_J = X_J^T v
+//               (X_J's rows prefetched), beta_J published; then block J's share of the
+//               prediction, sum_{a in J} x_va beta_a; F(b, 0) finally adds the shares (J
+//               ascending) and forms the fitness
+//   T(b, J, I)  tile (J, I), I < J: c_{J->I} = L_JI^T beta_J, the tile in registers before
+//               beta_J arrives
+// The one-workgroup-per-individual k_solve streams an individual's 4.7 MB (config 2) through one
+// CU at ~30 GB/s and waits out the block-row chain on top; here every tile is read by its own
+// workgroup and only the hand-offs stay on the chain.
+// Grid order: for J = NT-1 .. 0: F(., J), then T(., J, I < J).  A unit waits only on units with
+// smaller block ids (F(b, J) on T(b, K > J, J), T(b, J, I) on F(b, J), F(b, 0) on F(b, J > 0)),
+// and each XCD dispatches its share in block-id order, so the waits drain: the waiting unit with
+// the smallest id waits on units that are resident and not waiting.  Waits are bounded
+// (SPIN_MAX polls; one expired wait makes every later wait give up at once).  Every sum has a
+// fixed order, so the results do not depend on B, the timing or the grid.
+// ===========================================================================
+constexpr int CTH = 1024;   // single-trait: <= 64 VGPRs, two units (32 waves) per CU
+constexpr int SPIN_MAX = 1 << 20;
+enum { WGT_SROW = 7, WGT_STILE = 8 };
+
+// profiling only (TBLUP_WG_TRACE): {start, end, kind << 56 | I << 40 | b, J | (first wait done - start) << 16}
+struct ChainTrace {
+  uint64_t* rec = nullptr;
+  uint64_t t0 = 0, tw = 0;
+  __device__ explicit ChainTrace(uint64_t* base) {
+    if (base) {
+      rec = base + (int64_t)blockIdx.x * WGT_REC;
+      t0 = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __device__ void waited() {
+    if (rec && tw == 0) tw = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ void done(int kind, int J, int I, int64_t b) {
+    if (!rec) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      rec[0] = t0;
+      rec[1] = __builtin_amdgcn_s_memrealtime();
+      rec[2] = ((uint64_t)kind << 56) | ((uint64_t)I << 40) | (uint64_t)b;
+      rec[3] = (uint64_t)J | ((tw ? tw - t0 : 0) << 16);
+    }
+  }
+};
+
+__device__ __forceinline__ int32_t* flag_beta(const SolveChain& ch, int64_t b, int NT, int J) {
+  return ch.flags + b * chain_flags(NT) + J;
+}
+__device__ __forceinline__ int32_t* flag_part(const SolveChain& ch, int64_t b, int NT, int I, int J) {
+  return ch.flags + b * chain_flags(NT) + NT + I * NT + J;
+}
+__device__ __forceinline__ int32_t* flag_e(const SolveChain& ch, int64_t b, int NT, int J) {
+  return ch.flags + b * chain_flags(NT) + NT + NT * NT + J;
+}
+
+// Exchange through coherent (sc1) accesses: the producer stores its data and, once every wave's
+// stores have completed (s_waitcnt vmcnt(0) + barrier), the flag; the consumer polls the flag
+// and reads the data with sc1 loads.  No acquire/release fences: on gfx950 those are an L2
+// invalidate (buffer_inv sc1) per poll and an L2 write-back (buffer_wbl2 sc1) per publish, which
+// measured 25 us per hand-off and slowed every other workgroup of the XCD.
+// mode (TBLUP_CHAIN_SYNC): 0 = this, 1 = acquire/release atomics on the flag (reference).
+template <typename T>
+__device__ __forceinline__ T cload(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void cstore(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The whole workgroup waits until *f == seq (one lane polls).  False: gave up.
+__device__ bool chain_wait(const int32_t* f, int32_t seq, int32_t* err, int* sh, int mode) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    for (int it = 0;; ++it) {
+      const int32_t v = mode == 1 ? __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : cload(f);
+      if (v == seq) break;
+      if (it >= SPIN_MAX || cload(err) != 0) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) cstore(err, 1);
+    *sh = ok;
+  }
+  __syncthreads();
+  const int ok = *sh;
+  __syncthreads();
+  return ok != 0;
+}
+
+// every wave's stores completed, then the flag
+__device__ __forceinline__ void chain_publish(int32_t* f, int32_t seq, int mode) {
+  if (mode == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (mode == 1)
+      __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      cstore(f, seq);
+  }
+}
+
+template <int NTR>
+__device__ void chain_tile(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, int I, double (*bsh)[TILE],
+                           int* sh, ChainTrace& tr_) {
+  const int t = threadIdx.x, rc = t >> 3, qq = t & 7;
+  const int NT = c.sd.NT;
+  const int64_t ns = c.sd.ns;
+  // (L_JI^T beta_J)[rc] = sum_r Lt_(J,I)[rc][r] beta_J[r]: 8 threads per row, 16 r each
+  const double* row = c.L + ((b * NT + J) * (int64_t)NT + I) * TILE * TILE + rc * TILE + 16 * qq;
+  v2d x[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = *reinterpret_cast<const v2d*>(row + 2 * e);
+  if (!chain_wait(flag_beta(ch, b, NT, J), ch.seq, ch.err, sh, ch.mode)) return;
+  tr_.waited();
+  for (int i = t; i < NTR * TILE; i += CTH) bsh[i / TILE][i % TILE] = cload(ch.beta + (b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE);
+  __syncthreads();
+  double s[NTR];
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) s[tr] = 0.0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr) s[tr] += x[e][0] * bsh[tr][16 * qq + 2 * e] + x[e][1] * bsh[tr][16 * qq + 2 * e + 1];
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) {
+    s[tr] += __shfl_xor(s[tr], 1);
+    s[tr] += __shfl_xor(s[tr], 2);
+    s[tr] += __shfl_xor(s[tr], 4);
+    if (qq == 0) cstore(ch.cpart + (((b * NT + I) * NT + J) * NTR + tr) * TILE + rc, s[tr]);
+  }
+  chain_publish(flag_part(ch, b, NT, I, J), ch.seq, ch.mode);
+  tr_.done(WGT_STILE, J, I, b);
+}
+
+// F(b, 0)'s last step, out of line (inlined, its Pearson reductions pushed the whole kernel past
+// 64 VGPRs): EBV_v = sum_J e_J[v] - sm sum_J mb_J + mu (J ascending, J = 0 already in eall),
+// then |pearsonr| per trait, averaged over traits
+template <int NTR>
+__device__ __noinline__ void chain_final(const double* ep, const double* mbp, const double* mb0, int NT, int64_t nV,
+                                         bool muf, double sm, bool bad, const double* ymu, const double* yV,
+                                         double* eall, double* red, double* fit, double* ebv) {
+  const int t = threadIdx.x;
+  double fsum = 0.0;
+  for (int tr = 0; tr < NTR; ++tr) {
+    double mbt = mb0[tr];
+    for (int K = 1; K < NT; ++K) mbt += cload(mbp + K * NTR + tr);
+    const double MB = mbt * sm, mu = muf ? ymu[tr] : 0.0;
+    double* e = eall + tr * nV;
+    for (int64_t v = t; v < nV; v += CTH) {
+      double acc = e[v];
+      for (int K = 1; K < NT; ++K) acc += cload(ep + (K * NTR + tr) * nV + v);
+      e[v] = acc - MB + mu;
+    }
+    __syncthreads();
+    fsum += pearson_abs<CTH>(e, yV + tr * nV, nV, red);
+    if (ebv != nullptr)
+      for (int64_t v = t; v < nV; v += CTH) ebv[tr * nV + v] = e[v];
+  }
+  if (t == 0) *fit = bad ? __builtin_nan("") : (NTR == 1) ? fsum : fsum / (double)NTR;
+}
+
+template <int NTR>
+__device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, double* fit, double* ebv,
+                          double* eall, int* sh, ChainTrace& tr_) {
+  __shared__ double zsh[NTR][TILE];
+  __shared__ double vsh[NTR][TILE];
+  __shared__ double bsh[NTR][TILE];
+  __shared__ int32_t rowp[TILE];
+  __shared__ double red[CTH / 64];
+  const int t = threadIdx.x;
+  const int NT = c.sd.NT;
+  const int64_t ns = c.sd.ns, nV = c.d.nV, nTp = c.d.nTp;
+  const double* sc = c.scal + b * SCAL;
+  const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b];
+  const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));   // real SNP rows of block J
+  for (int i = t; i < NTR * TILE; i += CTH) zsh[i / TILE][i % TILE] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
+  for (int r = t; r < nr; r += CTH) rowp[r] = (int32_t)snp_col(c.idx[o0 + (int64_t)J * TILE + r], c.d.P);
+  // beta_J[rc] = (X_J^T v)[rc] = sum_i X[i][rc] v[i]: Dinv holds the lower blocks of X
+  // transposed, so thread (rc, seg) reads row rc%16 of block (seg, rc/16) -- 16 contiguous i --
+  // which exists iff seg >= rc/16 (as in k_solve)
+  const int rc = t >> 3, seg = t & 7;
+  const double* Db = c.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
+  v2d xr[8];
+  const bool xrow = seg >= (rc >> 4);
+  {
+    const double* xb = Db + (xrow ? pk(seg, rc >> 4) + (rc & 15) * NB : 0);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) xr[m] = *reinterpret_cast<const v2d*>(xb + 2 * m);
+  }
+  for (int K = J + 1; K < NT; ++K)
+    if (!chain_wait(flag_part(ch, b, NT, J, K), ch.seq, ch.err, sh, ch.mode)) {
+      if (J == 0 && t == 0) fit[b] = __builtin_nan("");
+      return;
+    }
+  tr_.waited();
+  __syncthreads();
+  for (int i = t; i < NTR * TILE; i += CTH) {
+    const int tr = i / TILE, cc = i % TILE;
+    double acc = 0.0;
+    for (int K = J + 1; K < NT; ++K) acc += cload(ch.cpart + (((b * NT + J) * NT + K) * NTR + tr) * TILE + cc);
+    vsh[tr][cc] = zsh[tr][cc] - acc;
+  }
+  __syncthreads();
+  {
+    double s2[NTR];
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr) s2[tr] = 0.0;
+    if (xrow) {
+      const int sw = (rc >> 1) & 7;   // bo(): 16-B chunk m of the row holds columns 2(m ^ sw), +1
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const v2d xv = xr[m];
+        const int i0 = 16 * seg + 2 * (m ^ sw);
+#pragma unroll
+        for (int tr = 0; tr < NTR; ++tr) s2[tr] += xv[0] * vsh[tr][i0] + xv[1] * vsh[tr][i0 + 1];
+      }
+    }
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr) {
+      s2[tr] += __shfl_xor(s2[tr], 1);
+      s2[tr] += __shfl_xor(s2[tr], 2);
+      s2[tr] += __shfl_xor(s2[tr], 4);
+      if (seg == 0) {
+        cstore(ch.beta + (b * NTR + tr) * ns + (int64_t)J * TILE + rc, s2[tr]);
+        bsh[tr][rc] = s2[tr];
+      }
+    }
+  }
+  chain_publish(flag_beta(ch, b, NT, J), ch.seq, ch.mode);
+
+  // block J's share of the prediction: e_J[v] = sum_{a in J} x_va beta_a (int8 split rows, V
+  // animals from byte nTp: thread (quad of animals, row group rg of 8) reads 4 B per row)
+  const int rg = t & 7;
+  const int64_t nq = (nV + 3) / 4;
+  double* eown = eall;   // [NTR][nV]: this block's share, then (F(b, 0)) the EBVs
+  for (int tr = 0; tr < NTR; ++tr)   // one trait at a time: 4 accumulators per thread
+    for (int64_t qd = t >> 3; qd < nq; qd += CTH / 8) {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+      for (int r = rg; r < nr; r += 8) {
+        const uint32_t xw = *reinterpret_cast<const uint32_t*>(c.gs + (int64_t)rowp[r] * c.gs_row + nTp + 4 * qd);
+        const double br = bsh[tr][r];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += (double)((xw >> (8 * j)) & 0xff) * br;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] += __shfl_xor(acc[j], 1);
+        acc[j] += __shfl_xor(acc[j], 2);
+        acc[j] += __shfl_xor(acc[j], 4);
+        const int64_t v = 4 * qd + j;
+        if (rg == 0 && v < nV) {
+          eown[tr * nV + v] = acc[j];
+          if (J > 0) cstore(ch.epart + ((b * NT + J) * NTR + tr) * nV + v, acc[j]);
+        }
+      }
+    }
+  // and of sum_a s_a beta_a (the train-centring term)
+  double mb[NTR];
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) {
+    const double m = t < nr ? c.u[b * c.sd.prow + (int64_t)J * TILE + t] * bsh[tr][t] : 0.0;
+    mb[tr] = block_sum<CTH>(m, red);
+    if (J > 0 && t == 0) cstore(ch.mbpart + (b * NT + J) * NTR + tr, mb[tr]);
+  }
+  if (J > 0) {
+    chain_publish(flag_e(ch, b, NT, J), ch.seq, ch.mode);
+    tr_.done(WGT_SROW, J, 0, b);
+    return;
+  }
+  // F(b, 0): EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu, J ascending; then the fitness
+  for (int K = 1; K < NT; ++K)
+    if (!chain_wait(flag_e(ch, b, NT, K), ch.seq, ch.err, sh, ch.mode)) {
+      if (t == 0) fit[b] = __builtin_nan("");
+      return;
+    }
+  chain_final<NTR>(ch.epart + b * NT * NTR * nV, ch.mbpart + b * NT * NTR, mb, NT, nV, sc[SC_MUF] != 0.0,
+                   sc[SC_SM], sc[SC_BAD] != 0.0, c.ymu, c.yV, eall, red, fit + b,
+                   ebv != nullptr ? ebv + b * NTR * nV : nullptr);
+  tr_.done(WGT_SROW, J, 1, b);
+}
+
+template <int NTR>
+__global__ __launch_bounds__(CTH, NTR <= 2 ? 8 : 4) void k_solve_chain(CholLaunch c, SolveChain ch, double* __restrict__ fit,
+                                                     double* __restrict__ ebv) {
+  extern __shared__ double eall[];   // [NTR][nV]
+  __shared__ double bsh[NTR][TILE];
+  __shared__ int sh;
+  const int NT = c.sd.NT;
+  const int64_t B = c.B;
+  int64_t g = blockIdx.x;
+  int J = NT - 1;
+  for (; J > 0 && g >= B * (1 + J); --J) g -= B * (1 + J);
+  ChainTrace tr(c.wgt);
+  if (g < B) {
+    chain_row<NTR>(c, ch, g, J, fit, ebv, eall, &sh, tr);
+  } else {
+    g -= B;
+    chain_tile<NTR>(c, ch, g / J, J, (int)(g % J), bsh, &sh, tr);
+  }
+}
+
+hipError_t launch_solve(const CholLaunch& c, const SolveChain* ch, double* fitness, double* ebv, hipStream_t s) {
   const size_t shm = (size_t)c.d.nt * (size_t)(c.sd.ns + c.d.nV) * sizeof(double) + (size_t)((c.sd.ns + 1) / 2) * sizeof(double);
   auto launch = [&](const void* fn, auto kernel) -> hipError_t {
     if (shm > 64 * 1024) {
@@ -319,6 +631,25 @@ hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipSt
     hipLaunchKernelGGL(kernel, dim3((unsigned)c.B), dim3(NTH), shm, s, c, fitness, ebv);
     return hipGetLastError();
   };
+  if (ch != nullptr && c.sd.form == FORM_PRIMAL) {
+    const size_t eshm = (size_t)c.d.nt * (size_t)c.d.nV * sizeof(double);
+    const dim3 grid((unsigned)(c.B * c.sd.NT * (c.sd.NT + 1) / 2));
+    auto launch_chain = [&](const void* fn, auto kernel) -> hipError_t {
+      if (eshm > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eshm);
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL(kernel, grid, dim3(CTH), eshm, s, c, *ch, fitness, ebv);
+      return hipGetLastError();
+    };
+    switch (c.d.nt) {
+      case 1: return launch_chain((const void*)k_solve_chain<1>, k_solve_chain<1>);
+      case 2: return launch_chain((const void*)k_solve_chain<2>, k_solve_chain<2>);
+      case 3: return launch_chain((const void*)k_solve_chain<3>, k_solve_chain<3>);
+      case 4: return launch_chain((const void*)k_solve_chain<4>, k_solve_chain<4>);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (c.d.nt) {
     case 1: return launch((const void*)k_solve<1>, k_solve<1>);
     case 2: return launch((const void*)k_solve<2>, k_solve<2>);

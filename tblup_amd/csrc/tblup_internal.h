@@ -194,7 +194,22 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 // counts into c.kc, diagonal tiles into Kd (replaces launch_diag_grm and the int8 phase of the
 // off-diagonal tiles)
 hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s);
-hipError_t launch_solve(const CholLaunch& c, double* fitness, double* ebv, hipStream_t s);
+// Back substitution, prediction and fitness.  ch == null: one workgroup per individual
+// (k_solve); else (SNP form) the chained solve (k_solve_chain): an individual's block rows and
+// tile products spread over the chip, handing beta_J and the partial products on through
+// per-call flags (SolveChain).
+struct SolveChain {
+  int32_t* flags;   // [B][chain_flags(NT)], compared with seq (never reset)
+  double* beta;     // [B][nt][ns]
+  double* cpart;    // [B][NT (row I)][NT (tile J)][nt][128]: L_JI^T beta_J
+  double* epart;    // [B][NT][nt][nV]: block J's share of X_V beta
+  double* mbpart;   // [B][NT][nt]: block J's share of sum_a s_a beta_a
+  int32_t* err;     // a wait gave up (the calls' fitness is then NaN)
+  int32_t seq;      // this call's flag value
+  int32_t mode;     // TBLUP_CHAIN_SYNC (k_solve.hip)
+};
+__host__ __device__ inline int64_t chain_flags(int NT) { return (int64_t)NT * (NT + 2); }
+hipError_t launch_solve(const CholLaunch& c, const SolveChain* ch, double* fitness, double* ebv, hipStream_t s);
 
 // ---- launcher (k_decode.hip): RandomKey genome decode, top-k of each key row ----
 hipError_t launch_decode_topk(const double* keys, int64_t B, int64_t d, int64_t ld, const int64_t* off, int64_t* out,

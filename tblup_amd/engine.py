@@ -342,8 +342,8 @@ class GpuBlupEngine:
                 for i, name in enumerate(_native.KCLASS_NAMES)}
 
     def wg_trace(self, raw=False):
-        """Per-workgroup records of the last evaluation's Cholesky launches (TBLUP_WG_TRACE=1):
-        structured array (start, end [s], kind, J, I, b); raw=True: the (n, 4) uint64 records
+        """Per-workgroup records of the last evaluation's Cholesky launches and chained solve
+        (TBLUP_WG_TRACE=1): structured array (start, end [s], kind, J, I, b, wait [s]); raw=True: the (n, 4) uint64 records
         (including each diagonal launch's phase-stamp block, kind 0)."""
         n = ctypes.c_int64(0)
         _native.check("tblup_get_wg_trace", self._lib.tblup_get_wg_trace(self._ctx, None, 0, ctypes.byref(n)))
@@ -355,13 +355,14 @@ class GpuBlupEngine:
         if raw_out:
             return raw
         out = np.zeros(len(raw), dtype=[("start", "f8"), ("end", "f8"), ("kind", "i4"), ("J", "i4"), ("I", "i4"),
-                                        ("b", "i8")])
+                                        ("b", "i8"), ("wait", "f8")])
         out["start"] = raw[:, 0] / 1e8
         out["end"] = raw[:, 1] / 1e8
         out["kind"] = (raw[:, 2] >> np.uint64(56)).astype(np.int32)
         out["I"] = ((raw[:, 2] >> np.uint64(40)) & np.uint64(0xFFFF)).astype(np.int32)
         out["b"] = (raw[:, 2] & np.uint64((1 << 40) - 1)).astype(np.int64)
-        out["J"] = raw[:, 3].astype(np.int32)
+        out["J"] = (raw[:, 3] & np.uint64(0xFFFF)).astype(np.int32)
+        out["wait"] = (raw[:, 3] >> np.uint64(16)) / 1e8      # chained-solve units: first wait done - start
         return out[out["kind"] != 0]
 
     def mem_in_use(self):
