@@ -101,7 +101,8 @@ struct tblup_ctx {
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
-  int solve_chain = 0;   // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain)
+  int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
+                         // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
   DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
   int32_t chain_seq = 0; // flag value of the last chained solve
 };
@@ -237,6 +238,13 @@ bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
   return false;
 }
 
+// SNP-form solve: the chained kernel below CHAIN_MAX_B individuals (measured: faster at 32 / 128,
+// slower at 256, where one workgroup per individual already streams L at the HBM rate)
+constexpr int64_t CHAIN_MAX_B = 192;
+bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B) {
+  return sd.form == FORM_PRIMAL && (c->solve_chain == 1 || (c->solve_chain < 0 && B <= CHAIN_MAX_B));
+}
+
 size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k,
                    bool with_ebv) {
   size_t s = 0;
@@ -253,7 +261,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
   add(any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
-  if (sd.form == FORM_PRIMAL && c->solve_chain) {               // chained solve: beta, c_{J->I}, EBV shares
+  if (use_chain(c, sd, B)) {                                    // chained solve: beta, c_{J->I}, EBV shares
     add((size_t)B * d.nt * sd.ns * 8);
     add((size_t)B * sd.NT * sd.NT * d.nt * TILE * 8);
     add((size_t)B * sd.NT * d.nt * d.nV * 8);
@@ -381,7 +389,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     int64_t nwg = 0;
     for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
-    if (sd.form == FORM_PRIMAL && c->solve_chain) nwg += B * sd.NT * (sd.NT + 1) / 2;   // chained solve units
+    if (use_chain(c, sd, B)) nwg += B * sd.NT * (sd.NT + 1) / 2;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
     wgt = (uint64_t*)c->wgt.p;
@@ -448,7 +456,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
                                  kbar * (double)(d.nT + d.nV));
   SolveChain ch{};
   const SolveChain* chp = nullptr;
-  if (sd.form == FORM_PRIMAL && c->solve_chain) {
+  if (use_chain(c, sd, B)) {
     const size_t fbytes = ((size_t)B * chain_flags(sd.NT) + 1) * 4;
     if (c->chain.bytes < fbytes || c->chain_seq >= INT32_MAX - 1) {
       HIPCHK(hipStreamSynchronize(s));   // the flags may still be read by an earlier chained solve
@@ -530,7 +538,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   const char* fp = getenv("TBLUP_FORM");
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   if (const char* e = getenv("TBLUP_AHEAD")) c->ahead = std::max(-1, std::min(1, atoi(e)));
-  if (const char* e = getenv("TBLUP_SOLVE_CHAIN")) c->solve_chain = atoi(e) != 0;
+  if (const char* e = getenv("TBLUP_SOLVE_CHAIN")) c->solve_chain = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_CHAIN_SYNC")) c->chain_sync = atoi(e);
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
   if (!panel) {

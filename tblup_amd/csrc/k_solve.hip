@@ -47,9 +47,10 @@ __device__ __forceinline__ double block_max(double v, double* red) {
 
 }  // namespace
 
+// (NTH_ may be below the block size: the threads past it hold no elements; red needs a slot per wave)
 template <int NTH_ = NTH>
 __device__ __forceinline__ double pearson_abs(const double* e, const double* yV, int64_t nV, double* red) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x < NTH_ ? (int)threadIdx.x : (int)nV;
   const double yb = yV[0], eb = e[0];
   double sx = 0.0, sy = 0.0, ncx = 0.0, ncy = 0.0;
   for (int64_t v = t; v < nV; v += NTH_) {
@@ -86,6 +87,87 @@ __device__ __forceinline__ double pearson_abs(const double* e, const double* yV,
   return fabs(r);
 }
 
+
+// ---- arithmetic shared by k_solve and k_solve_chain (the SNP-form results of the two are
+// bit-identical, so the launcher may pick either per batch) ----
+constexpr int PCTH = 512;   // Pearson / centring-term reductions as over 512 threads
+
+// p = (L_JI^T beta_J)[row] for the 16 r of lane group seg of the row's 8 threads (x: the row's
+// 16 doubles at r = 16 seg ..), xor-reduced over the 8 threads: every thread of the row holds p
+template <int NTR>
+__device__ __forceinline__ void tile_row_partial(const v2d (&x)[8], const double* beta, int64_t stride, int seg,
+                                                 double (&p)[NTR]) {
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) p[tr] = 0.0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)   // explicit fmas: no contraction choice left to the compiler
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr)
+      p[tr] = __builtin_fma(x[e][1], beta[tr * stride + 16 * seg + 2 * e + 1],
+                            __builtin_fma(x[e][0], beta[tr * stride + 16 * seg + 2 * e], p[tr]));
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) {
+    p[tr] += __shfl_xor(p[tr], 1);
+    p[tr] += __shfl_xor(p[tr], 2);
+    p[tr] += __shfl_xor(p[tr], 4);
+  }
+}
+
+// beta[row] = (X^T v)[row] = sum_i X[i][row] v[i]: Dinv holds the lower blocks of X transposed, so
+// thread (row, seg) reads row row%16 of block (seg, row/16) -- 16 contiguous i -- which exists iff
+// seg >= row/16; xor-reduced over the row's 8 threads
+__device__ __forceinline__ bool xrow_load(const double* Dj, int row, int seg, v2d (&xr)[8]) {
+  const bool ok = seg >= (row >> 4);
+  const double* xb = Dj + (ok ? pk(seg, row >> 4) + (row & 15) * NB : 0);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) xr[m] = *reinterpret_cast<const v2d*>(xb + 2 * m);
+  return ok;
+}
+template <int NTR>
+__device__ __forceinline__ void xrow_apply(const v2d (&xr)[8], bool ok, int row, int seg, const double (*vsh)[TILE],
+                                           double (&s2)[NTR]) {
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) s2[tr] = 0.0;
+  if (ok) {
+    const int sw = (row >> 1) & 7;   // bo(): 16-B chunk m of the row holds columns 2(m ^ sw), +1
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const v2d xv = xr[m];
+      const int i0 = 16 * seg + 2 * (m ^ sw);
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr) s2[tr] = __builtin_fma(xv[1], vsh[tr][i0 + 1], __builtin_fma(xv[0], vsh[tr][i0], s2[tr]));
+    }
+  }
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) {
+    s2[tr] += __shfl_xor(s2[tr], 1);
+    s2[tr] += __shfl_xor(s2[tr], 2);
+    s2[tr] += __shfl_xor(s2[tr], 4);
+  }
+}
+
+// block J's share of the SNP-form prediction for animals 4 qd .. 4 qd + 3: sum over the block's
+// rows r = rg, rg + 8, .. < nr of x_va beta_r (int8 split rows, V animals from byte nTp), then
+// xor-reduced over the 8 row groups
+__device__ __forceinline__ void pred_share(const int8_t* gs, int64_t gs_row, const int32_t* rowp, const double* br,
+                                           int nr, int64_t off, int rg, double (&acc)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = 0.0;
+#pragma unroll 4
+  for (int r = rg; r < nr; r += 8) {
+    const uint32_t xw = *reinterpret_cast<const uint32_t*>(gs + (int64_t)rowp[r] * gs_row + off);
+    const double bv = br[r];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = __builtin_fma((double)((xw >> (8 * j)) & 0xff), bv, acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc[j] += __shfl_xor(acc[j], 1);
+    acc[j] += __shfl_xor(acc[j], 2);
+    acc[j] += __shfl_xor(acc[j], 4);
+  }
+}
+
 template <int NTR>
 __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict__ fit, double* __restrict__ ebv) {
   extern __shared__ double dyn[];  // alpha[nt][ns], e[nt][nV], then (primal) int32 rowp[ns]
@@ -116,6 +198,8 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   for (int64_t i = t; i < nt * ns; i += NTH) alpha[i] = c.z[b * nt * ns + i];
   __syncthreads();
   for (int I = NT - 1; I >= 0; --I) {
+    // s = sum_{J > I} (L_JI^T alpha_J), one tile's row partial at a time, J ascending (the
+    // chained solve's order)
     double s[NTR] = {};
     // two tiles per step: 256 B per thread (256 KiB per workgroup) in flight
     for (int J = I + 1; J < ((c.skip & 1024) ? 0 : NT); J += 2) {
@@ -127,62 +211,28 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       for (int e = 0; e < 8; ++e) x0[e] = *reinterpret_cast<const v2d*>(row0 + 2 * e);
 #pragma unroll
       for (int e = 0; e < 8; ++e) x1[e] = *reinterpret_cast<const v2d*>(row1 + 2 * e);
+      double p[NTR];
+      tile_row_partial<NTR>(x0, alpha + J * TILE, ns, seg, p);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-#pragma unroll
-        for (int tr = 0; tr < NTR; ++tr) {
-          const double* al = alpha + tr * ns + J * TILE + 16 * seg;
-          s[tr] += x0[e][0] * al[2 * e] + x0[e][1] * al[2 * e + 1];
-        }
-      }
+      for (int tr = 0; tr < NTR; ++tr) s[tr] += p[tr];
       if (two) {
+        tile_row_partial<NTR>(x1, alpha + (J + 1) * TILE, ns, seg, p);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-#pragma unroll
-          for (int tr = 0; tr < NTR; ++tr) {
-            const double* al = alpha + tr * ns + (J + 1) * TILE + 16 * seg;
-            s[tr] += x1[e][0] * al[2 * e] + x1[e][1] * al[2 * e + 1];
-          }
-        }
+        for (int tr = 0; tr < NTR; ++tr) s[tr] += p[tr];
       }
     }
-    // alpha_I[c] = (X_I^T v)[c] = sum_i X[i][c] v[i].  Dinv holds the lower blocks of X
-    // transposed (block (q, jb) stores X_{q,jb}^T), so thread (c, seg) reads row c%16 of
-    // block (seg, c/16) -- 16 contiguous i -- which exists iff seg >= c/16.  Loaded before
-    // the reduction and barrier so that their latency overlaps them.
-    const bool xrow = seg >= (rc >> 4);
+    // alpha_I = X_I^T v, X_I's row loaded before the barrier so that its latency overlaps it
     v2d xr[8];
-    {
-      const double* xb = Db + (int64_t)I * NPACK * BLKD + (xrow ? pk(seg, rc >> 4) + (rc & 15) * NB : 0);
+    const bool xrow = xrow_load(Db + (int64_t)I * NPACK * BLKD, rc, seg, xr);
 #pragma unroll
-      for (int m = 0; m < 8; ++m) xr[m] = *reinterpret_cast<const v2d*>(xb + 2 * m);
-    }
-#pragma unroll
-    for (int tr = 0; tr < NTR; ++tr) {
-      s[tr] += __shfl_xor(s[tr], 1);
-      s[tr] += __shfl_xor(s[tr], 2);
-      s[tr] += __shfl_xor(s[tr], 4);
+    for (int tr = 0; tr < NTR; ++tr)
       if (seg == 0) vsh[tr][rc] = alpha[tr * ns + (int64_t)I * TILE + rc] - s[tr];
-    }
     __syncthreads();
-    double s2[NTR] = {};
-    if (xrow) {
-      const int sw = (rc >> 1) & 7;   // bo(): 16-B chunk m of the row holds columns 2(m ^ sw), +1
+    double s2[NTR];
+    xrow_apply<NTR>(xr, xrow, rc, seg, vsh, s2);
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const v2d x = xr[m];
-        const int i0 = 16 * seg + 2 * (m ^ sw);
-#pragma unroll
-        for (int tr = 0; tr < NTR; ++tr) s2[tr] += x[0] * vsh[tr][i0] + x[1] * vsh[tr][i0 + 1];
-      }
-    }
-#pragma unroll
-    for (int tr = 0; tr < NTR; ++tr) {
-      s2[tr] += __shfl_xor(s2[tr], 1);
-      s2[tr] += __shfl_xor(s2[tr], 2);
-      s2[tr] += __shfl_xor(s2[tr], 4);
+    for (int tr = 0; tr < NTR; ++tr)
       if (seg == 0) alpha[tr * ns + I * TILE + rc] = s2[tr];
-    }
     __syncthreads();
   }
 
@@ -205,51 +255,30 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     const double* yV = c.yV + tr * nV;
     const double mu = muf * c.ymu[tr];
     if (c.sd.form == FORM_PRIMAL) {
-      // EBV_v = sum_a x_va beta_a - sum_a (s_a / n_T) beta_a + mu, reduced over a by row groups
+      // EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu with block J's shares e_J[v] = sum_{a in J}
+      // x_va beta_a and mb_J = sum_{a in J} s_a beta_a, J ascending (the chained solve's order)
       const int64_t kk = (int64_t)sc[SC_K];
-      double s_ub = 0.0;
-      for (int64_t r = t; r < kk; r += NTH) s_ub += ub[r] * al[r];
-      const double MB = block_sum(s_ub, red) * sc[SC_SM];
-      // X_V read in place from the split's SNP-major rows (V animals start at byte nTp), in
-      // 256-animal chunks: thread (row group rg, lane lq) reads 16 animals of each of its rows
-      // with one 16-B load; the four row groups of a wave reduce by lane shuffles, the 16
-      // waves through LDS.
-      const int lq = t & 15, rg = t >> 4, l = t & 63, w = t >> 6;
-      double* pv = &part[0][0];   // [16 waves][256]
-      const int64_t nch = (nV + 255) / 256;
-      for (int64_t ch = 0; ch < nch; ++ch) {
-        double acc[16];
+      const int rg = t & 7;
+      const int64_t nq = (nV + 3) / 4;
+      double mbt = 0.0;
+      for (int J = 0; J < NT; ++J) {
+        const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));
+        for (int64_t qd = t >> 3; qd < ((c.skip & 2048) ? 0 : nq); qd += NTH / 8) {
+          double acc[4];
+          pred_share(c.gs, c.gs_row, rowp + J * TILE, al + J * TILE, nr, nTp + 4 * qd, rg, acc);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = 0.0;
-        const int64_t vo = nTp + ch * 256 + 16 * lq;
-#pragma unroll 4
-        for (int64_t r = rg; r < ((c.skip & 2048) ? 0 : kk); r += NTH / 16) {
-          const uint4 x = *reinterpret_cast<const uint4*>(c.gs + (int64_t)rowp[r] * c.gs_row + vo);
-          const double ar = al[r];
-          const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-          for (int d = 0; d < 4; ++d)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[4 * d + j] += (double)((xw[d] >> (8 * j)) & 0xff) * ar;
+          for (int j = 0; j < 4; ++j) {
+            const int64_t v = 4 * qd + j;
+            if (rg == 0 && v < nV) e[v] = (J == 0) ? acc[j] : e[v] + acc[j];
+          }
         }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          acc[j] += __shfl_xor(acc[j], 16);
-          acc[j] += __shfl_xor(acc[j], 32);
-        }
-        __syncthreads();
-        if (l < 16) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) pv[w * 256 + 16 * lq + j] = acc[j];
-        }
-        __syncthreads();
-        if (t < 256 && ch * 256 + t < nV) {
-          double sacc = 0.0;
-#pragma unroll
-          for (int q = 0; q < NTH / 64; ++q) sacc += pv[q * 256 + t];
-          e[ch * 256 + t] = sacc - MB + mu;
-        }
+        const double m = t < nr ? ub[(int64_t)J * TILE + t] * al[(int64_t)J * TILE + t] : 0.0;
+        const double mbj = block_sum<PCTH>(t < PCTH ? m : 0.0, red);
+        mbt = (J == 0) ? mbj : mbt + mbj;
       }
+      __syncthreads();
+      const double MB = mbt * sc[SC_SM];
+      for (int64_t v = t; v < nV; v += NTH) e[v] = e[v] - MB + mu;
       __syncthreads();
     } else {
       // EBV_V = K_VT alpha + mu without materialising K_VT (exact-integer factored form):
@@ -304,7 +333,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       __syncthreads();
     }
     // Pearson correlation (scipy.stats.pearsonr restated); multi-trait fitness is the mean |r|
-    fsum += pearson_abs(e, yV, nV, red);
+    fsum += pearson_abs<PCTH>(e, yV, nV, red);
     if (ebv != nullptr) {
       for (int64_t v = t; v < nV; v += NTH) ebv[(b * nt + tr) * nV + v] = e[v];
     }
@@ -331,7 +360,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 // (SPIN_MAX polls; one expired wait makes every later wait give up at once).  Every sum has a
 // fixed order, so the results do not depend on B, the timing or the grid.
 // ===========================================================================
-constexpr int CTH = 1024;   // single-trait: <= 64 VGPRs, two units (32 waves) per CU
+constexpr int CTH = 512;
 constexpr int SPIN_MAX = 1 << 20;
 enum { WGT_SROW = 7, WGT_STILE = 8 };
 
@@ -423,61 +452,29 @@ __device__ __forceinline__ void chain_publish(int32_t* f, int32_t seq, int mode)
 template <int NTR>
 __device__ void chain_tile(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, int I, double (*bsh)[TILE],
                            int* sh, ChainTrace& tr_) {
-  const int t = threadIdx.x, rc = t >> 3, qq = t & 7;
+  const int t = threadIdx.x, rc = t >> 3, seg = t & 7;   // rows rc and rc + 64, 8 threads per row
   const int NT = c.sd.NT;
   const int64_t ns = c.sd.ns;
-  // (L_JI^T beta_J)[rc] = sum_r Lt_(J,I)[rc][r] beta_J[r]: 8 threads per row, 16 r each
-  const double* row = c.L + ((b * NT + J) * (int64_t)NT + I) * TILE * TILE + rc * TILE + 16 * qq;
-  v2d x[8];
+  const double* tile = c.L + ((b * NT + J) * (int64_t)NT + I) * TILE * TILE + 16 * seg;
+  v2d x[2][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) x[e] = *reinterpret_cast<const v2d*>(row + 2 * e);
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[h][e] = *reinterpret_cast<const v2d*>(tile + (rc + 64 * h) * TILE + 2 * e);
   if (!chain_wait(flag_beta(ch, b, NT, J), ch.seq, ch.err, sh, ch.mode)) return;
   tr_.waited();
   for (int i = t; i < NTR * TILE; i += CTH) bsh[i / TILE][i % TILE] = cload(ch.beta + (b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE);
   __syncthreads();
-  double s[NTR];
 #pragma unroll
-  for (int tr = 0; tr < NTR; ++tr) s[tr] = 0.0;
+  for (int h = 0; h < 2; ++h) {
+    double p[NTR];
+    tile_row_partial<NTR>(x[h], &bsh[0][0], TILE, seg, p);
 #pragma unroll
-  for (int e = 0; e < 8; ++e)
-#pragma unroll
-    for (int tr = 0; tr < NTR; ++tr) s[tr] += x[e][0] * bsh[tr][16 * qq + 2 * e] + x[e][1] * bsh[tr][16 * qq + 2 * e + 1];
-#pragma unroll
-  for (int tr = 0; tr < NTR; ++tr) {
-    s[tr] += __shfl_xor(s[tr], 1);
-    s[tr] += __shfl_xor(s[tr], 2);
-    s[tr] += __shfl_xor(s[tr], 4);
-    if (qq == 0) cstore(ch.cpart + (((b * NT + I) * NT + J) * NTR + tr) * TILE + rc, s[tr]);
+    for (int tr = 0; tr < NTR; ++tr)
+      if (seg == 0) cstore(ch.cpart + (((b * NT + I) * NT + J) * NTR + tr) * TILE + rc + 64 * h, p[tr]);
   }
   chain_publish(flag_part(ch, b, NT, I, J), ch.seq, ch.mode);
   tr_.done(WGT_STILE, J, I, b);
-}
-
-// F(b, 0)'s last step, out of line (inlined, its Pearson reductions pushed the whole kernel past
-// 64 VGPRs): EBV_v = sum_J e_J[v] - sm sum_J mb_J + mu (J ascending, J = 0 already in eall),
-// then |pearsonr| per trait, averaged over traits
-template <int NTR>
-__device__ __noinline__ void chain_final(const double* ep, const double* mbp, const double* mb0, int NT, int64_t nV,
-                                         bool muf, double sm, bool bad, const double* ymu, const double* yV,
-                                         double* eall, double* red, double* fit, double* ebv) {
-  const int t = threadIdx.x;
-  double fsum = 0.0;
-  for (int tr = 0; tr < NTR; ++tr) {
-    double mbt = mb0[tr];
-    for (int K = 1; K < NT; ++K) mbt += cload(mbp + K * NTR + tr);
-    const double MB = mbt * sm, mu = muf ? ymu[tr] : 0.0;
-    double* e = eall + tr * nV;
-    for (int64_t v = t; v < nV; v += CTH) {
-      double acc = e[v];
-      for (int K = 1; K < NT; ++K) acc += cload(ep + (K * NTR + tr) * nV + v);
-      e[v] = acc - MB + mu;
-    }
-    __syncthreads();
-    fsum += pearson_abs<CTH>(e, yV + tr * nV, nV, red);
-    if (ebv != nullptr)
-      for (int64_t v = t; v < nV; v += CTH) ebv[tr * nV + v] = e[v];
-  }
-  if (t == 0) *fit = bad ? __builtin_nan("") : (NTR == 1) ? fsum : fsum / (double)NTR;
 }
 
 template <int NTR>
@@ -496,18 +493,13 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));   // real SNP rows of block J
   for (int i = t; i < NTR * TILE; i += CTH) zsh[i / TILE][i % TILE] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
   for (int r = t; r < nr; r += CTH) rowp[r] = (int32_t)snp_col(c.idx[o0 + (int64_t)J * TILE + r], c.d.P);
-  // beta_J[rc] = (X_J^T v)[rc] = sum_i X[i][rc] v[i]: Dinv holds the lower blocks of X
-  // transposed, so thread (rc, seg) reads row rc%16 of block (seg, rc/16) -- 16 contiguous i --
-  // which exists iff seg >= rc/16 (as in k_solve)
+  // X_J's rows rc and rc + 64 before the wait
   const int rc = t >> 3, seg = t & 7;
-  const double* Db = c.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
-  v2d xr[8];
-  const bool xrow = seg >= (rc >> 4);
-  {
-    const double* xb = Db + (xrow ? pk(seg, rc >> 4) + (rc & 15) * NB : 0);
+  const double* Dj = c.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
+  v2d xr[2][8];
+  bool xok[2];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) xr[m] = *reinterpret_cast<const v2d*>(xb + 2 * m);
-  }
+  for (int h = 0; h < 2; ++h) xok[h] = xrow_load(Dj, rc + 64 * h, seg, xr[h]);
   for (int K = J + 1; K < NT; ++K)
     if (!chain_wait(flag_part(ch, b, NT, J, K), ch.seq, ch.err, sh, ch.mode)) {
       if (J == 0 && t == 0) fit[b] = __builtin_nan("");
@@ -515,73 +507,45 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
     }
   tr_.waited();
   __syncthreads();
-  for (int i = t; i < NTR * TILE; i += CTH) {
+  for (int i = t; i < NTR * TILE; i += CTH) {   // v = z_J - sum_{K > J} c_{K->J}, K ascending
     const int tr = i / TILE, cc = i % TILE;
     double acc = 0.0;
     for (int K = J + 1; K < NT; ++K) acc += cload(ch.cpart + (((b * NT + J) * NT + K) * NTR + tr) * TILE + cc);
     vsh[tr][cc] = zsh[tr][cc] - acc;
   }
   __syncthreads();
-  {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
     double s2[NTR];
+    xrow_apply<NTR>(xr[h], xok[h], rc + 64 * h, seg, vsh, s2);
 #pragma unroll
-    for (int tr = 0; tr < NTR; ++tr) s2[tr] = 0.0;
-    if (xrow) {
-      const int sw = (rc >> 1) & 7;   // bo(): 16-B chunk m of the row holds columns 2(m ^ sw), +1
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const v2d xv = xr[m];
-        const int i0 = 16 * seg + 2 * (m ^ sw);
-#pragma unroll
-        for (int tr = 0; tr < NTR; ++tr) s2[tr] += xv[0] * vsh[tr][i0] + xv[1] * vsh[tr][i0 + 1];
-      }
-    }
-#pragma unroll
-    for (int tr = 0; tr < NTR; ++tr) {
-      s2[tr] += __shfl_xor(s2[tr], 1);
-      s2[tr] += __shfl_xor(s2[tr], 2);
-      s2[tr] += __shfl_xor(s2[tr], 4);
+    for (int tr = 0; tr < NTR; ++tr)
       if (seg == 0) {
-        cstore(ch.beta + (b * NTR + tr) * ns + (int64_t)J * TILE + rc, s2[tr]);
-        bsh[tr][rc] = s2[tr];
+        cstore(ch.beta + (b * NTR + tr) * ns + (int64_t)J * TILE + rc + 64 * h, s2[tr]);
+        bsh[tr][rc + 64 * h] = s2[tr];
       }
-    }
   }
   chain_publish(flag_beta(ch, b, NT, J), ch.seq, ch.mode);
 
-  // block J's share of the prediction: e_J[v] = sum_{a in J} x_va beta_a (int8 split rows, V
-  // animals from byte nTp: thread (quad of animals, row group rg of 8) reads 4 B per row)
+  // block J's share of the prediction and of the centring term
   const int rg = t & 7;
   const int64_t nq = (nV + 3) / 4;
-  double* eown = eall;   // [NTR][nV]: this block's share, then (F(b, 0)) the EBVs
-  for (int tr = 0; tr < NTR; ++tr)   // one trait at a time: 4 accumulators per thread
+  double mb[NTR];
+  for (int tr = 0; tr < NTR; ++tr) {
     for (int64_t qd = t >> 3; qd < nq; qd += CTH / 8) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-      for (int r = rg; r < nr; r += 8) {
-        const uint32_t xw = *reinterpret_cast<const uint32_t*>(c.gs + (int64_t)rowp[r] * c.gs_row + nTp + 4 * qd);
-        const double br = bsh[tr][r];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] += (double)((xw >> (8 * j)) & 0xff) * br;
-      }
+      double acc[4];
+      pred_share(c.gs, c.gs_row, rowp, bsh[tr], nr, nTp + 4 * qd, rg, acc);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        acc[j] += __shfl_xor(acc[j], 1);
-        acc[j] += __shfl_xor(acc[j], 2);
-        acc[j] += __shfl_xor(acc[j], 4);
         const int64_t v = 4 * qd + j;
         if (rg == 0 && v < nV) {
-          eown[tr * nV + v] = acc[j];
+          eall[tr * nV + v] = acc[j];
           if (J > 0) cstore(ch.epart + ((b * NT + J) * NTR + tr) * nV + v, acc[j]);
         }
       }
     }
-  // and of sum_a s_a beta_a (the train-centring term)
-  double mb[NTR];
-#pragma unroll
-  for (int tr = 0; tr < NTR; ++tr) {
     const double m = t < nr ? c.u[b * c.sd.prow + (int64_t)J * TILE + t] * bsh[tr][t] : 0.0;
-    mb[tr] = block_sum<CTH>(m, red);
+    mb[tr] = block_sum<PCTH>(m, red);
     if (J > 0 && t == 0) cstore(ch.mbpart + (b * NT + J) * NTR + tr, mb[tr]);
   }
   if (J > 0) {
@@ -595,16 +559,31 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
       if (t == 0) fit[b] = __builtin_nan("");
       return;
     }
-  chain_final<NTR>(ch.epart + b * NT * NTR * nV, ch.mbpart + b * NT * NTR, mb, NT, nV, sc[SC_MUF] != 0.0,
-                   sc[SC_SM], sc[SC_BAD] != 0.0, c.ymu, c.yV, eall, red, fit + b,
-                   ebv != nullptr ? ebv + b * NTR * nV : nullptr);
+  const double muf = sc[SC_MUF];
+  double fsum = 0.0;
+  for (int tr = 0; tr < NTR; ++tr) {
+    double mbt = mb[tr];
+    for (int K = 1; K < NT; ++K) mbt += cload(ch.mbpart + (b * NT + K) * NTR + tr);
+    const double MB = mbt * sc[SC_SM], mu = muf * c.ymu[tr];
+    double* e = eall + tr * nV;
+    for (int64_t v = t; v < nV; v += CTH) {
+      double acc = e[v];
+      for (int K = 1; K < NT; ++K) acc += cload(ch.epart + ((b * NT + K) * NTR + tr) * nV + v);
+      e[v] = acc - MB + mu;
+    }
+    __syncthreads();
+    fsum += pearson_abs<PCTH>(e, c.yV + tr * nV, nV, red);
+    if (ebv != nullptr)
+      for (int64_t v = t; v < nV; v += CTH) ebv[(b * NTR + tr) * nV + v] = e[v];
+  }
+  if (t == 0) fit[b] = sc[SC_BAD] != 0.0 ? __builtin_nan("") : (NTR == 1) ? fsum : fsum / (double)NTR;
   tr_.done(WGT_SROW, J, 1, b);
 }
 
 template <int NTR>
-__global__ __launch_bounds__(CTH, NTR <= 2 ? 8 : 4) void k_solve_chain(CholLaunch c, SolveChain ch, double* __restrict__ fit,
+__global__ __launch_bounds__(CTH) void k_solve_chain(CholLaunch c, SolveChain ch, double* __restrict__ fit,
                                                      double* __restrict__ ebv) {
-  extern __shared__ double eall[];   // [NTR][nV]
+  extern __shared__ double eall[];   // [NTR][nV]: the block's prediction share, then (F(b, 0)) the EBVs
   __shared__ double bsh[NTR][TILE];
   __shared__ int sh;
   const int NT = c.sd.NT;
