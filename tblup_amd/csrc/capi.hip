@@ -238,9 +238,10 @@ bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
   return false;
 }
 
-// SNP-form solve: the chained kernel below CHAIN_MAX_B individuals (measured: faster at 32 / 128,
-// slower at 256, where one workgroup per individual already streams L at the HBM rate)
-constexpr int64_t CHAIN_MAX_B = 192;
+// SNP-form solve: the chained kernel up to CHAIN_MAX_B individuals (measured at config 2: solve
+// 0.175 -> 0.078 ms at B = 32, 0.184 -> 0.102 at 64, 0.199 -> 0.166 at 128, even at 192, 0.238 ->
+// 0.305 at 256, where one workgroup per individual already streams L at the HBM rate)
+constexpr int64_t CHAIN_MAX_B = 160;
 bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B) {
   return sd.form == FORM_PRIMAL && (c->solve_chain == 1 || (c->solve_chain < 0 && B <= CHAIN_MAX_B));
 }

@@ -45,6 +45,29 @@ __device__ __forceinline__ double block_max(double v, double* red) {
   return s;
 }
 
+// N sums (max: N maxima) in one pass: each component reduced exactly as block_sum / block_max
+// reduce it alone (red: N x 16 slots)
+template <int NTH_, int N, bool MAX>
+__device__ __forceinline__ void block_reduce(double (&v)[N], double* red) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] = MAX ? fmax(v[k], __shfl_xor(v[k], o)) : v[k] + __shfl_xor(v[k], o);
+  __syncthreads();
+  if (l == 0)
+#pragma unroll
+    for (int k = 0; k < N; ++k) red[k * 16 + w] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    double s = MAX ? red[k * 16] : 0.0;
+#pragma unroll
+    for (int i = MAX ? 1 : 0; i < NTH_ / 64; ++i) s = MAX ? fmax(s, red[k * 16 + i]) : s + red[k * 16 + i];
+    v[k] = s;
+  }
+}
+
 }  // namespace
 
 // (NTH_ may be below the block size: the threads past it hold no elements; red needs a slot per wave)
@@ -52,35 +75,37 @@ template <int NTH_ = NTH>
 __device__ __forceinline__ double pearson_abs(const double* e, const double* yV, int64_t nV, double* red) {
   const int t = threadIdx.x < NTH_ ? (int)threadIdx.x : (int)nV;
   const double yb = yV[0], eb = e[0];
-  double sx = 0.0, sy = 0.0, ncx = 0.0, ncy = 0.0;
+  // red: 4 x 16 slots; four reductions (sums and non-constant counts, maxima, squares, products)
+  double m4[4] = {0.0, 0.0, 0.0, 0.0};   // sx, sy, ncx, ncy
   for (int64_t v = t; v < nV; v += NTH_) {
-    sx += e[v];
-    sy += yV[v];
-    ncx += (e[v] != eb) ? 1.0 : 0.0;
-    ncy += (yV[v] != yb) ? 1.0 : 0.0;
+    m4[0] += e[v];
+    m4[1] += yV[v];
+    m4[2] += (e[v] != eb) ? 1.0 : 0.0;
+    m4[3] += (yV[v] != yb) ? 1.0 : 0.0;
   }
-  const double mx = block_sum<NTH_>(sx, red) / (double)nV;
-  const double my = block_sum<NTH_>(sy, red) / (double)nV;
-  const double nonconst_x = block_sum<NTH_>(ncx, red);
-  const double nonconst_y = block_sum<NTH_>(ncy, red);
-  double ax = 0.0, ay = 0.0;
+  block_reduce<NTH_, 4, false>(m4, red);
+  const double mx = m4[0] / (double)nV, my = m4[1] / (double)nV;
+  const double nonconst_x = m4[2], nonconst_y = m4[3];
+  double a2[2] = {0.0, 0.0};
   for (int64_t v = t; v < nV; v += NTH_) {
-    ax = fmax(ax, fabs(e[v] - mx));
-    ay = fmax(ay, fabs(yV[v] - my));
+    a2[0] = fmax(a2[0], fabs(e[v] - mx));
+    a2[1] = fmax(a2[1], fabs(yV[v] - my));
   }
-  const double xmax = block_max<NTH_>(ax, red);
-  const double ymax = block_max<NTH_>(ay, red);
-  double qx = 0.0, qy = 0.0;
+  block_reduce<NTH_, 2, true>(a2, red);
+  const double xmax = a2[0], ymax = a2[1];
+  double q2[2] = {0.0, 0.0};
   for (int64_t v = t; v < nV; v += NTH_) {
     const double a = (e[v] - mx) / xmax, c = (yV[v] - my) / ymax;
-    qx += a * a;
-    qy += c * c;
+    q2[0] = __builtin_fma(a, a, q2[0]);
+    q2[1] = __builtin_fma(c, c, q2[1]);
   }
-  const double nx = xmax * sqrt(block_sum<NTH_>(qx, red));
-  const double ny = ymax * sqrt(block_sum<NTH_>(qy, red));
-  double rr = 0.0;
-  for (int64_t v = t; v < nV; v += NTH_) rr += ((e[v] - mx) / nx) * ((yV[v] - my) / ny);
-  double r = block_sum<NTH_>(rr, red);
+  block_reduce<NTH_, 2, false>(q2, red);
+  const double nx = xmax * sqrt(q2[0]);
+  const double ny = ymax * sqrt(q2[1]);
+  double r1[1] = {0.0};
+  for (int64_t v = t; v < nV; v += NTH_) r1[0] = __builtin_fma((e[v] - mx) / nx, (yV[v] - my) / ny, r1[0]);
+  block_reduce<NTH_, 1, false>(r1, red);
+  double r = r1[0];
   if (r == r) r = fmin(fmax(r, -1.0), 1.0);  // np.clip keeps NaN (fmin/fmax would drop it)
   if (nonconst_x == 0.0 || nonconst_y == 0.0) r = __builtin_nan("");
   if (nV == 2) r = rint(r);
@@ -174,7 +199,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   __shared__ double part[NTH / 64][2 * TILE];   // reused as [64][64]
   __shared__ double vsh[MAXT][TILE];
   __shared__ double wblk[KBLK];
-  __shared__ double red[NTH / 64];
+  __shared__ double red[4 * 16];
   const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, ns = c.sd.ns, prow = c.sd.prow;
   const int NT = c.sd.NT;
   constexpr int nt = NTR;
@@ -484,7 +509,7 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   __shared__ double vsh[NTR][TILE];
   __shared__ double bsh[NTR][TILE];
   __shared__ int32_t rowp[TILE];
-  __shared__ double red[CTH / 64];
+  __shared__ double red[4 * 16];
   const int t = threadIdx.x;
   const int NT = c.sd.NT;
   const int64_t ns = c.sd.ns, nV = c.d.nV, nTp = c.d.nTp;
