@@ -171,26 +171,34 @@ __device__ __forceinline__ void xrow_apply(const v2d (&xr)[8], bool ok, int row,
   }
 }
 
-// block J's share of the SNP-form prediction for animals 4 qd .. 4 qd + 3: sum over the block's
-// rows r = rg, rg + 8, .. < nr of x_va beta_r (int8 split rows, V animals from byte nTp), then
-// xor-reduced over the 8 row groups
-__device__ __forceinline__ void pred_share(const int8_t* gs, int64_t gs_row, const int32_t* rowp, const double* br,
-                                           int nr, int64_t off, int rg, double (&acc)[4]) {
+// block J's share of the SNP-form prediction for animals 4 qd .. 4 qd + 3, every trait: sum over
+// the block's rows r = rg, rg + 8, .. < nr of x_va beta_r (int8 split rows, V animals from byte
+// nTp; beta[tr * bstride + r]), then xor-reduced over the 8 row groups
+template <int NTR>
+__device__ __forceinline__ void pred_share(const int8_t* gs, int64_t gs_row, const int32_t* rowp, const double* beta,
+                                           int64_t bstride, int nr, int64_t off, int rg, double (&acc)[NTR][4]) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = 0.0;
+  for (int tr = 0; tr < NTR; ++tr)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[tr][j] = 0.0;
 #pragma unroll 4
   for (int r = rg; r < nr; r += 8) {
     const uint32_t xw = *reinterpret_cast<const uint32_t*>(gs + (int64_t)rowp[r] * gs_row + off);
-    const double bv = br[r];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = __builtin_fma((double)((xw >> (8 * j)) & 0xff), bv, acc[j]);
+    for (int tr = 0; tr < NTR; ++tr) {
+      const double bv = beta[tr * bstride + r];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[tr][j] = __builtin_fma((double)((xw >> (8 * j)) & 0xff), bv, acc[tr][j]);
+    }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    acc[j] += __shfl_xor(acc[j], 1);
-    acc[j] += __shfl_xor(acc[j], 2);
-    acc[j] += __shfl_xor(acc[j], 4);
-  }
+  for (int tr = 0; tr < NTR; ++tr)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[tr][j] += __shfl_xor(acc[tr][j], 1);
+      acc[tr][j] += __shfl_xor(acc[tr][j], 2);
+      acc[tr][j] += __shfl_xor(acc[tr][j], 4);
+    }
 }
 
 template <int NTR>
@@ -274,37 +282,50 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   const int dq = t & 15, rg = t >> 4;   // dword (4 bytes) within a 64-wide block row, row group (64)
   double* pw = &part[0][0];             // [64 row groups][64]
   double fsum = 0.0;
+  if (c.sd.form == FORM_PRIMAL) {
+    // EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu with block J's shares e_J[v] = sum_{a in J}
+    // x_va beta_a and mb_J = sum_{a in J} s_a beta_a, J ascending (the chained solve's order),
+    // every trait in one pass over the rows
+    const int64_t kk = (int64_t)sc[SC_K];
+    const int rg8 = t & 7;
+    const int64_t nq = (nV + 3) / 4;
+    double mbt[NTR];
+    for (int J = 0; J < NT; ++J) {
+      const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));
+      for (int64_t qd = t >> 3; qd < ((c.skip & 2048) ? 0 : nq); qd += NTH / 8) {
+        double acc[NTR][4];
+        pred_share<NTR>(c.gs, c.gs_row, rowp + J * TILE, alpha + J * TILE, ns, nr, nTp + 4 * qd, rg8, acc);
+#pragma unroll
+        for (int tr = 0; tr < NTR; ++tr)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t v = 4 * qd + j;
+            if (rg8 == 0 && v < nV) eall[tr * nV + v] = (J == 0) ? acc[tr][j] : eall[tr * nV + v] + acc[tr][j];
+          }
+      }
+      double m[NTR];
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr)
+        m[tr] = (t < nr && t < PCTH) ? ub[(int64_t)J * TILE + t] * alpha[tr * ns + (int64_t)J * TILE + t] : 0.0;
+      block_reduce<PCTH, NTR, false>(m, red);
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr) mbt[tr] = (J == 0) ? m[tr] : mbt[tr] + m[tr];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr) {
+      const double MB = mbt[tr] * sc[SC_SM], mu = muf * c.ymu[tr];
+      for (int64_t v = t; v < nV; v += NTH) eall[tr * nV + v] = eall[tr * nV + v] - MB + mu;
+    }
+    __syncthreads();
+  }
   for (int tr = 0; tr < nt; ++tr) {
     const double* al = alpha + tr * ns;
     double* e = eall + tr * nV;
     const double* yV = c.yV + tr * nV;
     const double mu = muf * c.ymu[tr];
     if (c.sd.form == FORM_PRIMAL) {
-      // EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu with block J's shares e_J[v] = sum_{a in J}
-      // x_va beta_a and mb_J = sum_{a in J} s_a beta_a, J ascending (the chained solve's order)
-      const int64_t kk = (int64_t)sc[SC_K];
-      const int rg = t & 7;
-      const int64_t nq = (nV + 3) / 4;
-      double mbt = 0.0;
-      for (int J = 0; J < NT; ++J) {
-        const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));
-        for (int64_t qd = t >> 3; qd < ((c.skip & 2048) ? 0 : nq); qd += NTH / 8) {
-          double acc[4];
-          pred_share(c.gs, c.gs_row, rowp + J * TILE, al + J * TILE, nr, nTp + 4 * qd, rg, acc);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int64_t v = 4 * qd + j;
-            if (rg == 0 && v < nV) e[v] = (J == 0) ? acc[j] : e[v] + acc[j];
-          }
-        }
-        const double m = t < nr ? ub[(int64_t)J * TILE + t] * al[(int64_t)J * TILE + t] : 0.0;
-        const double mbj = block_sum<PCTH>(t < PCTH ? m : 0.0, red);
-        mbt = (J == 0) ? mbj : mbt + mbj;
-      }
-      __syncthreads();
-      const double MB = mbt * sc[SC_SM];
-      for (int64_t v = t; v < nV; v += NTH) e[v] = e[v] - MB + mu;
-      __syncthreads();
+      // (the EBVs above)
     } else {
       // EBV_V = K_VT alpha + mu without materialising K_VT (exact-integer factored form):
       //   sum_t K_vt alpha_t = [sum_s a_vs w_s - u_v S/N - (u_T . alpha)/N + cN S] / d,
@@ -552,27 +573,30 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   }
   chain_publish(flag_beta(ch, b, NT, J), ch.seq, ch.mode);
 
-  // block J's share of the prediction and of the centring term
+  // block J's share of the prediction and of the centring term, every trait in one pass
   const int rg = t & 7;
   const int64_t nq = (nV + 3) / 4;
-  double mb[NTR];
-  for (int tr = 0; tr < NTR; ++tr) {
-    for (int64_t qd = t >> 3; qd < nq; qd += CTH / 8) {
-      double acc[4];
-      pred_share(c.gs, c.gs_row, rowp, bsh[tr], nr, nTp + 4 * qd, rg, acc);
+  for (int64_t qd = t >> 3; qd < nq; qd += CTH / 8) {
+    double acc[NTR][4];
+    pred_share<NTR>(c.gs, c.gs_row, rowp, &bsh[0][0], TILE, nr, nTp + 4 * qd, rg, acc);
+#pragma unroll
+    for (int tr = 0; tr < NTR; ++tr)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t v = 4 * qd + j;
         if (rg == 0 && v < nV) {
-          eall[tr * nV + v] = acc[j];
-          if (J > 0) cstore(ch.epart + ((b * NT + J) * NTR + tr) * nV + v, acc[j]);
+          eall[tr * nV + v] = acc[tr][j];
+          if (J > 0) cstore(ch.epart + ((b * NT + J) * NTR + tr) * nV + v, acc[tr][j]);
         }
       }
-    }
-    const double m = t < nr ? c.u[b * c.sd.prow + (int64_t)J * TILE + t] * bsh[tr][t] : 0.0;
-    mb[tr] = block_sum<PCTH>(m, red);
-    if (J > 0 && t == 0) cstore(ch.mbpart + (b * NT + J) * NTR + tr, mb[tr]);
   }
+  double mb[NTR];
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr) mb[tr] = t < nr ? c.u[b * c.sd.prow + (int64_t)J * TILE + t] * bsh[tr][t] : 0.0;
+  block_reduce<PCTH, NTR, false>(mb, red);
+#pragma unroll
+  for (int tr = 0; tr < NTR; ++tr)
+    if (J > 0 && t == 0) cstore(ch.mbpart + (b * NT + J) * NTR + tr, mb[tr]);
   if (J > 0) {
     chain_publish(flag_e(ch, b, NT, J), ch.seq, ch.mode);
     tr_.done(WGT_SROW, J, 0, b);

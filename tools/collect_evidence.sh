@@ -22,5 +22,5 @@ cp $O/wg_trace_$T.txt $P/${T}_wg_trace.txt
 cp $O/wg_trace128_$T.txt $P/${T}_wg_trace_pop128.txt
 cp $O/mfma_peak_$T.json $P/${T}_mfma_peak.json
 cp $O/fp4_probe_$T.json $P/${T}_fp4_probe.json
-cp $O/gputest_r03.log $P/${T}_gputest.log 2>/dev/null || true
+cp $O/gputest_$T.log $P/${T}_gputest.log 2>/dev/null || true
 ls -la $P | grep $T

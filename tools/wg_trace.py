@@ -17,7 +17,7 @@ os.environ["TBLUP_WG_TRACE"] = "1"
 
 import bench  # noqa: E402
 
-KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part"}
+KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part"}   # (7 / 8: chained solve, tools/solve_trace.py)
 
 
 def main():
@@ -38,6 +38,7 @@ def main():
     torch.cuda.synchronize()
     rec = eng.wg_trace()
     raw = eng.wg_trace(raw=True)
+    rec = rec[rec["kind"] <= 6]
     np.save(out, rec)
     np.save(out.replace(".npy", "_raw.npy"), raw)
     props = torch.cuda.get_device_properties(0)
