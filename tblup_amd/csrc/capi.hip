@@ -225,6 +225,10 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
     const double cap = std::max(per_slot, tw);
     p.nrs = nrs_pol > 0 ? nrs_pol : (jt <= cap ? 1 : jt / 2.0 <= cap ? 2 : 4);
     p.nds = dt * ((0.5 * jt <= cap && nrs_pol <= 1) ? 1 : 2);
+  } else if (dt && 0.5 * J > (p.ahead_cur ? 1.0 : (double)J) + 0.5) {
+    // after an ahead launch the T-units add one term: a whole D-unit (J / 2 GEMM units) would
+    // outlast them and bound the launch (pop 128, launch 6: D 83 us vs T 39 us)
+    p.nds = 2;
   }
   p.n_kd = (J == 0 && NT > 2 && !st) ? B * (NT - 2) : 0;
   return p;
