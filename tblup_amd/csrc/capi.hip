@@ -199,6 +199,26 @@ bool sys_tiles(const EvalDims& d, const SysDims& sd) {
 
 }  // namespace
 
+// Makespan of greedy list scheduling, in order, of classes {duration, count} on `slots` identical
+// slots (slot free times kept as {time: free slots} groups).
+static double list_makespan(std::initializer_list<std::pair<double, int64_t>> classes, int64_t slots) {
+  std::map<double, int64_t> fr{{0.0, slots}};
+  double end = 0.0;
+  for (const auto& cl : classes) {
+    int64_t n = cl.second;
+    while (n > 0) {
+      auto it = fr.begin();
+      const double t = it->first;
+      const int64_t use = std::min(n, it->second);
+      if ((it->second -= use) == 0) fr.erase(it);
+      fr[t + cl.first] += use;
+      end = std::max(end, t + cl.first);
+      n -= use;
+    }
+  }
+  return end;
+}
+
 OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol) {
   OffPlan p{};
   p.nI = NT - J - 1;
@@ -217,18 +237,33 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   const int dt = (J >= 1 && J + 1 < NT) ? 1 : 0;   // diagonal target J + 1 (its partial over L < J)
   p.nrs = 1;
   p.nds = dt;
-  if (p.nP > 0 && st) {   // row slices need k_sys_tiles' counts (the int8 K is a whole-tile product)
-    // unit work in 2*128^3-flop GEMM units: T-unit 1 + 0.5 (GEMM2), P-unit J / nrs, D-unit J / 2 / nds;
-    // slice until no P- or D-unit is longer than a T-unit or the launch's work per slot (two per CU)
-    const double jt = J, tw = 1.5;
-    const double per_slot = (double)B * (p.nI * tw + p.nP * jt + 0.5 * jt) / 512.0;
-    const double cap = std::max(per_slot, tw);
-    p.nrs = nrs_pol > 0 ? nrs_pol : (jt <= cap ? 1 : jt / 2.0 <= cap ? 2 : 4);
-    p.nds = dt * ((0.5 * jt <= cap && nrs_pol <= 1) ? 1 : 2);
-  } else if (dt && 0.5 * J > (p.ahead_cur ? 1.0 : (double)J) + 0.5) {
-    // after an ahead launch the T-units add one term: a whole D-unit (J / 2 GEMM units) would
-    // outlast them and bound the launch (pop 128, launch 6: D 83 us vs T 39 us)
-    p.nds = 2;
+  // Row slices of the P-units (they need k_sys_tiles' counts: the int8 K is a whole-tile
+  // product) and block slices of the D-unit: the pair whose greedy list schedule -- grid order
+  // P, D, T on 512 slots (two workgroups per CU), unit work in 2*128^3-flop GEMM units plus a
+  // fixed 0.25 -- ends first (ties: fewer units).  T-unit: the GEMM1 terms it still sums (1 after
+  // an ahead launch, else J) + 0.5 (GEMM2); P-unit: J / nrs; D-unit: J / 2 / nds.
+  // A slicing other than (1, 1) must gain 10%: the model ignores that tiles sharing a CU with
+  // tiles (not with the lighter D-units) slow each other down (round 2: D split in two at pop 256
+  // measured slower although such a model predicted -90 us).
+  const double jt = J, tw = (p.ahead_cur ? 1.0 : jt) + 0.5, c0 = 0.25;
+  const int64_t nT = B * p.nI;
+  auto span = [&](int nrs, int nds) {
+    return list_makespan({{c0 + jt / nrs, B * p.nP * nrs}, {c0 + 0.5 * jt / nds, B * dt * nds}, {c0 + tw, nT}}, 512);
+  };
+  const bool slice_p = p.nP > 0 && st;
+  double best = (nrs_pol > 1 && slice_p) ? 1e300 : 0.9 * span(1, 1);
+  for (int nrs : {1, 2, 4}) {
+    if (nrs > 1 && !slice_p) break;
+    if (nrs_pol > 0 && nrs != nrs_pol && slice_p) continue;
+    for (int nds = 1; nds <= (dt ? 2 : 1); ++nds) {
+      if (nrs == 1 && nds == 1) continue;
+      const double ms = span(nrs, nds);
+      if (ms < best) {
+        best = ms;
+        p.nrs = slice_p ? nrs : 1;
+        p.nds = dt * nds;
+      }
+    }
   }
   p.n_kd = (J == 0 && NT > 2 && !st) ? B * (NT - 2) : 0;
   return p;
