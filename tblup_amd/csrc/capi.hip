@@ -101,6 +101,7 @@ struct tblup_ctx {
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
+  int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (B <= LT_MAX_B), 0 never, 1 always (see use_last_term)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
   DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
@@ -285,6 +286,17 @@ bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B) {
   return sd.form == FORM_PRIMAL && (c->solve_chain == 1 || (c->solve_chain < 0 && B <= CHAIN_MAX_B));
 }
 
+// Last-term mode: the diagonal tile's last SYRK term computed by the previous launch's tile
+// (J, J-1) workgroup (dispatched first) instead of inside the diagonal launch, where one
+// workgroup per individual runs it on one CU.  Bit-identical either way.  Measured (config 2,
+// A/B): the diagonal launches lose ~8 us each at every B (0.349 -> 0.282 ms per step at B = 32,
+// 0.394 -> 0.331 at 256) but the off-diagonal launches gain 42 (B = 32) to 97 us (256): +3.3% at
+// 32, +2.0% at 64, -1.3% at 128, -1% at 192 and 256.
+constexpr int64_t LT_MAX_B = 64;
+bool use_last_term(const tblup_ctx* c, const SysDims& sd, int64_t B) {
+  return sd.NT >= 2 && (c->last_term == 1 || (c->last_term < 0 && B <= LT_MAX_B));
+}
+
 size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k,
                    bool with_ebv) {
   size_t s = 0;
@@ -307,6 +319,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
     add((size_t)B * sd.NT * d.nt * d.nV * 8);
     add((size_t)B * sd.NT * d.nt * 8);
   }
+  add(use_last_term(c, sd, B) ? (size_t)B * NPACK * BLKD * 8 : 0);   // diagonal tiles' last SYRK terms
   add((size_t)B * 8);                                           // fitness
   add(with_ebv ? (size_t)B * d.nt * d.nV * 8 : 0);              // ebv
   add((size_t)sum_k * 8 + (size_t)(B + 1) * 8);                 // idx, off
@@ -390,6 +403,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const bool use_st = sys_tiles(d, sd) && stop_stage != 1;
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
   double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
+  double* Qb = use_last_term(c, sd, B) ? cv.take<double>((size_t)B * NPACK * BLKD) : nullptr;
   std::vector<OffPlan> plan(sd.NT);
   for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
@@ -421,7 +435,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
                 (const double*)sp.ymu.p, panel, pstride, d_off,
                 (const int8_t*)sp.geno.p, d_idx, d.nRp, (const uint8_t*)sp.gpk.p, d.nRp / 4, u, scal,
-                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb, Pp};
+                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb, Pp, Qb};
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
@@ -465,8 +479,9 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     const OffPlan& p = plan[J];
     // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
     // forward-substitution GEMV (the exact system tiles are counted under KC_GRM)
-    const double fd = Bd * (T3 * std::min(jt, 1.0) + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
-    const double bd = Bd * (TILE * TILE * std::min(jt, 1.0) * 8.0 + 2.0 * TILE * TILE * 8.0);
+    const double lt_d = Qb ? 0.0 : std::min(jt, 1.0);   // the last SYRK term's share of this launch
+    const double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
+    const double bd = Bd * (TILE * TILE * lt_d * 8.0 + 2.0 * TILE * TILE * 8.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
       c->wgt_used += B + DTR_RECS;
@@ -478,7 +493,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       // P-units: 2*128^3 per L < J; D-unit: 128^3 per L < J (lower half); the fused int8 GRM
       // tiles' int-ops are excluded
       const double lt = p.ahead_cur ? 1.0 : jt;
-      const double fo = Bd * p.nI * (2.0 * T3 * lt + T3) + Bd * p.nP * 2.0 * T3 * jt + (p.nds ? Bd * T3 * jt : 0.0);
+      const double fo = Bd * p.nI * (2.0 * T3 * lt + T3) + Bd * p.nP * 2.0 * T3 * jt + (p.nds ? Bd * T3 * jt : 0.0) +
+                        (Qb ? Bd * T3 : 0.0);
       const double bo = Bd * p.nI * (TILE * TILE * lt * 8.0 + TILE * TILE * 8.0) +
                         Bd * p.nP * (2.0 * TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) +
                         (p.nds ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
@@ -580,6 +596,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_AHEAD")) c->ahead = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_SOLVE_CHAIN")) c->solve_chain = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_CHAIN_SYNC")) c->chain_sync = atoi(e);
+  if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
   if (!panel) {
     *out = c.release();

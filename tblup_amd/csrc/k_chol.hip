@@ -264,6 +264,7 @@ struct CholArgs {
   uint64_t* dtr;            // diagonal launch: phase timestamps of workgroup 0 (TBLUP_WG_TRACE), else null
   const int16_t* kc;        // SNP form: off-diagonal system-tile counts (k_sys_tiles), else null
   double* part;             // [2][B][NT][128*128] off-diagonal partial sums K - sum_{L<J-1} (acc layout), slot J&1
+  double* q;                // last-term mode: [B][NPACK*BLKD] L_{J,J-1} L_{J,J-1}^T, from launch J-1's tile (J, J-1)
   int64_t B;                // individuals in the chunk
 };
 
@@ -791,7 +792,19 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       const int chunk = (e * DW + w) * 64;
       __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
     }
-    if (J > L0 && !(a.skip & 2)) {
+    if (J > L0 && a.q != nullptr) {
+      // last-term mode: Q = L_{J,J-1} L_{J,J-1}^T came with launch J-1's tile (J, J-1)
+      const double* qg = a.q + b * (int64_t)NPACK * BLKD;
+#pragma unroll
+      for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {
+        const int chunk = (e * DW + w) * 64;
+        __builtin_amdgcn_global_load_lds(qg + 2 * (chunk + l), (lds_ptr_t)(Xp + 2 * chunk), 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int e = t; e < NPACK * BLKD; e += DTHR) Tp[e] -= Xp[e];
+      __syncthreads();
+    } else if (J > L0 && !(a.skip & 2)) {
       v4d acc[5];
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
@@ -1152,6 +1165,18 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
       }
     }
   }
+  // last-term mode: the diagonal tile J+1's last SYRK term L_{J+1,J} L_{J+1,J}^T from the tile
+  // just stored (read back through the same stage ring and MFMA chains the diagonal kernel would
+  // run, so its T = S - Q is bit-identical)
+  if (a.q != nullptr && I == J + 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    v4d qa[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) qa[i] = v4d{0.0, 0.0, 0.0, 0.0};
+    syrk_lower8_32(Lout, 8, lds, qa);
+    store_syrk_blocks(a.q + b * (int64_t)NPACK * BLKD, nullptr, qa, 0);
+  }
 }
 
 // K_JJ for every (individual, J) with the off-diagonal kernel's 8-wave int8 tile (A = B =
@@ -1265,9 +1290,22 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
   }
   bid -= n_d;
   if (bid < n_t) {
-    const int64_t lg = xcd_remap(bid, n_t);
-    const int64_t b = lg / p.nI;
-    const int I = a.J + 1 + (int)(lg % p.nI);
+    int64_t b;
+    int I;
+    if (a.q != nullptr) {   // last-term mode: the B tiles (J+1, J) first, then the rest
+      if (bid < a.B) {
+        b = xcd_remap(bid, a.B);
+        I = a.J + 1;
+      } else {
+        const int64_t lg = xcd_remap(bid - a.B, n_t - a.B);
+        b = lg / (p.nI - 1);
+        I = a.J + 2 + (int)(lg % (p.nI - 1));
+      }
+    } else {
+      const int64_t lg = xcd_remap(bid, n_t);
+      b = lg / p.nI;
+      I = a.J + 1 + (int)(lg % p.nI);
+    }
     tile_unit(a, b, I, p.ahead_cur, lds, uj_sh, ui_sh, zj_sh);
     tr.done(WGT_TILE, a.J, I, b);
     return;
@@ -1447,7 +1485,7 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
-             c.wgt, nullptr, c.kc, c.part, c.B};
+             c.wgt, nullptr, c.kc, c.part, c.q, c.B};
   return a;
 }
 

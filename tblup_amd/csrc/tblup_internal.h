@@ -151,6 +151,7 @@ struct CholLaunch {
   uint64_t* wgt;         // per-workgroup timestamp records of this launch (env TBLUP_WG_TRACE), else null
   int16_t* kc;           // SNP form: exact off-diagonal system-tile counts from k_sys_tiles, else null
   double* part;          // [2][B][NT][128*128] partial sums of the next column's tiles (ahead schedule)
+  double* q;             // last-term mode: [B][36*256] diagonal tile J's last SYRK term, from launch J-1
 };
 // k_sys_tiles output: per individual NT(NT-1)/2 off-diagonal tiles (I > J, t = I(I-1)/2 + J) of
 // 128 x 128 int16 counts, in the order the off-diagonal kernel's lanes read them:

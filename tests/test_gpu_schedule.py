@@ -1,11 +1,13 @@
 """Cholesky schedule invariance: the classic column schedule and the ahead schedule (partial sums
 of the next column's tiles computed one launch early, in 1 / 2 / 4 row slices, the diagonal
 target's in 1 / 2 block slices) redistribute the same MFMA chains over workgroups and launches,
-and the two solve kernels (k_solve: one workgroup per individual; k_solve_chain: an individual's
-block rows and tiles over the chip, chosen for small batches) share one arithmetic, so fitness
+the two solve kernels (k_solve: one workgroup per individual; k_solve_chain: an individual's
+block rows and tiles over the chip, chosen for small batches) share one arithmetic, and the
+diagonal tile's last SYRK term runs the same MFMA chains whether the diagonal launch or the
+previous launch's tile (J, J-1) workgroup computes it, so fitness
 and EBVs must be bit-identical under every setting, for both system forms and for system sizes
-from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS / TBLUP_SOLVE_CHAIN
-are read when a context is created.)"""
+from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS / TBLUP_SOLVE_CHAIN /
+TBLUP_LAST_TERM are read when a context is created.)"""
 import os
 
 import numpy as np
@@ -24,6 +26,8 @@ SETTINGS = [
     {"TBLUP_AHEAD": "-1", "TBLUP_NRS": "0"},        # the defaults
     {"TBLUP_SOLVE_CHAIN": "1"},                     # SNP form: chained solve at every batch size
     {"TBLUP_SOLVE_CHAIN": "0"},                     # one solve workgroup per individual
+    {"TBLUP_LAST_TERM": "1"},                       # diagonal's last SYRK term in the previous launch
+    {"TBLUP_LAST_TERM": "0"},                       # ... in the diagonal launch
 ]
 
 
@@ -87,7 +91,7 @@ def test_schedules_small_batches_and_traits(panel, gpu):
     for B in (1, 3, 40):
         genomes = [rng.choice(20_000, 1000, replace=False) for _ in range(B)]
         a = _evaluate(panel["geno"], None, genomes, panel["T"], panel["V"], SETTINGS[0], multi=multi)
-        for env in SETTINGS[-3:]:
+        for env in SETTINGS[-5:]:
             b = _evaluate(panel["geno"], None, genomes, panel["T"], panel["V"], env, multi=multi)
             np.testing.assert_array_equal(a[0], b[0], err_msg=str(env))
             np.testing.assert_array_equal(a[1], b[1], err_msg=str(env))
