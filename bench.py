@@ -42,7 +42,8 @@ TRAITS = {"config5": 3}
 # BASELINE.json's metric, verbatim
 METRIC = "GBLUP fitness evals/sec (whole node), 2k\u00d750k SNP, DE pop=256; 1/2/4/8 GPUs"
 
-# gfx950 peaks.  "measured": tools/mfma_peak.hip on the box (profiles/r02_mfma_peak.json; the
+# gfx950 peaks.  "measured": tools/mfma_peak.hip on the box (profiles/r02_mfma_peak.json, again
+# profiles/r03c_mfma_peak.json: f64 72.8 TF at 2 waves per SIMD; the
 # microarchitecture guide has no fp64 MFMA row): back-to-back MFMAs on independent accumulators,
 # 2 waves per SIMD, random operands, at the clock the chip holds under that load (~2.36 GHz).
 # "spec": AMD's MI355X dense figures (2.4 GHz).  HBM: the guide's 8 TB/s.
@@ -51,7 +52,7 @@ PEAKS = {
     "fp32_mfma_tflops": 154.6, "fp32_mfma_tflops_spec": 157.3,
     "int8_mfma_tops": 4140.0, "int8_mfma_tops_spec": 5033.0,
     # FP4 16x16x128 (e2m1 A and B, fp32 accumulate): tools/fp4_probe.hip, 4 waves per SIMD
-    # (profiles/r02b_fp4_probe.json); spec: the guide's ~10 PF dense FP4
+    # (profiles/r02b_fp4_probe.json, r03c: 8.73 POPS); spec: the guide's ~10 PF dense FP4
     "fp4_mfma_tops": 8811.0, "fp4_mfma_tops_spec": 10066.0,
     "hbm_gbs": 8000.0,
 }
@@ -347,7 +348,7 @@ def main():
     roofline = {"bound": bound, "kernel": dom, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4), "traffic": traffic, "mfma_busy": mfma_busy,
                 "launches": pd["launches"], "avg_launch_ms": round(pd["ms"] / max(pd["launches"], 1), 4),
-                "peak_source": "measured on the box (tools/mfma_peak.hip, profiles/r02_mfma_peak.json)",
+                "peak_source": "measured on the box (tools/mfma_peak.hip, profiles/r02_mfma_peak.json, r03c_mfma_peak.json)",
                 "peak_spec": peak_spec, "frac_spec": None if peak_spec is None else round(achieved / peak_spec, 4),
                 "flops": "algorithmic: library tile count x (k/ns)^3 = %.4f" % unpad,
                 "step": {"lower_bound_ms": round(step_bound_ms, 4), "system_tiles_ms": round(t_int8 * 1e3, 4),
