@@ -403,7 +403,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 // smaller block ids (F(b, J) on T(b, K > J, J), T(b, J, I) on F(b, J), F(b, 0) on F(b, J > 0)),
 // and each XCD dispatches its share in block-id order, so the waits drain: the waiting unit with
 // the smallest id waits on units that are resident and not waiting.  Waits are bounded
-// (SPIN_MAX polls; one expired wait makes every later wait give up at once).  Every sum has a
+// (SPIN_MAX polls; one expired wait makes every later wait of the same call give up at once).  Every sum has a
 // fixed order, so the results do not depend on B, the timing or the grid.
 // ===========================================================================
 constexpr int CTH = 512;
@@ -467,13 +467,13 @@ __device__ bool chain_wait(const int32_t* f, int32_t seq, int32_t* err, int* sh,
     for (int it = 0;; ++it) {
       const int32_t v = mode == 1 ? __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : cload(f);
       if (v == seq) break;
-      if (it >= SPIN_MAX || cload(err) != 0) {
+      if (it >= SPIN_MAX || cload(err) == seq) {   // this call's waits already expired elsewhere
         ok = 0;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (!ok) cstore(err, 1);
+    if (!ok) cstore(err, seq);   // the call's sequence number: later calls start unaffected
     *sh = ok;
   }
   __syncthreads();

@@ -205,7 +205,7 @@ struct SolveChain {
   double* cpart;    // [B][NT (row I)][NT (tile J)][nt][128]: L_JI^T beta_J
   double* epart;    // [B][NT][nt][nV]: block J's share of X_V beta
   double* mbpart;   // [B][NT][nt]: block J's share of sum_a s_a beta_a
-  int32_t* err;     // a wait gave up (the calls' fitness is then NaN)
+  int32_t* err;     // = seq of a call in which a wait gave up (that call's fitness is then NaN)
   int32_t seq;      // this call's flag value
   int32_t mode;     // TBLUP_CHAIN_SYNC (k_solve.hip)
 };
