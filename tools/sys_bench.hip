@@ -38,8 +38,8 @@ __device__ __forceinline__ void lds_load16(const uint8_t* src, uint8_t* dst) {
 template <int SUB>
 __device__ __forceinline__ int off(int row, int c) { return row * 64 * SUB + 16 * (c ^ ((row >> 2) & (4 * SUB - 1))); }
 
-template <int D, int SUB, int MODE, bool RT = false>
-__global__ __launch_bounds__(256, 2) void k_bench(const uint8_t* __restrict__ tab, const int32_t* __restrict__ idx,
+template <int D, int SUB, int MODE, bool RT = false, int WPE = 2>
+__global__ __launch_bounds__(256, WPE) void k_bench(const uint8_t* __restrict__ tab, const int32_t* __restrict__ idx,
                                                   int ntri, int* out, int16_t* kc, int nsub_rt = NSUB) {
   constexpr int TB = TILE_ * 64 * SUB;
   __shared__ __attribute__((aligned(16))) uint8_t lds[D * 2 * TB];
@@ -142,17 +142,17 @@ __global__ __launch_bounds__(256, 2) void k_bench(const uint8_t* __restrict__ ta
   }
 }
 
-template <int D, int SUB, int MODE, bool RT = false>
+template <int D, int SUB, int MODE, bool RT = false, int WPE = 2>
 void run(const char* name, const uint8_t* tab, const int32_t* idx, int B, int* out, int16_t* kc) {
   const int ntri = 36;
   dim3 g(B * ntri), blk(256);
-  for (int i = 0; i < 3; ++i) k_bench<D, SUB, MODE, RT><<<g, blk>>>(tab, idx, ntri, out, kc, NSUB);
+  for (int i = 0; i < 3; ++i) k_bench<D, SUB, MODE, RT, WPE><<<g, blk>>>(tab, idx, ntri, out, kc, NSUB);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int R = 20;
   hipEventRecord(e0);
-  for (int i = 0; i < R; ++i) k_bench<D, SUB, MODE, RT><<<g, blk>>>(tab, idx, ntri, out, kc, NSUB);
+  for (int i = 0; i < R; ++i) k_bench<D, SUB, MODE, RT, WPE><<<g, blk>>>(tab, idx, ntri, out, kc, NSUB);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -315,6 +315,10 @@ int main(int argc, char** argv) {
   hipMemcpy(idx, h_idx.data(), h_idx.size() * 4, hipMemcpyHostToDevice);
   int16_t* kc;
   hipMalloc(&kc, (size_t)B * 36 * 128 * 128 * 2);
+  run<2, 1, 3, true, 4>("D2 stores, <=128 VGPRs (4 WG/CU)", tab, idx, B, out, kc);
+  run<3, 1, 3, true, 3>("D3 stores, <=168 VGPRs", tab, idx, B, out, kc);
+  run<2, 1, 0, true, 4>("D2 no stores, <=128 VGPRs", tab, idx, B, out, kc);
+  run<3, 1, 0, true, 2>("D3 no stores (ref)", tab, idx, B, out, kc);
   run_persist<3, 0>("persistent", 3, tab, idx, B, out, kc);
   run_persist<3, 1>("persistent + int16 stores", 3, tab, idx, B, out, kc);
   run_persist<4, 1>("persistent D4 + stores", 2, tab, idx, B, out, kc);
