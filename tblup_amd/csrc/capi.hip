@@ -104,6 +104,8 @@ struct tblup_ctx {
   int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (B <= LT_MAX_B), 0 never, 1 always (see use_last_term)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
+  int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
+  std::vector<int64_t> fold_hoff;   // host offsets of the last fold-fused chunk (host-side shapes only)
   DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
   int32_t chain_seq = 0; // flag value of the last chained solve
 };
@@ -376,11 +378,34 @@ SysDims choose_sys(const tblup_ctx* c, const EvalDims& d, const int64_t* h_off, 
   return sd;
 }
 
-// Enqueue the full pipeline for one chunk whose idx/off already sit in device memory.
+// Every buffer carved so far lies inside the workspace (checked before the launches that use
+// them: a sizing mistake fails the call instead of faulting the GPU)
+int ws_check(const tblup_ctx* c, const Carve& cv) {
+  if (cv.base >= (char*)c->ws.p && cv.base + cv.used <= (char*)c->ws.p + c->ws.bytes) return 0;
+  return fail(TBLUP_ERR_STATE, "internal error: workspace carve of " + std::to_string(cv.used) +
+                                   " bytes overruns the " + std::to_string(c->ws.bytes) + "-byte workspace");
+}
+
+FoldTab single_fold(const Split& sp, int64_t B) {
+  FoldTab ft{};
+  ft.bpf = std::max<int64_t>(B, 1);
+  ft.nf = 1;
+  ft.gpk[0] = (const uint8_t*)sp.gpk.p;
+  ft.gs[0] = (const int8_t*)sp.geno.p;
+  ft.csT[0] = (const int32_t*)sp.colsumT.p;
+  ft.xty[0] = (const double*)sp.xty.p;
+  ft.yV[0] = (const double*)sp.yV.p;
+  ft.ymu[0] = (const double*)sp.ymu.p;
+  return ft;
+}
+
+// Enqueue the full pipeline for one chunk whose idx/off already sit in device memory.  ftp: the
+// systems' splits when they are not all sp (fold-fused evaluation; sp is then fold 0).
 int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& sd, hipStream_t s,
               const int64_t* d_idx, const int64_t* d_off, const int64_t* h_off, int64_t B, double h2,
               int branch, Carve& cv, double* d_fit, double* d_ebv, int stop_stage, double** K_out,
-              double** z_out) {
+              double** z_out, const FoldTab* ftp = nullptr) {
+  const FoldTab ft = ftp ? *ftp : single_fold(sp, B);
   double grm_flops = 0.0, gather_bytes = 0.0, stats_bytes = 0.0;
   const double tri = (double)d.nT * (d.nT + 1) / 2.0 + (double)d.nV * d.nT;
   for (int64_t b = 0; b < B; ++b) {
@@ -404,14 +429,14 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
   double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
   double* Qb = use_last_term(c, sd, B) ? cv.take<double>((size_t)B * NPACK * BLKD) : nullptr;
+  if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
   for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
   rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
-    return launch_indiv_stats(d_idx, d_off, B, csT, csA, (const double*)sp.xty.p, d, sd, branch, h2,
-                              scal, u, rhs, (int32_t*)c->idx_err.p, s);
+    return launch_indiv_stats(d_idx, d_off, B, ft, csA, d, sd, branch, h2, scal, u, rhs, (int32_t*)c->idx_err.p, s);
   });
   if (rc) return rc;
   if (sd.form == FORM_DUAL) {
@@ -426,16 +451,16 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     // parity readback only: the full K_{R,T} block of the unified form (k_grm); the
     // production path never materialises K (the Cholesky kernels rebuild each tile)
     double* K = cv.take<double>((size_t)B * d.nRp * d.nTp);
+    if (int rc2 = ws_check(c, cv)) return rc2;
     if (K_out) *K_out = K;
     const double kbytes = (double)B * ((double)d.nT * d.nT / 2.0 + (double)d.nV * d.nT) * 8.0;
     return timed(c, s, KC_GRM, grm_flops, kbytes + gather_bytes / 2.0,
                  [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
   }
   if (K_out) *K_out = L;
-  CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, (const double*)sp.yV.p,
-                (const double*)sp.ymu.p, panel, pstride, d_off,
-                (const int8_t*)sp.geno.p, d_idx, d.nRp, (const uint8_t*)sp.gpk.p, d.nRp / 4, u, scal,
-                c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb, Pp, Qb};
+  CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, panel, pstride, d_off, d_idx,
+                d.nRp, d.nRp / 4, ft, u, scal, c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
+                Pp, Qb};
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
@@ -526,6 +551,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     ch.cpart = cv.take<double>((size_t)B * sd.NT * sd.NT * d.nt * TILE);
     ch.epart = cv.take<double>((size_t)B * sd.NT * d.nt * d.nV);
     ch.mbpart = cv.take<double>((size_t)B * sd.NT * d.nt);
+    if (int rc2 = ws_check(c, cv)) return rc2;
     ch.seq = ++c->chain_seq;
     ch.mode = c->chain_sync;
     chp = &ch;
@@ -597,6 +623,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_SOLVE_CHAIN")) c->solve_chain = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_CHAIN_SYNC")) c->chain_sync = atoi(e);
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
   if (!panel) {
     *out = c.release();
@@ -873,8 +900,67 @@ int tblup_eval_batch_device(tblup_ctx* c, int split_id, const int64_t* d_idx, co
 }
 
 // IntraGCV's k folds (evaluator.py:509-537) or any set of splits: every individual against every
-// split, enqueued back to back on one stream (the folds reuse one workspace in stream order), one
-// host round trip for the whole set instead of one per fold.
+// split in one call, one host round trip for the whole set.  Fold-fused (the default whenever
+// the splits have equal dimensions and the batch takes the SNP form with k_sys_tiles): the
+// F x B systems (s = f * B + b: individual b against split f) run as ONE batch through one
+// launch sequence -- 18 launches instead of 18 F, each filling the chip F times over, the
+// system's split picked per workgroup from the FoldTab.  Otherwise the folds' batches run back to
+// back on one stream, reusing one workspace in stream order.  Results are bit-identical either
+// way (every system's arithmetic is independent of the batch it runs in).
+
+// Fused layout of a chunk: the F splits of equal dimensions in the SNP form with system tiles
+// (otherwise 0).  sd: the common system shape.
+static bool fold_fusable(const tblup_ctx* c, const std::vector<Split*>& sps, const int64_t* h_off, int64_t B,
+                         int branch, SysDims& sd) {
+  const int64_t F = (int64_t)sps.size();
+  if (!c->fold_fuse || F < 2 || F > MAXF || F * B > 65535 || B < 1) return false;
+  for (const Split* sp : sps)
+    if (sp->nT != sps[0]->nT || sp->nV != sps[0]->nV || sp->nTp != sps[0]->nTp || sp->nRp != sps[0]->nRp) return false;
+  const EvalDims d = dims_of(c, *sps[0]);
+  sd = choose_sys(c, d, h_off, B, branch, c->form_pref);
+  return sd.form == FORM_PRIMAL && sys_tiles(d, sd);
+}
+
+// The fused chunk: the index lists replicated per fold (F x sum_k, device to device), the fused
+// offsets built on the device, then run_chunk over F x B systems.
+static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd, hipStream_t s,
+                           const int64_t* d_idx, const int64_t* d_off, const int64_t* h_off, int64_t B, double h2, int branch, Carve& cv,
+                           double* d_fit) {
+  const int64_t F = (int64_t)sps.size(), FB = F * B, sum_k = h_off[B];
+  const EvalDims d = dims_of(c, *sps[0]);
+  int64_t* idx_f = cv.take<int64_t>((size_t)(F * sum_k));
+  int64_t* off_f = cv.take<int64_t>((size_t)FB + 1);
+  std::vector<int64_t>& ho = c->fold_hoff;   // host copy (run_chunk's work accounting and shapes)
+  ho.assign((size_t)FB + 1, 0);
+  for (int64_t f = 0; f < F; ++f)
+    for (int64_t b = 0; b < B; ++b) ho[f * B + b] = f * sum_k + h_off[b];
+  ho[FB] = F * sum_k;
+  for (int64_t f = 0; f < F; ++f)
+    HIPCHK(hipMemcpyAsync(idx_f + f * sum_k, d_idx, (size_t)sum_k * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(launch_fold_offsets(d_off, B, F, sum_k, off_f, s));
+  FoldTab ft{};
+  ft.bpf = B;
+  ft.nf = (int)F;
+  for (int64_t f = 0; f < F; ++f) {
+    ft.gpk[f] = (const uint8_t*)sps[f]->gpk.p;
+    ft.gs[f] = (const int8_t*)sps[f]->geno.p;
+    ft.csT[f] = (const int32_t*)sps[f]->colsumT.p;
+    ft.xty[f] = (const double*)sps[f]->xty.p;
+    ft.yV[f] = (const double*)sps[f]->yV.p;
+    ft.ymu[f] = (const double*)sps[f]->ymu.p;
+  }
+  return run_chunk(c, *sps[0], d, sd, s, idx_f, off_f, ho.data(), FB, h2, branch, cv, d_fit, nullptr, 0, nullptr,
+                   nullptr, &ft);
+}
+
+// workspace of a fused chunk: its replicated index lists included, plus room for the host
+// entry's own copy of the chunk's index list and offsets ahead of it
+static size_t fused_bytes(const tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd, int64_t B,
+                          int64_t sum_k) {
+  const int64_t F = (int64_t)sps.size();
+  return chunk_bytes(c, dims_of(c, *sps[0]), sd, F * B, F * sum_k, false) + (size_t)(sum_k + B + 1) * 8 + 1024;
+}
+
 static int validate_splits(tblup_ctx* c, const int* split_ids, int n_splits, std::vector<Split*>& sps) {
   if (!split_ids || n_splits < 1) return fail(TBLUP_ERR_ARG, "need n_splits >= 1 split ids");
   sps.resize(n_splits);
@@ -898,15 +984,26 @@ int tblup_eval_folds_device(tblup_ctx* c, const int* split_ids, int n_splits, co
   if (batch > 65535) return fail(TBLUP_ERR_ARG, "device batch limited to 65535 individuals per call");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  SysDims fsd{};
+  const bool fused = fold_fusable(c, sps, h_offsets, batch, branch, fsd) &&
+                     fused_bytes(c, sps, fsd, batch, h_offsets[batch]) <= c->budget;
   size_t need = 0;
-  for (int f = 0; f < n_splits; ++f) {
-    const EvalDims d = dims_of(c, *sps[f]);
-    need = std::max(need, chunk_bytes(c, d, choose_sys(c, d, h_offsets, batch, branch, c->form_pref), batch, 0, false));
+  if (fused) {
+    need = fused_bytes(c, sps, fsd, batch, h_offsets[batch]);
+  } else {
+    for (int f = 0; f < n_splits; ++f) {
+      const EvalDims d = dims_of(c, *sps[f]);
+      need = std::max(need, chunk_bytes(c, d, choose_sys(c, d, h_offsets, batch, branch, c->form_pref), batch, 0, false));
+    }
   }
   if (need > c->ws.bytes) {
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (int rc = dev_alloc(c, c->ws, need)) return rc;
+  }
+  if (fused) {
+    Carve cv{(char*)c->ws.p};
+    return run_folds_fused(c, sps, fsd, s, d_idx, d_offsets, h_offsets, batch, h2, branch, cv, d_fitness);
   }
   for (int f = 0; f < n_splits; ++f) {
     const EvalDims d = dims_of(c, *sps[f]);
@@ -936,6 +1033,8 @@ int tblup_eval_folds(tblup_ctx* c, const int* split_ids, int n_splits, const int
     size_t m = 0;
     for (int f = 0; f < n_splits; ++f)
       m = std::max(m, chunk_bytes(c, ds[f], choose_sys(c, ds[f], off, B, branch, c->form_pref), B, sum_k, false));
+    SysDims fsd{};
+    if (fold_fusable(c, sps, off, B, branch, fsd)) m = std::max(m, fused_bytes(c, sps, fsd, B, sum_k));
     return m + (size_t)n_splits * B * 8 + 256;
   };
   int64_t b0 = 0;
@@ -965,12 +1064,19 @@ int tblup_eval_folds(tblup_ctx* c, const int* split_ids, int n_splits, const int
     double* d_fit = head.take<double>((size_t)n_splits * B);
     HIPCHK(hipMemcpyAsync(d_idx, idx + offsets[b0], (size_t)sum_k * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(d_off, hoff.data(), (size_t)(B + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    for (int f = 0; f < n_splits; ++f) {
-      Carve cv = head;   // every fold reuses the same workspace after the inputs, in stream order
-      const SysDims sd = choose_sys(c, ds[f], hoff.data(), B, branch, c->form_pref);
-      if (int rc = run_chunk(c, *sps[f], ds[f], sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv,
-                             d_fit + (int64_t)f * B, nullptr, 0, nullptr, nullptr))
+    SysDims fsd{};
+    if (fold_fusable(c, sps, hoff.data(), B, branch, fsd)) {
+      Carve cv = head;
+      if (int rc = run_folds_fused(c, sps, fsd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv, d_fit))
         return rc;
+    } else {
+      for (int f = 0; f < n_splits; ++f) {
+        Carve cv = head;   // every fold reuses the same workspace after the inputs, in stream order
+        const SysDims sd = choose_sys(c, ds[f], hoff.data(), B, branch, c->form_pref);
+        if (int rc = run_chunk(c, *sps[f], ds[f], sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv,
+                               d_fit + (int64_t)f * B, nullptr, 0, nullptr, nullptr))
+          return rc;
+      }
     }
     for (int f = 0; f < n_splits; ++f)
       HIPCHK(hipMemcpyAsync(fitness + (int64_t)f * batch + b0, d_fit + (int64_t)f * B, (size_t)B * 8,

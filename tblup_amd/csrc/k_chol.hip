@@ -250,12 +250,10 @@ struct CholArgs {
   int64_t ns, prow;         // padded system size, panel rows per contraction block
   int form;
   // primal form: rows read in place from the split's 2-bit packed SNP-major matrix
-  // (row P is zero)
-  const uint8_t* gs;
+  // (row P is zero; ft.gpk of the system's split)
   const int64_t* idx;
   const int64_t* off;
   int64_t gs_row, P;
-  const double* ymu;        // [nt] mean(y_T) per trait
   int64_t ytp;              // yT stride (nTp)
   int nt;                   // traits (right-hand sides)
   int NT, J;
@@ -266,6 +264,7 @@ struct CholArgs {
   double* part;             // [2][B][NT][128*128] off-diagonal partial sums K - sum_{L<J-1} (acc layout), slot J&1
   double* q;                // last-term mode: [B][NPACK*BLKD] L_{J,J-1} L_{J,J-1}^T, from launch J-1's tile (J, J-1)
   int64_t B;                // individuals in the chunk
+  FoldTab ft;               // each system's split (ymu, packed rows)
 };
 
 // st: profiling only (phase stamps of one factorisation in diagonal workgroup 0), else null
@@ -318,7 +317,7 @@ __device__ __forceinline__ const uint8_t* row_packed(const CholArgs& a, int64_t 
   if (r < k) {
     p = snp_col(a.idx[o0 + r], a.P);
   }
-  return a.gs + p * a.gs_row;
+  return a.ft.gpk[fold_of(a.ft, b)] + p * a.gs_row;
 }
 
 // ---------------------------------------------------------------------------
@@ -776,7 +775,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       if (tr < nt) {
         const int64_t o = (b * nt + tr) * ns + gi;
         const double wv = (J > 0) ? a.w[o] : 0.0;
-        rv[tr] = ((a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ymu[tr]) - wv;
+        rv[tr] = ((a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ft.ymu[0][tr]) - wv;
       }
     }
   }
@@ -1484,8 +1483,8 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
 
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
-             c.sd.prow, c.sd.form, c.gpk, c.idx, c.off, c.gpk_row, c.d.P, c.ymu, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
-             c.wgt, nullptr, c.kc, c.part, c.q, c.B};
+             c.sd.prow, c.sd.form, c.idx, c.off, c.gpk_row, c.d.P, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
+             c.wgt, nullptr, c.kc, c.part, c.q, c.B, c.ft};
   return a;
 }
 

@@ -140,18 +140,32 @@ hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const
   return hipGetLastError();
 }
 
+// fold-fused offsets: system s = f * B + b takes individual b's index list from the f-th copy
+__global__ void k_fold_offsets(const int64_t* __restrict__ off, int64_t B, int64_t F, int64_t sum_k,
+                               int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < F * B) out[i] = (i / B) * sum_k + off[i % B];
+  if (i == 0) out[F * B] = F * sum_k;
+}
+
+hipError_t launch_fold_offsets(const int64_t* off, int64_t B, int64_t F, int64_t sum_k, int64_t* out, hipStream_t s) {
+  const int64_t n = F * B;
+  hipLaunchKernelGGL(k_fold_offsets, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, off, B, F, sum_k, out);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // per-individual scalars: branch, 1/N, q/N^2, 1/d, mu, lambda
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
-                                                     const int32_t* __restrict__ csT,
-                                                     const int32_t* __restrict__ csA, const double* __restrict__ xty,
-                                                     int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
+                                                     FoldTab ft, const int32_t* __restrict__ csA, int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
                                                      int64_t ns, int nt, int branch, double h2,
                                                      double* __restrict__ scal, double* __restrict__ u,
                                                      double* __restrict__ rhs, int32_t* __restrict__ err) {
   const int64_t b = blockIdx.x;
   const int64_t o0 = off[b], k = off[b + 1] - o0;
+  const int32_t* __restrict__ csT = ft.csT[fold_of(ft, b)];   // the system's split
+  const double* __restrict__ xty = ft.xty[fold_of(ft, b)];
   int mode = branch;
   if (mode == 0) mode = (k > n) ? 1 : 2;  // evaluator.py:257
   const int32_t* cs = (mode == 1) ? csA : csT;
@@ -211,11 +225,11 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
   }
 }
 
-hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
-                              const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
+hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const FoldTab& ft,
+                              const int32_t* colsum_all, const EvalDims& d, const SysDims& sd,
                               int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
                               hipStream_t s) {
-  hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, colsum_T, colsum_all, xty, d.n,
+  hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, ft, colsum_all, d.n,
                      d.nT, d.nTp, d.P, sd.form, sd.ns, d.nt, branch, h2, scal, u, rhs, err);
   return hipGetLastError();
 }

@@ -220,6 +220,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   const double* Db = c.Dinv + b * (int64_t)NT * NPACK * BLKD;
   const double* sc = c.scal + b * SCAL;
   const double invN = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], muf = sc[SC_MUF];
+  const int fo = fold_of(c.ft, b);   // the system's split
 
   // alpha = L^{-T} z for every trait in one pass over L, block rows from the bottom, using
   // the stored diagonal inverses.  (L_JI^T alpha_J)[c] = sum_r Lt_(J,I)[c][r] alpha_J[r]:
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));
       for (int64_t qd = t >> 3; qd < ((c.skip & 2048) ? 0 : nq); qd += NTH / 8) {
         double acc[NTR][4];
-        pred_share<NTR>(c.gs, c.gs_row, rowp + J * TILE, alpha + J * TILE, ns, nr, nTp + 4 * qd, rg8, acc);
+        pred_share<NTR>(c.ft.gs[fo], c.gs_row, rowp + J * TILE, alpha + J * TILE, ns, nr, nTp + 4 * qd, rg8, acc);
 #pragma unroll
         for (int tr = 0; tr < NTR; ++tr)
 #pragma unroll
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     __syncthreads();
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr) {
-      const double MB = mbt[tr] * sc[SC_SM], mu = muf * c.ymu[tr];
+      const double MB = mbt[tr] * sc[SC_SM], mu = muf * c.ft.ymu[fo][tr];
       for (int64_t v = t; v < nV; v += NTH) eall[tr * nV + v] = eall[tr * nV + v] - MB + mu;
     }
     __syncthreads();
@@ -322,8 +323,8 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   for (int tr = 0; tr < nt; ++tr) {
     const double* al = alpha + tr * ns;
     double* e = eall + tr * nV;
-    const double* yV = c.yV + tr * nV;
-    const double mu = muf * c.ymu[tr];
+    const double* yV = c.ft.yV[fo] + tr * nV;
+    const double mu = muf * c.ft.ymu[fo][tr];
     if (c.sd.form == FORM_PRIMAL) {
       // (the EBVs above)
     } else {
@@ -578,7 +579,7 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   const int64_t nq = (nV + 3) / 4;
   for (int64_t qd = t >> 3; qd < nq; qd += CTH / 8) {
     double acc[NTR][4];
-    pred_share<NTR>(c.gs, c.gs_row, rowp, &bsh[0][0], TILE, nr, nTp + 4 * qd, rg, acc);
+    pred_share<NTR>(c.ft.gs[fold_of(c.ft, b)], c.gs_row, rowp, &bsh[0][0], TILE, nr, nTp + 4 * qd, rg, acc);
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr)
 #pragma unroll
@@ -613,7 +614,7 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   for (int tr = 0; tr < NTR; ++tr) {
     double mbt = mb[tr];
     for (int K = 1; K < NT; ++K) mbt += cload(ch.mbpart + (b * NT + K) * NTR + tr);
-    const double MB = mbt * sc[SC_SM], mu = muf * c.ymu[tr];
+    const double MB = mbt * sc[SC_SM], mu = muf * c.ft.ymu[fold_of(c.ft, b)][tr];
     double* e = eall + tr * nV;
     for (int64_t v = t; v < nV; v += CTH) {
       double acc = e[v];
@@ -621,7 +622,7 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
       e[v] = acc - MB + mu;
     }
     __syncthreads();
-    fsum += pearson_abs<PCTH>(e, c.yV + tr * nV, nV, red);
+    fsum += pearson_abs<PCTH>(e, c.ft.yV[fold_of(c.ft, b)] + tr * nV, nV, red);
     if (ebv != nullptr)
       for (int64_t v = t; v < nV; v += CTH) ebv[(b * NTR + tr) * nV + v] = e[v];
   }

@@ -101,6 +101,22 @@ __host__ __device__ __forceinline__ int pk(int q, int s) { return (q * (q + 1) /
 // element (r, c) of a 16x16 block; 16-B chunk swizzle makes the fragment reads conflict-free
 __host__ __device__ __forceinline__ int bo(int r, int c) { return r * NB + 2 * ((c >> 1) ^ ((r >> 1) & 7)) + (c & 1); }
 
+// Per-split device data of the systems of one launch sequence.  One split: nf = 1.  Fold-fused
+// evaluation (tblup_eval_folds*: IntraGCV's k folds as one batch of F x B systems, system
+// s = f * bpf + b against split f; every split of equal dimensions): one entry per fold.
+constexpr int MAXF = 16;
+struct FoldTab {
+  int64_t bpf;                 // systems per fold (the chunk's B when nf = 1)
+  int nf;
+  const uint8_t* gpk[MAXF];    // 2-bit packed split rows [P+1][nRp/4]
+  const int8_t* gs[MAXF];      // int8 split rows [P+1][nRp]
+  const int32_t* csT[MAXF];    // train allele counts [P]
+  const double* xty[MAXF];     // [nt][P]
+  const double* yV[MAXF];      // [nt][nV]
+  const double* ymu[MAXF];     // [nt]
+};
+__host__ __device__ __forceinline__ int fold_of(const FoldTab& ft, int64_t s) { return (int)(s / ft.bpf); }
+
 // ---- launchers (k_prep.hip) ----
 hipError_t launch_transpose_geno(const int8_t* src, int8_t* dst, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, int64_t P, hipStream_t s);
@@ -108,9 +124,12 @@ hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const
                               int64_t nRp, int64_t nT, const double* yT, const double* ymu, int nt,
                               int8_t* geno_split, uint8_t* geno_packed, int32_t* colsum_T, double* xty,
                               hipStream_t s);
+// fused offsets of F copies of a B-individual index list (sum_k indices each): out[F * B + 1]
+hipError_t launch_fold_offsets(const int64_t* off, int64_t B, int64_t F, int64_t sum_k, int64_t* out, hipStream_t s);
 // primal form (sd.form): also u[b][a] = s_a and rhs[b][t][a] = xty[t][p_a] / d over the ns rows
-hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const int32_t* colsum_T,
-                              const int32_t* colsum_all, const double* xty, const EvalDims& d, const SysDims& sd,
+// (colsum_T / xty of system b: ft's fold of b)
+hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const FoldTab& ft,
+                              const int32_t* colsum_all, const EvalDims& d, const SysDims& sd,
                               int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
                               hipStream_t s);
 hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int64_t* off,
@@ -134,17 +153,14 @@ struct CholLaunch {
   const double* rhs;     // [B][nt][ns] primal right-hand sides (dual: y_T - mu on the fly)
   double* S;             // [B][2][36*256] diagonal-tile preparation, slot J&1
   double* Kd;            // [B][NT][36*256] GRM diagonal tiles
-  const double* yT;      // split phenotypes [nt][nTp]
-  const double* yV;      // [nt][nV]
-  const double* ymu;     // [nt] mean(y_T) per trait
+  const double* yT;      // split phenotypes [nt][nTp] (kernel form: one split)
   const int8_t* panel;   // gathered genotypes
   int64_t pstride;       // panel bytes per individual
   const int64_t* off;    // [B+1] device offsets
-  const int8_t* gs;      // split SNP-major matrix [P+1][gs_row] (row P zero): primal rows in place
   const int64_t* idx;    // device SNP indices of the chunk
-  int64_t gs_row;        // bytes per split row (nRp)
-  const uint8_t* gpk;    // the same matrix 2-bit packed [P+1][gpk_row] (4 animals per byte)
-  int64_t gpk_row;       // nRp / 4
+  int64_t gs_row;        // bytes per int8 split row (nRp): split SNP-major matrix, row P zero
+  int64_t gpk_row;       // bytes per 2-bit packed split row (nRp / 4)
+  FoldTab ft;            // split rows, counts, right-hand sides and phenotypes of each system's split
   const double* u;       // [B][prow]
   const double* scal;    // [B][SCAL]
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production

@@ -262,6 +262,31 @@ def test_config2_folds_batched_equal_per_split(config2):
         eng.evaluate_folds_device([sids[0], 12345], d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr())
 
 
+def test_config2_folds_ragged_and_unfused(config2, monkeypatch):
+    """Folds of unequal sizes (1277 train animals in 5 folds: 256, 256, 255, 255, 255) take the
+    split-by-split path, folds of equal sizes the fold-fused one (one launch sequence of 5 x B
+    systems); TBLUP_FOLD_FUSE=0 forces split by split.  Every row equals that split's own
+    evaluation bit for bit."""
+    from tblup_amd.engine import GpuBlupEngine
+    from tblup_amd.evaluator import InterGCVBlupParallelEvaluator
+    c = config2
+    eng = c["eng"]
+    genomes = c["genomes"][:40]
+    ragged = InterGCVBlupParallelEvaluator.make_fold_indices(np.asarray(c["T"])[:-3], 5)
+    assert len({len(t) for t, _ in ragged}) == 2
+    got = eng.evaluate_folds(genomes, ragged, 0.4)
+    for k, (t, v) in enumerate(ragged):
+        np.testing.assert_array_equal(got[k], eng.evaluate(genomes, t, v, 0.4))
+    folds = InterGCVBlupParallelEvaluator.make_fold_indices(np.asarray(c["T"]), 5)
+    fused = eng.evaluate_folds(genomes, folds, 0.4)
+    monkeypatch.setenv("TBLUP_FOLD_FUSE", "0")   # read at context creation
+    eng2 = GpuBlupEngine(c["geno"], c["pheno"], device=0)
+    try:
+        np.testing.assert_array_equal(eng2.evaluate_folds(genomes, folds, 0.4), fused)
+    finally:
+        eng2.close()
+
+
 def test_config2_gblup_branch_sample(config2):
     """k > n at config-2 size: the GBLUP branch (p over all n animals, no y centring)."""
     c = config2
