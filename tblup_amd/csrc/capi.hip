@@ -48,6 +48,7 @@ struct DevBuf {
 
 struct Split {
   int64_t nT = 0, nV = 0, nTp = 0, nVp = 0, nRp = 0;
+  std::vector<int64_t> rows;   // train + valid animals, sorted (fold sets: shared counts)
   std::vector<double> meanyT;   // [nt]
   DevBuf geno, gpk, colsumT, xty, yT, yV, ymu;
 };
@@ -105,6 +106,7 @@ struct tblup_ctx {
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
+  int fold_share = 1;    // TBLUP_FOLD_SHARE: 0 builds every fold's system tiles from its own rows
   std::vector<int64_t> fold_hoff;   // host offsets of the last fold-fused chunk (host-side shapes only)
   DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
   int32_t chain_seq = 0; // flag value of the last chained solve
@@ -429,6 +431,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
   double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
   double* Qb = use_last_term(c, sd, B) ? cv.take<double>((size_t)B * NPACK * BLKD) : nullptr;
+  const bool fold_share = use_st && ft.nf > 1 && ft.share;   // k_sys_tiles_folds
+  int16_t* kcd = fold_share ? cv.take<int16_t>((size_t)B * sd.NT * KC_TILE) : nullptr;
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
   for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs);
@@ -485,7 +489,9 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       cl.wgt = wgt + c->wgt_used * WGT_REC;
       c->wgt_used += B * sd.NT * (sd.NT + 1) / 2;
     }
-    rc = timed(c, s, KC_GRM, fg, bg, [&] { return launch_sys_tiles(cl, s); });
+    rc = timed(c, s, KC_GRM, fg, bg, [&] {
+      return fold_share ? launch_sys_tiles_folds(cl, kcd, s) : launch_sys_tiles(cl, s);
+    });
     if (rc) return rc;
   } else {
     // int ops of the diagonal GRM tiles J < 2 (J >= 2 run inside the column-0 off-diagonal launch)
@@ -624,6 +630,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_CHAIN_SYNC")) c->chain_sync = atoi(e);
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
+  if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
   if (!panel) {
     *out = c.release();
@@ -704,6 +711,9 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   sp->nTp = round_up(nT, TILE);
   sp->nVp = round_up(nV, TILE);
   sp->nRp = sp->nTp + sp->nVp;
+  sp->rows.assign(train, train + nT);
+  sp->rows.insert(sp->rows.end(), valid, valid + nV);
+  std::sort(sp->rows.begin(), sp->rows.end());
   std::vector<int32_t> rowmap(sp->nRp, -1);
   for (int64_t i = 0; i < nT; ++i) rowmap[i] = (int32_t)train[i];
   for (int64_t i = 0; i < nV; ++i) rowmap[sp->nTp + i] = (int32_t)valid[i];
@@ -941,6 +951,8 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
   FoldTab ft{};
   ft.bpf = B;
   ft.nf = (int)F;
+  ft.share = c->fold_share;
+  for (int64_t f = 1; f < F; ++f) ft.share = ft.share && sps[f]->rows == sps[0]->rows;
   for (int64_t f = 0; f < F; ++f) {
     ft.gpk[f] = (const uint8_t*)sps[f]->gpk.p;
     ft.gs[f] = (const int8_t*)sps[f]->geno.p;
@@ -953,12 +965,13 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
                    nullptr, &ft);
 }
 
-// workspace of a fused chunk: its replicated index lists included, plus room for the host
-// entry's own copy of the chunk's index list and offsets ahead of it
+// workspace of a fused chunk: its replicated index lists and the diagonal tiles' counts included,
+// plus room for the host entry's own copy of the chunk's index list and offsets ahead of it
 static size_t fused_bytes(const tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd, int64_t B,
                           int64_t sum_k) {
   const int64_t F = (int64_t)sps.size();
-  return chunk_bytes(c, dims_of(c, *sps[0]), sd, F * B, F * sum_k, false) + (size_t)(sum_k + B + 1) * 8 + 1024;
+  return chunk_bytes(c, dims_of(c, *sps[0]), sd, F * B, F * sum_k, false) + (size_t)(sum_k + B + 1) * 8 +
+         (size_t)F * B * sd.NT * KC_TILE * 2 + 1024;   // + the diagonal tiles' counts (shared counts)
 }
 
 static int validate_splits(tblup_ctx* c, const int* split_ids, int n_splits, std::vector<Split*>& sps) {

@@ -1445,8 +1445,8 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
   tr.done(WGT_SYS, J, I, b);
 }
 
-__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
-                                       int l) {
+__device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr,
+                                                      int qc, int l) {
   const double* sc = a.scal + b * SCAL;
   const int64_t j0 = (int64_t)J * TILE;
   const double sa_ = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
@@ -1481,6 +1481,165 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
     }
 }
 
+// a 128 x 128 count tile from the fp32 accumulators (exact integers) as int16, in the lane order
+// of the off-diagonal kernel's reads (see kc in tblup_internal.h)
+__device__ __forceinline__ void store_counts16(int16_t* kt, const v4f (&cnt)[4][4], int qr, int qc, int l) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cb = 4 * qr + m, ib = 4 * qc + n;
+      const v4f c = cnt[m][n];
+      const int2 packed = {(int)((uint32_t)((int)c[0] & 0xffff) | ((uint32_t)(int)c[1] << 16)),
+                           (int)((uint32_t)((int)c[2] & 0xffff) | ((uint32_t)(int)c[3] << 16))};
+      *reinterpret_cast<int2*>(kt + ((ib * 8 + cb) * 64 + l) * 4) = packed;
+    }
+}
+
+// K_JJ + lambda I of system s from its diagonal tile's counts (k_sys_tiles_folds): the epilogue of
+// k_sys_tiles on the same lanes, one 4-wave workgroup per (system, J)
+__global__ __launch_bounds__(64 * STW) void k_sys_diag_counts(CholArgs a, const int16_t* kcd) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, qr = w >> 1, qc = w & 1;
+  const int64_t s = blockIdx.x / a.NT;
+  const int J = (int)(blockIdx.x % a.NT);
+  if (qr < qc) return;   // the upper quadrant is never read
+  const int16_t* kt = kcd + (s * a.NT + J) * KC_TILE;
+  v4f cnt[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int2 p = *reinterpret_cast<const int2*>(kt + (((4 * qc + n) * 8 + 4 * qr + m) * 64 + l) * 4);
+      cnt[m][n] = v4f{(float)(int16_t)(p.x & 0xffff), (float)(int16_t)(p.x >> 16), (float)(int16_t)(p.y & 0xffff),
+                      (float)(int16_t)(p.y >> 16)};
+    }
+  sys_diag_epilogue_inl(a, cnt, s, J, qr, qc, l);
+}
+
+// Fold-fused evaluation with shared counts (IntraGCV's folds, tblup_eval_folds*): when every fold's
+// training rows R_f and validation rows V_f make up the same multiset T_all, C_{R_f} = C_{T_all} -
+// C_{V_f}.  One workgroup per (individual b, tile) accumulates C_{T_all} over fold 0's rows
+// [0, nRp) (train, zero padding, validation, zero padding), then for f = 0 .. F-1 adds C_{V_{f-1}}
+// back (f > 0) and subtracts C_{V_f} -- the A operand negated through the e2m1 sign bits -- and
+// stores system f * B + b's tile after each subtraction.  The stage sequence runs through one
+// 3-deep LDS-DMA ring across these segments.  Every partial sum is an exact integer in fp32, so
+// the tiles equal k_sys_tiles' per-fold ones bit for bit; contraction (nRp + (2F - 1) nVp) / (F nTp)
+// of the per-fold launch's (config 2, 5 folds of 256: 14 stages of 256 animals instead of 20).
+__global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles_folds(CholArgs a, int16_t* kc, int16_t* kcd, int ntri) {
+  constexpr int D = 3;
+  constexpr int TB = TILE * 64;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[D * 2 * TB];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, qr = w >> 1, qc = w & 1;
+  WgTrace tr(a.wgt);
+  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t b = lg / ntri;   // individual: system b of fold 0
+  const int t = (int)(lg % ntri);
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  const int J = t - I * (I + 1) / 2;
+  const bool compute = (I != J) || (qr >= qc);
+  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
+  const int F = a.ft.nf;
+  const int64_t bpf = a.ft.bpf;
+  const int64_t vbyte = a.ytp / 4;                           // validation rows start (nTp animals)
+  const int64_t nblkA = a.gs_row / 16, nsA = (nblkA + 3) >> 2;   // all nRp animals, 64 per block
+  const int64_t nblkV = nblkA - a.ytp / 64, nsV = (nblkV + 3) >> 2;
+  const int64_t nst = nsA + (2 * F - 1) * nsV;
+  // the same SNP rows in every fold's layout: per-lane row offsets, fold bases per stage
+  int64_t oa[2], ob[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 16 * (2 * w + h) + (l >> 2), pos = l & 3;
+    oa[h] = (row_packed(a, b, j0 + row) - a.ft.gpk[0]) + 16 * (pos ^ ((row >> 2) & 3));
+    ob[h] = (row_packed(a, b, i0 + row) - a.ft.gpk[0]) + 16 * (pos ^ ((row >> 2) & 2));
+  }
+  // stage g -> segment k (0: T_all of fold 0, 2f + 1: minus V_f, 2f + 2: plus V_f) and its stage
+  auto seg_of = [&](int64_t g, int& k, int64_t& st) {
+    if (g < nsA) {
+      k = 0;
+      st = g;
+    } else {
+      k = 1 + (int)((g - nsA) / nsV);
+      st = (g - nsA) % nsV;
+    }
+  };
+  auto issue = [&](int64_t g) {
+    int k;
+    int64_t st;
+    seg_of(g, k, st);
+    const uint8_t* base = a.ft.gpk[k == 0 ? 0 : (k - 1) >> 1] + (k == 0 ? 0 : vbyte) + st * 64;
+    uint8_t* slot = lds + (int)(g % D) * 2 * TB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_global_load_lds(base + oa[h], (lds_ptr_t)(slot + (2 * w + h) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(base + ob[h], (lds_ptr_t)(slot + TB + (2 * w + h) * 1024), 16, 0, 0);
+    }
+  };
+  v4f cnt[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) cnt[m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int64_t g = 0; g < D - 1 && g < nst; ++g) issue(g);
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  int64_t g = 0;
+  for (int k = 0; k < 2 * F; ++k) {
+    const int64_t ns_k = k == 0 ? nsA : nsV;
+    const int tail_ch = (int)((k == 0 ? nblkA : nblkV) & 3);
+    const int neg = (k & 1) ? (int)0x88888888u : 0;   // e2m1 sign bits: subtract this segment
+    for (int64_t st = 0; st < ns_k; ++st, ++g) {
+      if (g + D - 2 < nst) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 4) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      if (g + D - 1 < nst) issue(g + D - 1);
+      if (compute) {
+        const uint8_t* As = lds + (int)(g % D) * 2 * TB;
+        const uint8_t* Bs = As + TB;
+        const bool ztail = (st == ns_k - 1 && tail_ch != 0 && ch >= tail_ch);   // past the segment's rows
+        uint4 aq[4], bq[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          aq[m] = *reinterpret_cast<const uint4*>(As + i8off_a(16 * (4 * qr + m) + prow, ch));
+          bq[m] = *reinterpret_cast<const uint4*>(Bs + i8off_b(16 * (4 * qc + m) + rho, ch));
+          if (ztail) bq[m] = uint4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          v4i av[4], bv[4];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            av[m] = s2 == 0 ? fp4_operand(aq[m].x, aq[m].y) : fp4_operand(aq[m].z, aq[m].w);
+            av[m] |= neg;
+            bv[m] = s2 == 0 ? fp4_operand(bq[m].x, bq[m].y) : fp4_operand(bq[m].z, bq[m].w);
+          }
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+              cnt[m][n] = mfma_fp4_16x16x128(av[m], bv[n], cnt[m][n], 4, 4, 0, 128, 0, 128);
+        }
+      }
+    }
+    if (!(k & 1) || !compute) continue;
+    const int64_t s = (int64_t)((k - 1) >> 1) * bpf + b;   // C_{T_all} - C_{V_f}: system f * B + b
+    // off-diagonal tile: counts into kc; diagonal tile: counts into kcd (k_sys_diag_counts then
+    // forms K_JJ + lambda I: that epilogue beside the live accumulators spilled)
+    store_counts16(I != J ? kc + ((s * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE
+                          : kcd + (s * a.NT + J) * KC_TILE,
+                   cnt, qr, qc, l);
+  }
+  tr.done(WGT_SYS, J, I, b);
+}
+
+
+__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
+                                       int l) {
+  sys_diag_epilogue_inl(a, cnt, b, J, qr, qc, l);
+}
+
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.idx, c.off, c.gpk_row, c.d.P, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
@@ -1492,6 +1651,16 @@ hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
   CholArgs a = make_args(c, 0);
   const int ntri = c.sd.NT * (c.sd.NT + 1) / 2;
   hipLaunchKernelGGL(k_sys_tiles, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
+  return hipGetLastError();
+}
+
+hipError_t launch_sys_tiles_folds(const CholLaunch& c, int16_t* kcd, hipStream_t s) {
+  CholArgs a = make_args(c, 0);
+  const int ntri = c.sd.NT * (c.sd.NT + 1) / 2;
+  hipLaunchKernelGGL(k_sys_tiles_folds, dim3((unsigned)(c.ft.bpf * ntri)), dim3(64 * STW), 0, s, a, c.kc, kcd, ntri);
+  if (hipError_t e = hipGetLastError()) return e;
+  a.wgt = nullptr;
+  hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * c.sd.NT)), dim3(64 * STW), 0, s, a, (const int16_t*)kcd);
   return hipGetLastError();
 }
 

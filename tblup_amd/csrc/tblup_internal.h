@@ -108,6 +108,7 @@ constexpr int MAXF = 16;
 struct FoldTab {
   int64_t bpf;                 // systems per fold (the chunk's B when nf = 1)
   int nf;
+  int share;                   // every fold's train + valid rows are one multiset (k_sys_tiles_folds)
   const uint8_t* gpk[MAXF];    // 2-bit packed split rows [P+1][nRp/4]
   const int8_t* gs[MAXF];      // int8 split rows [P+1][nRp]
   const int32_t* csT[MAXF];    // train allele counts [P]
@@ -211,6 +212,10 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 // counts into c.kc, diagonal tiles into Kd (replaces launch_diag_grm and the int8 phase of the
 // off-diagonal tiles)
 hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s);
+// the same for a fold-fused chunk whose folds share their train + valid rows (FoldTab::share):
+// C_{R_f} = C_{T_all} - C_{V_f}, one workgroup per (individual, tile) for all F folds
+// (diagonal tiles through their counts in kcd [B][NT][KC_TILE] int16, then k_sys_diag_counts)
+hipError_t launch_sys_tiles_folds(const CholLaunch& c, int16_t* kcd, hipStream_t s);
 // Back substitution, prediction and fitness.  ch == null: one workgroup per individual
 // (k_solve); else (SNP form) the chained solve (k_solve_chain): an individual's block rows and
 // tile products spread over the chip, handing beta_J and the partial products on through

@@ -265,8 +265,9 @@ def test_config2_folds_batched_equal_per_split(config2):
 def test_config2_folds_ragged_and_unfused(config2, monkeypatch):
     """Folds of unequal sizes (1277 train animals in 5 folds: 256, 256, 255, 255, 255) take the
     split-by-split path, folds of equal sizes the fold-fused one (one launch sequence of 5 x B
-    systems); TBLUP_FOLD_FUSE=0 forces split by split.  Every row equals that split's own
-    evaluation bit for bit."""
+    systems, system tiles from the shared counts C_T - C_V_f); TBLUP_FOLD_SHARE=0 builds every
+    fold's tiles from its own rows, TBLUP_FOLD_FUSE=0 runs split by split.  Every row equals that
+    split's own evaluation bit for bit."""
     from tblup_amd.engine import GpuBlupEngine
     from tblup_amd.evaluator import InterGCVBlupParallelEvaluator
     c = config2
@@ -279,12 +280,13 @@ def test_config2_folds_ragged_and_unfused(config2, monkeypatch):
         np.testing.assert_array_equal(got[k], eng.evaluate(genomes, t, v, 0.4))
     folds = InterGCVBlupParallelEvaluator.make_fold_indices(np.asarray(c["T"]), 5)
     fused = eng.evaluate_folds(genomes, folds, 0.4)
-    monkeypatch.setenv("TBLUP_FOLD_FUSE", "0")   # read at context creation
-    eng2 = GpuBlupEngine(c["geno"], c["pheno"], device=0)
-    try:
-        np.testing.assert_array_equal(eng2.evaluate_folds(genomes, folds, 0.4), fused)
-    finally:
-        eng2.close()
+    for var in ("TBLUP_FOLD_SHARE", "TBLUP_FOLD_FUSE"):   # read at context creation
+        monkeypatch.setenv(var, "0")
+        eng2 = GpuBlupEngine(c["geno"], c["pheno"], device=0)
+        try:
+            np.testing.assert_array_equal(eng2.evaluate_folds(genomes, folds, 0.4), fused)
+        finally:
+            eng2.close()
 
 
 def test_config2_gblup_branch_sample(config2):

@@ -3,8 +3,9 @@ fold's evaluation on the GPU: config 1 (200 x 1000, k = 100, pop 32) and config 
 k = 1000, pop 256).  Per config one JSON line with
   * device-resident genomes (no host decode in the ratio): one fold's evaluate_device and the
     k folds' evaluate_folds_device (tblup_eval_folds_device: fold-fused, the k x pop systems as
-    one batch through one launch sequence; beside it the same call with TBLUP_FOLD_FUSE=0, the
-    folds back to back on one stream), medians over repeats, and their ratio;
+    one batch through one launch sequence, system tiles from shared counts; beside it the same
+    call with TBLUP_FOLD_SHARE=0 -- every fold's tiles from its own rows -- and with
+    TBLUP_FOLD_FUSE=0, the folds back to back on one stream), medians over repeats, and ratios;
   * end to end through the drop-in classes: the median time of a fresh population's evaluate()
     for the plain evaluator (one split) and for IntraGCV (one evaluate_folds call).
 (A variant with the folds on k contexts driven from k host threads measured slower in round 2:
@@ -83,14 +84,17 @@ def main():
         for f in (0, 4):   # the batched folds are each split's own evaluation
             assert np.array_equal(got[f], eng.evaluate(genomes, *splits[f], 0.4))
         eng.close()
-        os.environ["TBLUP_FOLD_FUSE"] = "0"   # read at context creation
-        eng = GpuBlupEngine(geno, np.load(pp), device=0)
-        del os.environ["TBLUP_FOLD_FUSE"]
-        sids = [eng.split_id(t, v) for t, v in splits]
-        seq_dev = dev_ms(lambda: eng.evaluate_folds_device(sids, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4,
-                                                           d_fit.data_ptr(), stream_ptr=st.cuda_stream))
-        assert np.array_equal(d_fit.cpu().numpy(), got)
-        eng.close()
+        alt = {}
+        for var in ("TBLUP_FOLD_SHARE", "TBLUP_FOLD_FUSE"):
+            os.environ[var] = "0"   # read at context creation
+            eng = GpuBlupEngine(geno, np.load(pp), device=0)
+            del os.environ[var]
+            sids = [eng.split_id(t, v) for t, v in splits]
+            alt[var] = dev_ms(lambda: eng.evaluate_folds_device(sids, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4,
+                                                                d_fit.data_ptr(), stream_ptr=st.cuda_stream))
+            assert np.array_equal(d_fit.cpu().numpy(), got)
+            eng.close()
+        seq_dev = alt["TBLUP_FOLD_FUSE"]
         random.seed(1)
         np.random.seed(1)
         one = timed_evals(E.BlupParallelEvaluator(gp, pp, 0.4), make_pop, 5)
@@ -100,6 +104,7 @@ def main():
         print(json.dumps({"config": name, "pop": pop,
                           "device_one_fold_ms": round(one_dev, 3), "device_k_folds_ms": round(folds_dev, 3),
                           "device_ratio": round(folds_dev / one_dev, 2),
+                          "device_k_folds_unshared_ms": round(alt["TBLUP_FOLD_SHARE"], 3),
                           "device_k_folds_unfused_ms": round(seq_dev, 3),
                           "device_ratio_unfused": round(seq_dev / one_dev, 2),
                           "one_split_ms": round(one, 3), "intragcv_ms": round(intra, 3),
