@@ -101,12 +101,18 @@ struct tblup_ctx {
   // Cholesky schedule (results are bit-identical under every setting; see OffPlan):
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
+  int64_t ahead_slots = AHEAD_SLOTS;   // TBLUP_AHEAD_SLOTS: the auto rule's threshold (A/B timing)
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
   int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (B <= LT_MAX_B), 0 never, 1 always (see use_last_term)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
   int fold_share = 1;    // TBLUP_FOLD_SHARE: 0 builds every fold's system tiles from its own rows
+  // SNP form: the padding rows (ns - k) lead the system, so the contractions over block column 0
+  // skip them (TBLUP_PAD_FIRST=0: trailing padding; TBLUP_PAD_SKIP=0: leading padding, no skip --
+  // bit-identical to the skip).  A/B knobs only.
+  int pad_first = 1;
+  int pad_skip = 1;
   std::vector<int64_t> fold_hoff;   // host offsets of the last fold-fused chunk (host-side shapes only)
   DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
   int32_t chain_seq = 0; // flag value of the last chained solve
@@ -224,7 +230,7 @@ static double list_makespan(std::initializer_list<std::pair<double, int64_t>> cl
   return end;
 }
 
-OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol) {
+OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol, int64_t slots) {
   OffPlan p{};
   p.nI = NT - J - 1;
   if (p.nI <= 0) {
@@ -234,7 +240,7 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   // launch j computes the partial sums of column j + 1's tiles; auto: when the launch's P-units
   // (B x (NT - 2 - j)) fit in AHEAD_SLOTS workgroup slots, i.e. run beside its T-units in one wave
   auto ahead_at = [&](int j) {
-    const bool on = ahead == 1 || (ahead < 0 && B * (NT - 2 - j) < AHEAD_SLOTS);
+    const bool on = ahead == 1 || (ahead < 0 && B * (NT - 2 - j) < slots);
     return on && j >= 1 && j + 2 <= NT - 1;
   };
   p.nP = ahead_at(J) ? NT - 2 - J : 0;
@@ -278,7 +284,7 @@ namespace {
 
 bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
   for (int J = 0; J < NT; ++J)
-    if (off_plan(B, NT, J, st, c->ahead, c->nrs).nP > 0) return true;
+    if (off_plan(B, NT, J, st, c->ahead, c->nrs, c->ahead_slots).nP > 0) return true;
   return false;
 }
 
@@ -367,6 +373,7 @@ SysDims choose_sys(const tblup_ctx* c, const EvalDims& d, const int64_t* h_off, 
   SysDims sd;
   if (primal) {
     sd.form = FORM_PRIMAL;
+    sd.pad_first = c->pad_first;
     sd.ns = kp;
     sd.prow = kp;
     sd.cblk = d.nRp / KBLK;
@@ -435,7 +442,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   int16_t* kcd = fold_share ? cv.take<int16_t>((size_t)B * sd.NT * KC_TILE) : nullptr;
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
-  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs);
+  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, c->ahead_slots);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
@@ -465,6 +472,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, panel, pstride, d_off, d_idx,
                 d.nRp, d.nRp / 4, ft, u, scal, c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
                 Pp, Qb};
+  cl.padskip = (sd.form == FORM_PRIMAL && sd.pad_first && c->pad_skip) ? 1 : 0;
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
@@ -631,6 +639,9 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
+  if (const char* e = getenv("TBLUP_AHEAD_SLOTS")) c->ahead_slots = std::max(0, atoi(e));
+  if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
+  if (const char* e = getenv("TBLUP_PAD_SKIP")) c->pad_skip = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
   if (!panel) {
     *out = c.release();

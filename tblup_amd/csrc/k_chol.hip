@@ -28,6 +28,7 @@
 // become the fp64 accumulators of the Cholesky GEMM without any data movement.
 #include "i8_tile.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace tblup {
 
@@ -265,7 +266,15 @@ struct CholArgs {
   double* q;                // last-term mode: [B][NPACK*BLKD] L_{J,J-1} L_{J,J-1}^T, from launch J-1's tile (J, J-1)
   int64_t B;                // individuals in the chunk
   FoldTab ft;               // each system's split (ymu, packed rows)
+  int padskip;              // contractions over block column 0 skip the leading padding rows (TBLUP_PAD_SKIP)
+  int padfirst;             // SNP form: padding rows lead (SC_PAD = ns - k)
 };
+
+// Leading contraction rows of block column 0 that a GEMM1 / SYRK run starting at L = 0 skips:
+// individual b's leading padding rows (SC_PAD), rounded down to the MFMA's 4-row k-step.
+__device__ __forceinline__ int skip_rows(const CholArgs& a, int64_t b) {
+  return a.padskip ? ((int)a.scal[b * SCAL + SC_PAD] & ~3) : 0;
+}
 
 // st: profiling only (phase stamps of one factorisation in diagonal workgroup 0), else null
 __device__ __forceinline__ void factor16_any(const CholArgs& a, double* D, double* X, int l, uint64_t* st = nullptr) {
@@ -310,12 +319,14 @@ struct WgTrace {
 __device__ __forceinline__ const int8_t* row_base(const CholArgs& a, int64_t b, int64_t r) {
   return a.panel + b * a.pstride + r * KBLK;
 }
-// Packed split row of system row r (primal; padding rows -> the zero row P; stage kb at + 16 kb).
+// Packed split row of system row r (primal: row r holds selected SNP r - pad; padding rows -> the
+// zero row P; stage kb at + 16 kb).
 __device__ __forceinline__ const uint8_t* row_packed(const CholArgs& a, int64_t b, int64_t r) {
   const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
+  const int64_t pad = a.padfirst ? a.ns - k : 0;   // = SC_PAD, without a dependent scal load
   int64_t p = a.P;
-  if (r < k) {
-    p = snp_col(a.idx[o0 + r], a.P);
+  if (sys_real(r, pad, k)) {
+    p = snp_col(a.idx[o0 + r - pad], a.P);
   }
   return a.ft.gpk[fold_of(a.ft, b)] + p * a.gs_row;
 }
@@ -537,13 +548,22 @@ __device__ __forceinline__ void i8_tt2d_pk64(const uint8_t* sa, const uint8_t* s
 // ring has twice the barriers and measured 2% slower.)  Every accumulator element's chain of MFMAs
 // is the same whatever NCB / cb0 and wherever the L range is split, so partial sums handed from
 // one launch to the next reproduce the one-workgroup result bit for bit.
+//
+// r0 (a multiple of 4): leading contraction rows skipped -- the SNP form's leading padding rows,
+// whose columns of block column 0 are exact zeros (sys_real), so only a range that starts at L = 0
+// passes r0 > 0: whole 32-row stages, then the first stage computed from k-step (r0 & 31) / 4 (a
+// peeled stage: the main loop stays the branch-free one; a short LAST stage instead, or a per-k-step
+// bound inside the loop, made the compiler spill or split the MFMA chains).  The MFMAs skipped would
+// only have added exact zeros, so the result is the same bit for bit.
 template <int NCB>
 __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const double* __restrict__ ltI, int nL,
-                                          int cb0, double* lds, v4d (&acc)[NCB]) {
+                                          int cb0, double* lds, v4d (&acc)[NCB], int r0 = 0) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   constexpr int AS = 32 * TILE;   // doubles per 32-row stage
+  const int s0 = r0 >> 5;         // whole leading stages skipped
+  const int kf = (r0 & 31) >> 2;  // leading k-steps skipped in the first stage computed
   const int nst = 4 * nL;
-  if (nst == 0) return;
+  if (nst <= s0) return;
   auto src_of = [&](int s) { return (int64_t)(s >> 2) * TT + (s & 3) * AS; };
   auto issue_a = [&](int s) {
     double* slot = lds + (s & 1) * AS;
@@ -557,10 +577,36 @@ __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const 
   };
   const double* bcol = ltI + 16 * w + (l & 15) + (l >> 4) * TILE;
   double bc[8];
-  issue_a(0);
+  issue_a(s0);
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) bc[kk] = bcol[4 * kk * TILE];
-  for (int s = 0; s < nst; ++s) {
+  for (int kk = 0; kk < 8; ++kk) bc[kk] = bcol[src_of(s0) + 4 * kk * TILE];
+  int s = s0;
+  if (kf > 0) {   // the first stage from k-step kf
+    // the next stage's A issued before this short stage's wait, not after it (its 4 LDS-DMA ops
+    // stay outstanding: vmcnt(4))
+    const bool more = s + 1 < nst;
+    if (more) {
+      issue_a(s + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const double* bs = bcol + src_of(more ? s + 1 : s);
+    const double* As = lds + (s & 1) * AS;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = 4 * kk + (l >> 4);
+      if (kk >= kf) {
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          acc[cb] = mfma64_nega(As[lt_off(k, 16 * (cb0 + cb) + (l & 15))], bc[kk], acc[cb]);
+      }
+      if (more) bc[kk] = bs[4 * kk * TILE];
+    }
+    ++s;
+  }
+  for (; s < nst; ++s) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const bool more = s + 1 < nst;
@@ -583,11 +629,13 @@ __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const 
 
 // SYRK of Lt stages restricted to the 36 lower blocks, 8 waves: wave W takes blocks
 // W + 8i (5 blocks for W < 4, 4 for W >= 4); only the i in MASK (a diagonal-target slice).
-template <int W, int MASK>
-__device__ __forceinline__ void syrk_stage8(const double* As, v4d (&acc)[5], int l) {
+// PART: from k-step ks on (the first stage of a run that starts past padding rows).
+template <int W, int MASK, bool PART = false>
+__device__ __forceinline__ void syrk_stage8(const double* As, v4d (&acc)[5], int l, int ks = 0) {
   constexpr int NBW = (W < 4) ? 5 : 4;
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
+    if (PART && kk < ks) continue;
     const int k = 4 * kk + (l >> 4);
     double a8[8];
 #pragma unroll
@@ -603,12 +651,15 @@ __host__ __device__ constexpr int slice_mask(int sl) { return sl == 0 ? 0x1F : s
 
 // SYRK of Lt rows restricted to the 36 lower blocks, 8 waves (wave W takes blocks W + 8i, i in
 // slice_mask(sl)), on 32-row stages through a 2 x 32 KiB LDS-DMA ring: one barrier per 32 k rows.
+// r0 (a multiple of 4): leading rows skipped, as in gemm1_a32 (zero padding columns of block
+// column 0): whole stages, then the first stage computed from k-step (r0 & 31) / 4.
 __device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, int nst16, double* lds, v4d (&acc)[5],
-                                               int sl = 0) {
+                                               int sl = 0, int r0 = 0) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (nst16 <= 0) return;
   constexpr int AS = 32 * TILE;
   const int nst = nst16 >> 1;   // 8 x (number of Lt tiles): always even
+  const int s0 = r0 >> 5, kf = (r0 & 31) >> 2;
+  if (nst <= s0) return;
   auto issue = [&](int s) {
     double* slot = lds + (s & 1) * AS;
 #pragma unroll
@@ -618,29 +669,52 @@ __device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, i
                                        (lds_ptr_t)(slot + k * TILE), 16, 0, 0);
     }
   };
-  issue(0);
+  issue(s0);
   const int ws = w + 8 * sl;   // wave-uniform (wave, slice) instantiation
-  for (int s = 0; s < nst; ++s) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + 1 < nst) issue(s + 1);
-    const double* As = lds + (s & 1) * AS;
 #define SYRK_CASE(W, SL)                                    \
   case W + 8 * SL:                                          \
     syrk_stage8<W, slice_mask(SL)>(As, acc, l);             \
     syrk_stage8<W, slice_mask(SL)>(As + LTS, acc, l);       \
     break;
-#define SYRK_CASES(SL) SYRK_CASE(0, SL) SYRK_CASE(1, SL) SYRK_CASE(2, SL) SYRK_CASE(3, SL) \
-                       SYRK_CASE(4, SL) SYRK_CASE(5, SL) SYRK_CASE(6, SL) SYRK_CASE(7, SL)
+#define SYRK_PCASE(W, SL)                                                             \
+  case W + 8 * SL:                                                                    \
+    if (kf < 4) syrk_stage8<W, slice_mask(SL), true>(As, acc, l, kf);                 \
+    syrk_stage8<W, slice_mask(SL), true>(As + LTS, acc, l, kf < 4 ? 0 : kf - 4);      \
+    break;
+#define SYRK_CASES(C, SL) C(0, SL) C(1, SL) C(2, SL) C(3, SL) C(4, SL) C(5, SL) C(6, SL) C(7, SL)
+  int s = s0;
+  if (kf > 0) {   // the next stage issued before this short stage's wait (as in gemm1_a32)
+    if (s + 1 < nst) {
+      issue(s + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const double* As = lds + (s & 1) * AS;
     switch (ws) {
-      SYRK_CASES(0)
-      SYRK_CASES(1)
-      SYRK_CASES(2)
+      SYRK_CASES(SYRK_PCASE, 0)
+      SYRK_CASES(SYRK_PCASE, 1)
+      SYRK_CASES(SYRK_PCASE, 2)
       default: break;
     }
-#undef SYRK_CASES
-#undef SYRK_CASE
+    ++s;
   }
+  for (; s < nst; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nst) issue(s + 1);
+    const double* As = lds + (s & 1) * AS;
+    switch (ws) {
+      SYRK_CASES(SYRK_CASE, 0)
+      SYRK_CASES(SYRK_CASE, 1)
+      SYRK_CASES(SYRK_CASE, 2)
+      default: break;
+    }
+  }
+#undef SYRK_CASES
+#undef SYRK_PCASE
+#undef SYRK_CASE
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 }
@@ -669,7 +743,7 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
   v4d acc[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
-  if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc, sl);
+  if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc, sl, skip_rows(a, b));
   store_syrk_blocks(a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD,
                     a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD, acc, sl);
 }
@@ -759,7 +833,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   const int64_t j0 = (int64_t)J * TILE;
   const double* sc = a.scal + b * SCAL;
   const double muf = sc[SC_MUF];
-  const int64_t nrow = (int64_t)sc[SC_NROW];
+  const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
   const int nt = a.nt;
   double* Tp = lds;
   double* Xp = lds + NPACK * BLKD;
@@ -808,6 +882,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
       // waits for all its stages (and the older S loads) and ends in a barrier
+      // (no padding skip here: at J = 1 only, and it keeps the peeled stage out of this kernel)
       syrk_lower8_32(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
@@ -832,7 +907,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   }
   if (t < TILE) {
 #pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr) rsh[tr][t] = (tr < nt && gi < nrow) ? rv[tr] : 0.0;
+    for (int tr = 0; tr < MAXT; ++tr) rsh[tr][t] = (tr < nt && sys_real(gi, pad, nrow)) ? rv[tr] : 0.0;
   }
   dstamp(a, 1);
   __syncthreads();
@@ -998,9 +1073,9 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)Jt * TILE;
   const double* sc = a.scal + b * SCAL;
   const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], sm = sc[SC_SM];
-  const int64_t nrow = (int64_t)sc[SC_NROW];
+  const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
   const int il = 16 * w + (l & 15);
-  const bool ireal = i0 + il < nrow;
+  const bool ireal = sys_real(i0 + il, pad, nrow);
   if (a.kc) {
     // counts issued before the u / z loads landed; exact ints -> fp64 K
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1012,7 +1087,7 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * (cb0 + cb) + (l >> 4) + 4 * r;
         const double v = grm_value(c4[r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
-        acc[cb][r] = (ireal && j0 + cl < nrow) ? v : 0.0;
+        acc[cb][r] = (ireal && sys_real(j0 + cl, pad, nrow)) ? v : 0.0;
       }
     }
     return;
@@ -1039,7 +1114,7 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * cb + (l >> 4) + 4 * r;
         const double v = grm_value(cnt[cb][r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
-        acc[cb][r] = (ireal && j0 + cl < nrow) ? v : 0.0;
+        acc[cb][r] = (ireal && sys_real(j0 + cl, pad, nrow)) ? v : 0.0;
       }
     }
   }
@@ -1067,7 +1142,8 @@ __device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, i
   v4d acc[NCB];
   k_acc<NCB>(a, b, I, Jt, cb0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
   const double* Lb = a.L + b * (int64_t)NT * NT * TT;
-  if (!(a.skip & 64)) gemm1_a32<NCB>(Lb + (int64_t)Jt * NT * TT, Lb + (int64_t)I * NT * TT, J, cb0, lds, acc);
+  if (!(a.skip & 64))
+    gemm1_a32<NCB>(Lb + (int64_t)Jt * NT * TT, Lb + (int64_t)I * NT * TT, J, cb0, lds, acc, skip_rows(a, b));
   double* pd = part_ptr(a, b, I, Jt);
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
@@ -1112,7 +1188,7 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
   const int Ls = ahead_cur ? J - 1 : 0;
   if (J > Ls && !(a.skip & 64))
     gemm1_a32<8>(Lb + (int64_t)J * NT * TT + (int64_t)Ls * TT, Lb + (int64_t)I * NT * TT + (int64_t)Ls * TT, J - Ls, 0,
-                 lds, acc);
+                 lds, acc, Ls == 0 ? skip_rows(a, b) : 0);
 
   // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X in the
   //    packed block layout (blocks transposed): all 36 blocks (72 KiB) land in LDS in one
@@ -1173,7 +1249,7 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
     v4d qa[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) qa[i] = v4d{0.0, 0.0, 0.0, 0.0};
-    syrk_lower8_32(Lout, 8, lds, qa);
+    syrk_lower8_32(Lout, 8, lds, qa, 0, J == 0 ? skip_rows(a, b) : 0);
     store_syrk_blocks(a.q + b * (int64_t)NPACK * BLKD, nullptr, qa, 0);
   }
 }
@@ -1190,7 +1266,7 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
   const int64_t j0 = (int64_t)J * TILE;
   const double* sc = a.scal + b * SCAL;
   const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
-  const int64_t nrow = (int64_t)sc[SC_NROW], nblk = (int64_t)sc[SC_CBLK];
+  const int64_t nrow = (int64_t)sc[SC_NROW], nblk = (int64_t)sc[SC_CBLK], pad = (int64_t)sc[SC_PAD];
   if (t < TILE) u_sh[t] = a.u[b * a.prow + j0 + t];
   double* Kd = a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD;
   v4i cnt[8];
@@ -1245,7 +1321,8 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
         const int cl = 16 * cb + (l >> 4) + 4 * r;
         const int64_t gi = j0 + cl;
         const double kv = grm_value(cnt[cb][r], u_sh[cl], uj, sa, cN, invd, sm);
-        const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
+        const double v = (sys_real(gi, pad, nrow) && sys_real(gj, pad, nrow)) ? kv + ((gi == gj) ? lam : 0.0)
+                                                                              : ((gi == gj) ? 1.0 : 0.0);
         Kd[pk(cb, wc) + bo(cl & 15, il & 15)] = v;
       }
     }
@@ -1450,7 +1527,7 @@ __device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v
   const double* sc = a.scal + b * SCAL;
   const int64_t j0 = (int64_t)J * TILE;
   const double sa_ = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
-  const int64_t nrow = (int64_t)sc[SC_NROW];
+  const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
   const double* ub = a.u + b * a.prow + j0;
   double* Kd = a.Kd + (b * a.NT + J) * (int64_t)NPACK * BLKD;
   // every centring sum this lane needs, loaded before the first store (Kd and u are both double
@@ -1475,7 +1552,8 @@ __device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v
         const int cl = 16 * cb + (l >> 4) + 4 * r;
         const int64_t gi = j0 + cl;
         const double kv = grm_value((int32_t)cnt[m][n][r], ur[m][r], uc[n], sa_, cN, invd, sm);
-        const double v = (gi < nrow && gj < nrow) ? kv + ((gi == gj) ? lam : 0.0) : ((gi == gj) ? 1.0 : 0.0);
+        const double v = (sys_real(gi, pad, nrow) && sys_real(gj, pad, nrow)) ? kv + ((gi == gj) ? lam : 0.0)
+                                                                              : ((gi == gj) ? 1.0 : 0.0);
         Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
       }
     }
@@ -1643,7 +1721,8 @@ __device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4]
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.idx, c.off, c.gpk_row, c.d.P, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
-             c.wgt, nullptr, c.kc, c.part, c.q, c.B, c.ft};
+             c.wgt, nullptr, c.kc, c.part, c.q, c.B, c.ft, c.padskip,
+             (c.sd.form == FORM_PRIMAL && c.sd.pad_first) ? 1 : 0};
   return a;
 }
 

@@ -159,7 +159,7 @@ hipError_t launch_fold_offsets(const int64_t* off, int64_t B, int64_t F, int64_t
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
                                                      FoldTab ft, const int32_t* __restrict__ csA, int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
-                                                     int64_t ns, int nt, int branch, double h2,
+                                                     int64_t ns, int pad_first, int nt, int branch, double h2,
                                                      double* __restrict__ scal, double* __restrict__ u,
                                                      double* __restrict__ rhs, int32_t* __restrict__ err) {
   const int64_t b = blockIdx.x;
@@ -210,16 +210,19 @@ __global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__
     sc[SC_NROW] = primal ? (double)k : (double)nT;
     sc[SC_CBLK] = primal ? (double)(nTp / KBLK) : (double)((k + KBLK - 1) / KBLK);
     sc[SC_BAD] = any_bad ? 1.0 : 0.0;
+    sc[SC_PAD] = (primal && pad_first) ? (double)(ns - k) : 0.0;
     invd_sh = 1.0 / d;
   }
   if (!primal) return;
   __syncthreads();
   // u_a = s_a (train allele count), rhs_ta = X_c^T (y_T,t - mu_t) / d = xty[t][p_a] / d
-  // (the sklearn primal right-hand side in 1/d units); zero on padding rows
+  // (the sklearn primal right-hand side in 1/d units); zero on padding rows (system row a holds
+  // selected SNP a - pad)
   const double invd = invd_sh;
+  const int64_t pad = pad_first ? ns - k : 0;
   for (int64_t a = threadIdx.x; a < ns; a += 256) {
-    const bool real = a < k;
-    const int64_t p = real ? snp_col(idx[o0 + a], P) : 0;
+    const bool real = sys_real(a, pad, k);
+    const int64_t p = real ? snp_col(idx[o0 + a - pad], P) : 0;
     u[b * ns + a] = real ? (double)csT[p] : 0.0;
     for (int t = 0; t < nt; ++t) rhs[(b * nt + t) * ns + a] = real ? xty[t * P + p] * invd : 0.0;
   }
@@ -230,7 +233,7 @@ hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B,
                               int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
                               hipStream_t s) {
   hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, ft, colsum_all, d.n,
-                     d.nT, d.nTp, d.P, sd.form, sd.ns, d.nt, branch, h2, scal, u, rhs, err);
+                     d.nT, d.nTp, d.P, sd.form, sd.ns, sd.pad_first, d.nt, branch, h2, scal, u, rhs, err);
   return hipGetLastError();
 }
 

@@ -274,9 +274,10 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   const double* ub = c.u + b * prow;
   const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
   if (c.sd.form == FORM_PRIMAL) {
-    const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b];
-    for (int64_t r = t; r < kk; r += NTH) {
-      rowp[r] = (int32_t)snp_col(c.idx[o0 + r], c.d.P);
+    // system row r holds selected SNP r - pad (leading padding rows: the zero split row P)
+    const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b], pad = (int64_t)sc[SC_PAD];
+    for (int64_t r = t; r < pad + kk; r += NTH) {
+      rowp[r] = (r < pad) ? (int32_t)c.d.P : (int32_t)snp_col(c.idx[o0 + r - pad], c.d.P);
     }
     __syncthreads();
   }
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     // EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu with block J's shares e_J[v] = sum_{a in J}
     // x_va beta_a and mb_J = sum_{a in J} s_a beta_a, J ascending (the chained solve's order),
     // every trait in one pass over the rows
-    const int64_t kk = (int64_t)sc[SC_K];
+    const int64_t kk = (int64_t)sc[SC_K] + (int64_t)sc[SC_PAD];   // rows up to the last real one
     const int rg8 = t & 7;
     const int64_t nq = (nV + 3) / 4;
     double mbt[NTR];
@@ -536,10 +537,15 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   const int NT = c.sd.NT;
   const int64_t ns = c.sd.ns, nV = c.d.nV, nTp = c.d.nTp;
   const double* sc = c.scal + b * SCAL;
-  const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b];
-  const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));   // real SNP rows of block J
+  const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b], pad = (int64_t)sc[SC_PAD];
+  // rows of block J up to the last real one (system row r holds selected SNP r - pad; the leading
+  // padding rows read the zero split row P)
+  const int nr = (int)max((int64_t)0, min((int64_t)TILE, pad + kk - (int64_t)J * TILE));
   for (int i = t; i < NTR * TILE; i += CTH) zsh[i / TILE][i % TILE] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
-  for (int r = t; r < nr; r += CTH) rowp[r] = (int32_t)snp_col(c.idx[o0 + (int64_t)J * TILE + r], c.d.P);
+  for (int r = t; r < nr; r += CTH) {
+    const int64_t g = (int64_t)J * TILE + r;
+    rowp[r] = (g < pad) ? (int32_t)c.d.P : (int32_t)snp_col(c.idx[o0 + g - pad], c.d.P);
+  }
   // X_J's rows rc and rc + 64 before the wait
   const int rc = t >> 3, seg = t & 7;
   const double* Dj = c.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;

@@ -51,7 +51,16 @@ enum {
   SC_NROW = 9,  // real system rows (dual n_T, primal k); the rest is identity padding
   SC_CBLK = 10, // contraction blocks of 64 for the system matrix
   SC_BAD = 11,  // 1 when an index lies outside [-P, P) (numpy would raise IndexError): fitness NaN
+  SC_PAD = 12,  // leading padding rows (SNP form: ns - k, see SysDims::pad_first; kernel form 0)
 };
+// System row r is real (not identity padding) when pad <= r < pad + nrow.  SNP form: real row r
+// holds selected SNP r - pad.  The padding leads so that its exact-zero rows and columns fall at
+// the START of block column 0, where the Cholesky's contractions over L = 0 skip them
+// (gemm1_a32 / syrk_lower8_32 start at row pad); trailing padding would sit in the output rows of
+// the last tile row instead, split unevenly over the waves.
+__host__ __device__ __forceinline__ bool sys_real(int64_t r, int64_t pad, int64_t nrow) {
+  return (uint64_t)(r - pad) < (uint64_t)nrow;
+}
 enum { FORM_DUAL = 0, FORM_PRIMAL = 1 };
 
 // Panel column of a selected-SNP index with numpy's fancy-index rule (the reference's
@@ -71,6 +80,7 @@ struct SysDims {
   int NT;            // ns / TILE
   int64_t prow;      // panel rows per contraction block
   int64_t cblk;      // contraction blocks per individual in the panel (max over the chunk)
+  int pad_first = 0; // SNP form: padding rows lead (SC_PAD = ns - k; TBLUP_PAD_FIRST, default on)
 };
 
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -169,6 +179,7 @@ struct CholLaunch {
   int16_t* kc;           // SNP form: exact off-diagonal system-tile counts from k_sys_tiles, else null
   double* part;          // [2][B][NT][128*128] partial sums of the next column's tiles (ahead schedule)
   double* q;             // last-term mode: [B][36*256] diagonal tile J's last SYRK term, from launch J-1
+  int padskip;           // contractions over block column 0 skip the leading padding rows (SC_PAD)
 };
 // k_sys_tiles output: per individual NT(NT-1)/2 off-diagonal tiles (I > J, t = I(I-1)/2 + J) of
 // 128 x 128 int16 counts, in the order the off-diagonal kernel's lanes read them:
@@ -200,7 +211,7 @@ struct OffPlan {
 //   and thresholds 512 / 1024 were slower at 128), 0 never, 1 always; nrs: 0 auto (fill >= 2 units per CU
 //   slot pair), else fixed 1 / 2 / 4; dual: no k_sys_tiles counts (int8 K in-tile: nrs = 1)
 constexpr int64_t AHEAD_SLOTS = 256;
-OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs);
+OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs, int64_t slots = AHEAD_SLOTS);
 inline int64_t offdiag_grid(const OffPlan& p, int64_t B) { return p.nI > 0 ? B * p.units() + p.n_kd : 0; }
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
 // then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.

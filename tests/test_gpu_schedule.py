@@ -4,10 +4,11 @@ target's in 1 / 2 block slices) redistribute the same MFMA chains over workgroup
 the two solve kernels (k_solve: one workgroup per individual; k_solve_chain: an individual's
 block rows and tiles over the chip, chosen for small batches) share one arithmetic, and the
 diagonal tile's last SYRK term runs the same MFMA chains whether the diagonal launch or the
-previous launch's tile (J, J-1) workgroup computes it, so fitness
+previous launch's tile (J, J-1) workgroup computes it, and the contractions over block column 0
+skip the SNP form's leading padding rows (exact zeros) or multiply them, so fitness
 and EBVs must be bit-identical under every setting, for both system forms and for system sizes
 from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS / TBLUP_SOLVE_CHAIN /
-TBLUP_LAST_TERM are read when a context is created.)"""
+TBLUP_LAST_TERM / TBLUP_PAD_SKIP / TBLUP_PAD_FIRST are read when a context is created.)"""
 import os
 
 import numpy as np
@@ -28,6 +29,7 @@ SETTINGS = [
     {"TBLUP_SOLVE_CHAIN": "0"},                     # one solve workgroup per individual
     {"TBLUP_LAST_TERM": "1"},                       # diagonal's last SYRK term in the previous launch
     {"TBLUP_LAST_TERM": "0"},                       # ... in the diagonal launch
+    {"TBLUP_PAD_SKIP": "0"},                        # SNP form: leading padding rows multiplied, not skipped
 ]
 
 
@@ -95,3 +97,21 @@ def test_schedules_small_batches_and_traits(panel, gpu):
             b = _evaluate(panel["geno"], None, genomes, panel["T"], panel["V"], env, multi=multi)
             np.testing.assert_array_equal(a[0], b[0], err_msg=str(env))
             np.testing.assert_array_equal(a[1], b[1], err_msg=str(env))
+
+
+def test_leading_padding_matches_trailing(panel, gpu):
+    """SNP form: padding rows leading the system (the default: the contractions over block column 0
+    skip them) or trailing it (TBLUP_PAD_FIRST=0) -- the same systems with moved block boundaries,
+    so equal up to rounding, and both equal to the oracle.  Batches with one k (pad 24 < 128) and
+    with mixed k (pads up to 896: whole padding tiles skipped)."""
+    rng = np.random.default_rng(8)
+    groups = [[rng.choice(20_000, 1000, replace=False) for _ in range(5)],
+              [rng.choice(20_000, k, replace=False) for k in (128, 1000, 777, 1024, 901, 420)]]
+    genomes = [g for grp in groups for g in grp]
+    lead = _evaluate(panel["geno"], panel["pheno"], groups, panel["T"], panel["V"], {})
+    trail = _evaluate(panel["geno"], panel["pheno"], groups, panel["T"], panel["V"], {"TBLUP_PAD_FIRST": "0"})
+    np.testing.assert_allclose(lead[0], trail[0], rtol=0, atol=1e-11)
+    np.testing.assert_allclose(lead[1], trail[1], rtol=1e-9, atol=1e-9)
+    for i in range(len(genomes)):
+        f, _ = O.blup_grm_form(genomes[i], panel["T"], panel["V"], panel["geno"], panel["pheno"], 0.4)
+        assert abs(lead[0][i] - f) <= 1e-9, i
