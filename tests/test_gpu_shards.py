@@ -123,3 +123,37 @@ def test_bench_multi_rank_rehearsal(gpu, tmp_path):
     assert l2["n_gpus"] == 2 and l2["config"]["pop_total"] == 1024 and l2["config"]["pop_per_gpu"] == 512
     assert l2["scaling"] == "strong"
     assert l1["fitness_checksum"] == l2["fitness_checksum"]
+
+
+RCCL_SNIPPET = r"""
+import os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["TBLUP_ROOT"])
+from tblup_amd import distributed as td
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+assert td.backend_name() == "RCCL"
+loc = torch.arange(5, dtype=torch.float64, device="cuda") * 0.5
+out = torch.empty(5, dtype=torch.float64, device="cuda")
+td.allgather_device(out, loc)
+torch.cuda.synchronize()
+assert torch.equal(out.cpu(), loc.cpu())
+full = td.allgather_fitness(np.array([0.25, -1.0, 3.0]), 3, device=0)
+assert np.array_equal(full, [0.25, -1.0, 3.0])
+td.destroy()
+print("rccl ok")
+"""
+
+
+def test_rccl_all_gather_on_device(gpu):
+    """The multi-GPU path's collective on this box's GPU: an RCCL (backend "nccl") group of one
+    rank, all_gather_into_tensor through `allgather_device` and `allgather_fitness` on device
+    memory -- the RCCL library, its device-side init and the collective run on hardware (the 2-
+    and 4-rank tests above share one GPU, which RCCL does not allow, so they use gloo)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0", TBLUP_ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", RCCL_SNIPPET], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "rccl ok" in r.stdout
