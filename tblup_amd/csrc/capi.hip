@@ -102,6 +102,7 @@ struct tblup_ctx {
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
   int64_t ahead_slots = AHEAD_SLOTS;   // TBLUP_AHEAD_SLOTS: the auto rule's threshold (A/B timing)
+  int diag_d = -1;    // TBLUP_DIAG_D: D-units in the diagonal launch (-1 auto, 0 never, 1 always)
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
   int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (B <= LT_MAX_B), 0 never, 1 always (see use_last_term)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
@@ -230,7 +231,7 @@ static double list_makespan(std::initializer_list<std::pair<double, int64_t>> cl
   return end;
 }
 
-OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol, int64_t slots) {
+OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol, int64_t slots, int diag_d) {
   OffPlan p{};
   p.nI = NT - J - 1;
   if (p.nI <= 0) {
@@ -245,7 +246,13 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   };
   p.nP = ahead_at(J) ? NT - 2 - J : 0;
   p.ahead_cur = (J >= 2 && ahead_at(J - 1)) ? 1 : 0;
-  const int dt = (J >= 1 && J + 1 < NT) ? 1 : 0;   // diagonal target J + 1 (its partial over L < J)
+  int dt = (J >= 1 && J + 1 < NT) ? 1 : 0;   // diagonal target J + 1 (its partial over L < J)
+  // small batches: the D-units in the diagonal launch J (its B workgroups leave 256 - B CUs idle
+  // for ~45 us; a D-unit alone on a CU sums J / 2 SYRK terms, so J <= DD_MAX_J keeps it shorter)
+  if (dt && (diag_d == 1 || (diag_d < 0 && B > DD_MIN_B && B <= DD_MAX_B && J <= DD_MAX_J))) {
+    p.ndd = 1;
+    dt = 0;
+  }
   p.nrs = 1;
   p.nds = dt;
   // Row slices of the P-units (they need k_sys_tiles' counts: the int8 K is a whole-tile
@@ -284,7 +291,7 @@ namespace {
 
 bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
   for (int J = 0; J < NT; ++J)
-    if (off_plan(B, NT, J, st, c->ahead, c->nrs, c->ahead_slots).nP > 0) return true;
+    if (off_plan(B, NT, J, st, c->ahead, c->nrs, c->ahead_slots, c->diag_d).nP > 0) return true;
   return false;
 }
 
@@ -442,7 +449,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   int16_t* kcd = fold_share ? cv.take<int16_t>((size_t)B * sd.NT * KC_TILE) : nullptr;
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
-  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, c->ahead_slots);
+  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, c->ahead_slots, c->diag_d);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
@@ -478,7 +485,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   uint64_t* wgt = nullptr;
   if (c->wg_trace) {
     int64_t nwg = 0;
-    for (int J = 0; J < sd.NT; ++J) nwg += B + DTR_RECS + offdiag_grid(plan[J], B);
+    for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
     if (use_chain(c, sd, B)) nwg += B * sd.NT * (sd.NT + 1) / 2;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
@@ -519,13 +526,15 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
     // forward-substitution GEMV (the exact system tiles are counted under KC_GRM)
     const double lt_d = Qb ? 0.0 : std::min(jt, 1.0);   // the last SYRK term's share of this launch
-    const double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt);
-    const double bd = Bd * (TILE * TILE * lt_d * 8.0 + 2.0 * TILE * TILE * 8.0);
+    // (+ the D-units when they run in this launch: 128^3 per L < J, as in the off-diagonal launch)
+    const double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt) + (p.ndd ? Bd * T3 * jt : 0.0);
+    const double bd = Bd * (TILE * TILE * lt_d * 8.0 + 2.0 * TILE * TILE * 8.0) +
+                      (p.ndd ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
-      c->wgt_used += B + DTR_RECS;
+      c->wgt_used += B * (1 + p.ndd) + DTR_RECS;
     }
-    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, s); });
+    rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, p, s); });
     if (rc) return rc;
     if (p.nI > 0) {
       // T-units: GEMM1 over the L not summed ahead (2*128^3 each) + the triangular solve 128^3;
@@ -640,6 +649,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_AHEAD_SLOTS")) c->ahead_slots = std::max(0, atoi(e));
+  if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_PAD_SKIP")) c->pad_skip = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;

@@ -1035,8 +1035,16 @@ __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
   __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
   __shared__ double rsh[MAXT][TILE];
   WgTrace tr(a.wgt);
+  if ((int64_t)blockIdx.x >= a.B) {
+    // OffPlan::ndd: the D-unit of diagonal target J+1 (S = K - sum_{L<J}), on a CU the diagonal
+    // workgroups (dispatched first) leave idle; blocks B + x and x share an XCD when 8 | B
+    const int64_t b = xcd_remap(blockIdx.x - a.B, gridDim.x - a.B);
+    syrk_partial8(a, b, a.J + 1, a.J, lds, 0);
+    tr.done(WGT_DPREP, a.J, a.J + 1, b);
+    return;
+  }
   // individual b on the XCD that runs its off-diagonal tiles (same L2 for L, S, X, w)
-  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t b = xcd_remap(blockIdx.x, a.B);
   diag_tile(a, b, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
   tr.done(WGT_DIAG, a.J, a.J, b);
 }
@@ -1758,11 +1766,12 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s) {
+hipError_t launch_chol_diag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s) {
   CholArgs a = make_args(c, J);
-  // profiling: the phase stamps of this launch follow its B workgroup records
-  if (c.wgt) a.dtr = c.wgt + c.B * WGT_REC;
-  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)c.B), dim3(DTHR), 0, s, a);
+  const int64_t nwg = c.B * (1 + p.ndd);
+  // profiling: the phase stamps of this launch follow its workgroup records
+  if (c.wgt) a.dtr = c.wgt + nwg * WGT_REC;
+  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)nwg), dim3(DTHR), 0, s, a);
   return hipGetLastError();
 }
 

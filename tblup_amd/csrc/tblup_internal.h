@@ -192,15 +192,18 @@ constexpr int WGT_REC = 4;
 // a diagonal launch's records are followed by DTR_RECS records holding the phase stamps of
 // its workgroup 0 (8 waves x 64 uint64), written as kind-0 records
 constexpr int DTR_RECS = 8 * 64 / WGT_REC;
-enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_PART = 6 };
+enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_PART = 6, WGT_DPREP = 7 };
 // Work units of the off-diagonal launch of column J, per individual (k_chol.hip):
 //   nI  T-units: tiles (I, J), I > J
 //   nP  x nrs P-units (ahead schedule): partial sums K - sum_{L<J} of tiles (I, J+1), I >= J+2, in
 //       nrs row slices -- launch J+1's T-units then start from them (ahead_cur) and sum one L
 //   nds D-units: the diagonal tile J+1's partial sum over L < J (1 or 2 block slices)
 //   n_kd K_JJ workgroups (column 0 of the kernel form only)
+//   ndd: the D-units run in the DIAGONAL launch J instead (whole, one per individual; nds = 0), on
+//   the CUs its B workgroups leave idle -- they need only the columns L < J, complete before it
 struct OffPlan {
   int nI, nP, nrs, nds, ahead_cur;
+  int ndd;
   int64_t n_kd;
   __host__ __device__ int64_t units() const { return (int64_t)nP * nrs + nds + nI; }
 };
@@ -211,11 +214,19 @@ struct OffPlan {
 //   and thresholds 512 / 1024 were slower at 128), 0 never, 1 always; nrs: 0 auto (fill >= 2 units per CU
 //   slot pair), else fixed 1 / 2 / 4; dual: no k_sys_tiles counts (int8 K in-tile: nrs = 1)
 constexpr int64_t AHEAD_SLOTS = 256;
-OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs, int64_t slots = AHEAD_SLOTS);
+// diag_d: D-units in the diagonal launch, -1 auto (DD_MIN_B < B <= DD_MAX_B and J <= DD_MAX_J), 0 never,
+// 1 always.  Measured (config 2, A/B): pop 128 +2.4% (off-diagonal -49 us, diagonal +11 us per step);
+// pop 64 -0.8%, pop 32 -1.5% (their off-diagonal launches are bound by other units, and the diagonal
+// launches still grow); every J (TBLUP_DIAG_D=1): diagonal +100 us at pop 128
+constexpr int64_t DD_MIN_B = 64;
+constexpr int64_t DD_MAX_B = 128;
+constexpr int DD_MAX_J = 3;
+OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs, int64_t slots = AHEAD_SLOTS,
+                 int diag_d = 0);
 inline int64_t offdiag_grid(const OffPlan& p, int64_t B) { return p.nI > 0 ? B * p.units() + p.n_kd : 0; }
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
 // then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.
-hipError_t launch_chol_diag(const CholLaunch& c, int J, hipStream_t s);
+hipError_t launch_chol_diag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s);
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s);
 // all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
