@@ -103,6 +103,7 @@ struct tblup_ctx {
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
   int64_t ahead_slots = AHEAD_SLOTS;   // TBLUP_AHEAD_SLOTS: the auto rule's threshold (A/B timing)
   int diag_d = -1;    // TBLUP_DIAG_D: D-units in the diagonal launch (-1 auto, 0 never, 1 always)
+  int dd_maxj = DD_MAX_J;   // TBLUP_DD_MAXJ: the auto rule's last column (A/B timing)
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
   int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (B <= LT_MAX_B), 0 never, 1 always (see use_last_term)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
@@ -231,7 +232,8 @@ static double list_makespan(std::initializer_list<std::pair<double, int64_t>> cl
   return end;
 }
 
-OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol, int64_t slots, int diag_d) {
+OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol, int64_t slots, int diag_d,
+                        int dd_maxj) {
   OffPlan p{};
   p.nI = NT - J - 1;
   if (p.nI <= 0) {
@@ -249,7 +251,7 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   int dt = (J >= 1 && J + 1 < NT) ? 1 : 0;   // diagonal target J + 1 (its partial over L < J)
   // small batches: the D-units in the diagonal launch J (its B workgroups leave 256 - B CUs idle
   // for ~45 us; a D-unit alone on a CU sums J / 2 SYRK terms, so J <= DD_MAX_J keeps it shorter)
-  if (dt && (diag_d == 1 || (diag_d < 0 && B > DD_MIN_B && B <= DD_MAX_B && J <= DD_MAX_J))) {
+  if (dt && (diag_d == 1 || (diag_d < 0 && B > DD_MIN_B && B <= DD_MAX_B && J <= dd_maxj))) {
     p.ndd = 1;
     dt = 0;
   }
@@ -291,7 +293,7 @@ namespace {
 
 bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
   for (int J = 0; J < NT; ++J)
-    if (off_plan(B, NT, J, st, c->ahead, c->nrs, c->ahead_slots, c->diag_d).nP > 0) return true;
+    if (off_plan(B, NT, J, st, c->ahead, c->nrs, c->ahead_slots, c->diag_d, c->dd_maxj).nP > 0) return true;
   return false;
 }
 
@@ -449,7 +451,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   int16_t* kcd = fold_share ? cv.take<int16_t>((size_t)B * sd.NT * KC_TILE) : nullptr;
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
-  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, c->ahead_slots, c->diag_d);
+  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, c->ahead_slots, c->diag_d, c->dd_maxj);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
@@ -650,6 +652,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_AHEAD_SLOTS")) c->ahead_slots = std::max(0, atoi(e));
   if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_DD_MAXJ")) c->dd_maxj = atoi(e);
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_PAD_SKIP")) c->pad_skip = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;

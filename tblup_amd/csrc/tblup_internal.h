@@ -192,7 +192,7 @@ constexpr int WGT_REC = 4;
 // a diagonal launch's records are followed by DTR_RECS records holding the phase stamps of
 // its workgroup 0 (8 waves x 64 uint64), written as kind-0 records
 constexpr int DTR_RECS = 8 * 64 / WGT_REC;
-enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_PART = 6, WGT_DPREP = 7 };
+enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_PART = 6, WGT_DPREP = 9 };   // 7 / 8: the chained solve (k_solve.hip)
 // Work units of the off-diagonal launch of column J, per individual (k_chol.hip):
 //   nI  T-units: tiles (I, J), I > J
 //   nP  x nrs P-units (ahead schedule): partial sums K - sum_{L<J} of tiles (I, J+1), I >= J+2, in
@@ -222,7 +222,7 @@ constexpr int64_t DD_MIN_B = 64;
 constexpr int64_t DD_MAX_B = 128;
 constexpr int DD_MAX_J = 3;
 OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs, int64_t slots = AHEAD_SLOTS,
-                 int diag_d = 0);
+                 int diag_d = 0, int dd_maxj = DD_MAX_J);
 inline int64_t offdiag_grid(const OffPlan& p, int64_t B) { return p.nI > 0 ? B * p.units() + p.n_kd : 0; }
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
 // then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.

@@ -17,7 +17,7 @@ os.environ["TBLUP_WG_TRACE"] = "1"
 
 import bench  # noqa: E402
 
-KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part"}   # (7 / 8: chained solve, tools/solve_trace.py)
+KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part", 9: "dprep"}   # (7 / 8: chained solve, tools/solve_trace.py)
 
 
 def main():
@@ -38,7 +38,7 @@ def main():
     torch.cuda.synchronize()
     rec = eng.wg_trace()
     raw = eng.wg_trace(raw=True)
-    rec = rec[rec["kind"] <= 7]
+    rec = rec[(rec["kind"] <= 6) | (rec["kind"] == 9)]
     np.save(out, rec)
     np.save(out.replace(".npy", "_raw.npy"), raw)
     props = torch.cuda.get_device_properties(0)
@@ -53,7 +53,7 @@ def main():
         launches.append((rec[sysm]["start"].min(), -1, False, sysm))
     for J in sorted(set(rec["J"].tolist())):
         for is_diag in (True, False):
-            m = (rec["J"] == J) & (((rec["kind"] == 1) | (rec["kind"] == 7)) == is_diag) & ~sysm
+            m = (rec["J"] == J) & (((rec["kind"] == 1) | (rec["kind"] == 9)) == is_diag) & ~sysm
             if not m.any():
                 continue
             launches.append((rec[m]["start"].min(), J, is_diag, m))
