@@ -227,6 +227,9 @@ def main():
     elapsed_events = timed_steps()
     eng.set_profiling(False)
     prof = eng.profile()
+    # every timed evaluation must have succeeded: raises for an index error or an expired
+    # chained-solve wait (tblup_solve_error), never reports a rate over invalid fitnesses
+    eng.check_device_status(stream.cuda_stream)
 
     # GPU genome decode of the same population (RandomKeyIndividual.genome, individual.py:154-156)
     # from device-resident keys: reported beside the metric, not part of it

@@ -111,7 +111,8 @@ int tblup_get_traits(tblup_ctx* ctx, int64_t* n_traits);
  *   fitness  : out, batch doubles, |pearson(EBV_V, y_V)| (NaN when undefined)
  *   ebv      : optional out (may be NULL), batch x n_valid predicted breeding values
  *              (batch x n_traits x n_valid after tblup_set_traits)
- * Synchronous; host pointers.
+ * Synchronous; host pointers.  TBLUP_ERR_STATE if a chained-solve hand-off wait expired
+ * (tblup_solve_error); the outputs are then invalid.
  */
 int tblup_eval_batch(tblup_ctx* ctx, int split_id, const int64_t* idx, const int64_t* offsets,
                      int64_t batch, double h2, int branch, double* fitness, double* ebv);
@@ -286,6 +287,21 @@ int tblup_de_donors(int strategy, int64_t pop, int64_t L, int32_t best, uint32_t
  * stream), sets *flag = 1 if any individual evaluated since the last call had an index
  * outside [-n_snps, n_snps) (its fitness is NaN), and clears the flag. */
 int tblup_index_error(tblup_ctx* ctx, void* stream, int* flag);
+
+/* Solve-error flag: the chained back substitution (SNP form, small batches) hands block rows
+ * between workgroups and bounds every wait; a wait that gives up leaves the batch's fitnesses
+ * invalid.  The synchronous entries (tblup_eval_batch, tblup_eval_folds) then fail with
+ * TBLUP_ERR_STATE; after device entries read the flag here: synchronises `stream` (NULL = the
+ * context's stream), *flag = 1 if a wait expired since the last read, clears it.  (The reference
+ * has no such failure mode -- a dead worker hangs its parent, tblup/evaluator.py:397-398; here it
+ * is an error, never a silent NaN.) */
+int tblup_solve_error(tblup_ctx* ctx, void* stream, int* flag);
+
+/* Both status words without synchronising: enqueues on `stream` (NULL = the context's stream) a
+ * copy of {index error, solve error} (2 x int32, nonzero = raised) into `host_status`
+ * (page-locked host memory) and clears them on the device; valid once the stream has passed
+ * that point (the caller's event). */
+int tblup_status_async(tblup_ctx* ctx, void* stream, int32_t* host_status);
 
 /* Device memory currently held by the context (bytes). */
 int tblup_mem_info(tblup_ctx* ctx, int64_t* bytes_in_use);

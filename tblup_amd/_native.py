@@ -18,6 +18,8 @@ MAX_TRAITS = 4
 ERR_STATE = -4   # TBLUP_ERR_STATE: call out of order
 ERR_INDEX = -5   # TBLUP_ERR_INDEX: numpy's IndexError for data[:, indices]
 KCLASS_NAMES = ("stats", "gather", "grm", "chol_diag", "chol_offdiag", "solve")
+CHAIN_EXPIRED = ("chained solve: a block-row hand-off wait expired (CHAIN_SPIN_MAX polls); the affected "
+                 "individuals' fitnesses are invalid")
 
 # Every symbol of include/tblup_gpu.h with (restype, argtypes).
 _c = ctypes
@@ -48,6 +50,8 @@ SIGNATURES = {
     "tblup_debug_grm": (_c.c_int, [_P, _c.c_int, _I64P, _c.c_int64, _c.c_double, _c.c_int, _c.c_int, _DP, _DP]),
     "tblup_mem_info": (_c.c_int, [_P, _I64P]),
     "tblup_index_error": (_c.c_int, [_P, _P, _c.POINTER(_c.c_int)]),
+    "tblup_solve_error": (_c.c_int, [_P, _P, _c.POINTER(_c.c_int)]),
+    "tblup_status_async": (_c.c_int, [_P, _P, _P]),
     "tblup_get_wg_trace": (_c.c_int, [_P, _c.POINTER(_c.c_uint64), _c.c_int64, _I64P]),
     "tblup_decode_topk": (_c.c_int, [_P, _DP, _c.c_int64, _c.c_int64, _I64P, _I64P]),
     "tblup_decode_topk_device": (_c.c_int, [_P, _P, _c.c_int64, _c.c_int64, _c.c_int64, _P, _I64P, _P, _P]),

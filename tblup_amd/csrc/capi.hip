@@ -67,7 +67,8 @@ struct tblup_ctx {
   hipStream_t stream = nullptr;
   int64_t n = 0, P = 0;
   DevBuf geno_sm, colsum_all, scratch;
-  DevBuf idx_err;              // int32 device flag: an index outside [-P, P) reached k_indiv_stats
+  DevBuf status;               // int32 [ST_WORDS] device status words: ST_INDEX an index outside
+                               // [-P, P) reached k_indiv_stats; ST_SOLVE a chained-solve wait expired
   std::vector<double> pheno;   // [n][nt] animal-major
   int nt = 1;                  // traits (tblup_set_traits)
   std::map<int, std::unique_ptr<Split>> splits;
@@ -101,9 +102,7 @@ struct tblup_ctx {
   // Cholesky schedule (results are bit-identical under every setting; see OffPlan):
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
-  int64_t ahead_slots = AHEAD_SLOTS;   // TBLUP_AHEAD_SLOTS: the auto rule's threshold (A/B timing)
   int diag_d = -1;    // TBLUP_DIAG_D: D-units in the diagonal launch (-1 auto, 0 never, 1 always)
-  int dd_maxj = DD_MAX_J;   // TBLUP_DD_MAXJ: the auto rule's last column (A/B timing)
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
   int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (B <= LT_MAX_B), 0 never, 1 always (see use_last_term)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
@@ -111,13 +110,15 @@ struct tblup_ctx {
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
   int fold_share = 1;    // TBLUP_FOLD_SHARE: 0 builds every fold's system tiles from its own rows
   // SNP form: the padding rows (ns - k) lead the system, so the contractions over block column 0
-  // skip them (TBLUP_PAD_FIRST=0: trailing padding; TBLUP_PAD_SKIP=0: leading padding, no skip --
-  // bit-identical to the skip).  A/B knobs only.
+  // skip them (TBLUP_PAD_FIRST=0: trailing padding, equal up to rounding -- a test knob).
   int pad_first = 1;
-  int pad_skip = 1;
   std::vector<int64_t> fold_hoff;   // host offsets of the last fold-fused chunk (host-side shapes only)
   DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
   int32_t chain_seq = 0; // flag value of the last chained solve
+  bool chain_used = false;   // a chained solve was enqueued since the status was last read
+  // debug knob (TBLUP_CHAIN_DEBUG="spin,delay,shots"): the next `shots` chained solves poll at
+  // most `spin` times and delay one producer by `delay` sleep rounds -- forces an expiry (tests)
+  int32_t chain_dbg_spin = 0, chain_dbg_delay = 0, chain_dbg_shots = 0;
 };
 
 namespace {
@@ -200,14 +201,10 @@ struct Carve {
 };
 
 // SNP (primal) form: the batched system-tile launch (k_sys_tiles) builds every exact tile up
-// front; int16 counts stay exact while n_T <= KC_MAX_NT.  TBLUP_SYS_TILES=0 keeps the in-tile
-// int8 path (A/B timing).
+// front; int16 counts stay exact while n_T <= KC_MAX_NT (beyond it, and for one-tile systems, the
+// in-tile int8 products of the off-diagonal kernel).
 bool sys_tiles(const EvalDims& d, const SysDims& sd) {
-  static const int env = [] {
-    const char* e = getenv("TBLUP_SYS_TILES");
-    return e ? atoi(e) : 1;
-  }();
-  return env != 0 && sd.form == FORM_PRIMAL && d.nT <= KC_MAX_NT && sd.NT >= 2;
+  return sd.form == FORM_PRIMAL && d.nT <= KC_MAX_NT && sd.NT >= 2;
 }
 
 }  // namespace
@@ -293,7 +290,7 @@ namespace {
 
 bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
   for (int J = 0; J < NT; ++J)
-    if (off_plan(B, NT, J, st, c->ahead, c->nrs, c->ahead_slots, c->diag_d, c->dd_maxj).nP > 0) return true;
+    if (off_plan(B, NT, J, st, c->ahead, c->nrs, AHEAD_SLOTS, c->diag_d).nP > 0) return true;
   return false;
 }
 
@@ -451,12 +448,13 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   int16_t* kcd = fold_share ? cv.take<int16_t>((size_t)B * sd.NT * KC_TILE) : nullptr;
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
-  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, c->ahead_slots, c->diag_d, c->dd_maxj);
+  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, AHEAD_SLOTS, c->diag_d);
   const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
   rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
-    return launch_indiv_stats(d_idx, d_off, B, ft, csA, d, sd, branch, h2, scal, u, rhs, (int32_t*)c->idx_err.p, s);
+    return launch_indiv_stats(d_idx, d_off, B, ft, csA, d, sd, branch, h2, scal, u, rhs,
+                              (int32_t*)c->status.p + ST_INDEX, s);
   });
   if (rc) return rc;
   if (sd.form == FORM_DUAL) {
@@ -481,7 +479,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, panel, pstride, d_off, d_idx,
                 d.nRp, d.nRp / 4, ft, u, scal, c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
                 Pp, Qb};
-  cl.padskip = (sd.form == FORM_PRIMAL && sd.pad_first && c->pad_skip) ? 1 : 0;
+  cl.padskip = (sd.form == FORM_PRIMAL && sd.pad_first) ? 1 : 0;
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
@@ -577,8 +575,17 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     ch.epart = cv.take<double>((size_t)B * sd.NT * d.nt * d.nV);
     ch.mbpart = cv.take<double>((size_t)B * sd.NT * d.nt);
     if (int rc2 = ws_check(c, cv)) return rc2;
+    ch.expired = (int32_t*)c->status.p + ST_SOLVE;
     ch.seq = ++c->chain_seq;
     ch.mode = c->chain_sync;
+    ch.spin_max = CHAIN_SPIN_MAX;
+    ch.delay = 0;
+    if (c->chain_dbg_shots > 0) {
+      --c->chain_dbg_shots;
+      ch.spin_max = c->chain_dbg_spin;
+      ch.delay = c->chain_dbg_delay;
+    }
+    c->chain_used = true;
     chp = &ch;
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
@@ -592,6 +599,22 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
 int check_ctx(tblup_ctx* c) {
   if (!c) return fail(TBLUP_ERR_ARG, "null context");
   return 0;
+}
+
+const char* const kChainExpired =
+    "chained solve: a block-row hand-off wait expired (CHAIN_SPIN_MAX polls); the affected "
+    "individuals' fitnesses are invalid";
+
+// Synchronous entries, after their last synchronisation: fail the call if a chained solve it ran
+// gave up a wait (the status word is sticky on the device; reading clears it).
+int check_chain_status(tblup_ctx* c) {
+  if (!c->chain_used || !c->status.p) return 0;
+  c->chain_used = false;
+  int32_t h = 0;
+  HIPCHK(hipMemcpy(&h, (int32_t*)c->status.p + ST_SOLVE, 4, hipMemcpyDeviceToHost));
+  if (h == 0) return 0;
+  HIPCHK(hipMemset((int32_t*)c->status.p + ST_SOLVE, 0, 4));
+  return fail(TBLUP_ERR_STATE, kChainExpired);
 }
 
 Split* find_split(tblup_ctx* c, int id) {
@@ -650,12 +673,17 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
-  if (const char* e = getenv("TBLUP_AHEAD_SLOTS")) c->ahead_slots = std::max(0, atoi(e));
   if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
-  if (const char* e = getenv("TBLUP_DD_MAXJ")) c->dd_maxj = atoi(e);
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
-  if (const char* e = getenv("TBLUP_PAD_SKIP")) c->pad_skip = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
+  if (const char* e = getenv("TBLUP_CHAIN_DEBUG")) {
+    int sp = 0, dl = 0, sh = 0;
+    if (sscanf(e, "%d,%d,%d", &sp, &dl, &sh) == 3 && sp > 0 && dl >= 0 && sh > 0) {
+      c->chain_dbg_spin = sp;
+      c->chain_dbg_delay = dl;
+      c->chain_dbg_shots = sh;
+    }
+  }
   if (!panel) {
     *out = c.release();
     return 0;
@@ -663,8 +691,8 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   const size_t gbytes = (size_t)n * (size_t)P;
   if (int rc = dev_alloc(c.get(), c->geno_sm, gbytes)) return rc;
   if (int rc = dev_alloc(c.get(), c->colsum_all, (size_t)P * 4)) return rc;
-  if (int rc = dev_alloc(c.get(), c->idx_err, 4)) return rc;
-  HIPCHK(hipMemsetAsync(c->idx_err.p, 0, 4, c->stream));
+  if (int rc = dev_alloc(c.get(), c->status, ST_WORDS * 4)) return rc;
+  HIPCHK(hipMemsetAsync(c->status.p, 0, ST_WORDS * 4, c->stream));
   if (layout == TBLUP_LAYOUT_SNP_MAJOR) {
     HIPCHK(hipMemcpyAsync(c->geno_sm.p, geno, gbytes, hipMemcpyHostToDevice, c->stream));
   } else {
@@ -699,7 +727,7 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   }
   c->geno_sm.release();
   c->colsum_all.release();
-  c->idx_err.release();
+  c->status.release();
   c->scratch.release();
   c->ws.release();
   c->wgt.release();
@@ -902,6 +930,7 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
     HIPCHK(hipStreamSynchronize(c->stream));
     b0 = b1;
   }
+  if (int rc = check_chain_status(c)) return rc;
   if (c->profiling) return drain_events(c);
   return 0;
 }
@@ -1121,6 +1150,7 @@ int tblup_eval_folds(tblup_ctx* c, const int* split_ids, int n_splits, const int
     HIPCHK(hipStreamSynchronize(c->stream));
     b0 = b1;
   }
+  if (int rc = check_chain_status(c)) return rc;
   if (c->profiling) return drain_events(c);
   return 0;
 }
@@ -1498,19 +1528,38 @@ int tblup_get_wg_trace(tblup_ctx* c, uint64_t* out, int64_t cap, int64_t* n_reco
   return 0;
 }
 
-int tblup_index_error(tblup_ctx* c, void* stream, int* flag) {
+static int read_status_word(tblup_ctx* c, void* stream, int* flag, int word) {
   g_err.clear();
   if (int rc = check_ctx(c)) return rc;
   if (!flag) return fail(TBLUP_ERR_ARG, "null flag");
   *flag = 0;
-  if (!c->idx_err.p) return 0;
+  if (!c->status.p) return 0;
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   int32_t h = 0;
-  HIPCHK(hipMemcpyAsync(&h, c->idx_err.p, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemsetAsync(c->idx_err.p, 0, 4, s));
+  int32_t* w = (int32_t*)c->status.p + word;
+  HIPCHK(hipMemcpyAsync(&h, w, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemsetAsync(w, 0, 4, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (word == ST_SOLVE) c->chain_used = false;
   *flag = h != 0;
+  return 0;
+}
+
+int tblup_index_error(tblup_ctx* c, void* stream, int* flag) { return read_status_word(c, stream, flag, ST_INDEX); }
+
+int tblup_solve_error(tblup_ctx* c, void* stream, int* flag) { return read_status_word(c, stream, flag, ST_SOLVE); }
+
+int tblup_status_async(tblup_ctx* c, void* stream, int32_t* host_status) {
+  g_err.clear();
+  if (int rc = check_ctx(c)) return rc;
+  if (!host_status) return fail(TBLUP_ERR_ARG, "null host_status");
+  if (!c->status.p) return fail(TBLUP_ERR_STATE, "context has no genotype panel");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  HIPCHK(hipMemcpyAsync(host_status, c->status.p, ST_WORDS * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemsetAsync(c->status.p, 0, ST_WORDS * 4, s));
+  c->chain_used = false;
   return 0;
 }
 

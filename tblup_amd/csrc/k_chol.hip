@@ -266,7 +266,7 @@ struct CholArgs {
   double* q;                // last-term mode: [B][NPACK*BLKD] L_{J,J-1} L_{J,J-1}^T, from launch J-1's tile (J, J-1)
   int64_t B;                // individuals in the chunk
   FoldTab ft;               // each system's split (ymu, packed rows)
-  int padskip;              // contractions over block column 0 skip the leading padding rows (TBLUP_PAD_SKIP)
+  int padskip;              // contractions over block column 0 skip the leading padding rows (SNP form)
   int padfirst;             // SNP form: padding rows lead (SC_PAD = ns - k)
 };
 

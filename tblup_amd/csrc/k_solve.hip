@@ -403,13 +403,20 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 // workgroup and only the hand-offs stay on the chain.
 // Grid order: for J = NT-1 .. 0: F(., J), then T(., J, I < J).  A unit waits only on units with
 // smaller block ids (F(b, J) on T(b, K > J, J), T(b, J, I) on F(b, J), F(b, 0) on F(b, J > 0)),
-// and each XCD dispatches its share in block-id order, so the waits drain: the waiting unit with
-// the smallest id waits on units that are resident and not waiting.  Waits are bounded
-// (SPIN_MAX polls; one expired wait makes every later wait of the same call give up at once).  Every sum has a
-// fixed order, so the results do not depend on B, the timing or the grid.
+// and each XCD dispatches its share in block-id order, so the waits drain.  Argument: let u be the
+// smallest block id not yet dispatched.  u's XCD is full, and every block resident there has an
+// id < u, so the smallest waiting unit w anywhere has w < u: every unit it waits on (ids < w) is
+// dispatched, and, being smaller than w, is not waiting -- it runs to completion.  Workgroups of
+// other kernels (other streams, other processes) holding CU slots only delay dispatch; they end
+// on their own.  The one assumption is the per-XCD in-order dispatch of one kernel's blocks, an
+// observed hardware behaviour, not a documented guarantee -- hence the bound on every wait:
+// CHAIN_SPIN_MAX polls, after which the unit stores the call's seq into ch.err (every later wait
+// of the same call gives up at once), raises the context's sticky status word ch.expired, and
+// the host entries fail the call with TBLUP_ERR_STATE (device entries: tblup_solve_error /
+// tblup_status_async) -- an error, never a silent NaN fitness.  Every sum has a fixed order, so
+// the results do not depend on B, the timing or the grid.
 // ===========================================================================
 constexpr int CTH = 512;
-constexpr int SPIN_MAX = 1 << 20;
 enum { WGT_SROW = 7, WGT_STILE = 8 };
 
 // profiling only (TBLUP_WG_TRACE): {start, end, kind << 56 | I << 40 | b, J | (first wait done - start) << 16}
@@ -463,19 +470,23 @@ __device__ __forceinline__ void cstore(T* p, T v) {
 }
 
 // The whole workgroup waits until *f == seq (one lane polls).  False: gave up.
-__device__ bool chain_wait(const int32_t* f, int32_t seq, int32_t* err, int* sh, int mode) {
+__device__ bool chain_wait(const int32_t* f, const SolveChain& ch, int* sh) {
+  const int32_t seq = ch.seq;
   if (threadIdx.x == 0) {
     int ok = 1;
     for (int it = 0;; ++it) {
-      const int32_t v = mode == 1 ? __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : cload(f);
+      const int32_t v = ch.mode == 1 ? __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : cload(f);
       if (v == seq) break;
-      if (it >= SPIN_MAX || cload(err) == seq) {   // this call's waits already expired elsewhere
+      if (it >= ch.spin_max || cload(ch.err) == seq) {   // this call's waits already expired elsewhere
         ok = 0;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (!ok) cstore(err, seq);   // the call's sequence number: later calls start unaffected
+    if (!ok) {
+      cstore(ch.err, seq);          // the call's sequence number: later calls start unaffected
+      cstore(ch.expired, (int32_t)1);   // sticky until the host reads it
+    }
     *sh = ok;
   }
   __syncthreads();
@@ -509,7 +520,7 @@ __device__ void chain_tile(const CholLaunch& c, const SolveChain& ch, int64_t b,
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[h][e] = *reinterpret_cast<const v2d*>(tile + (rc + 64 * h) * TILE + 2 * e);
-  if (!chain_wait(flag_beta(ch, b, NT, J), ch.seq, ch.err, sh, ch.mode)) return;
+  if (!chain_wait(flag_beta(ch, b, NT, J), ch, sh)) return;
   tr_.waited();
   for (int i = t; i < NTR * TILE; i += CTH) bsh[i / TILE][i % TILE] = cload(ch.beta + (b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE);
   __syncthreads();
@@ -554,7 +565,7 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
 #pragma unroll
   for (int h = 0; h < 2; ++h) xok[h] = xrow_load(Dj, rc + 64 * h, seg, xr[h]);
   for (int K = J + 1; K < NT; ++K)
-    if (!chain_wait(flag_part(ch, b, NT, J, K), ch.seq, ch.err, sh, ch.mode)) {
+    if (!chain_wait(flag_part(ch, b, NT, J, K), ch, sh)) {
       if (J == 0 && t == 0) fit[b] = __builtin_nan("");
       return;
     }
@@ -577,6 +588,9 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
         cstore(ch.beta + (b * NTR + tr) * ns + (int64_t)J * TILE + rc + 64 * h, s2[tr]);
         bsh[tr][rc + 64 * h] = s2[tr];
       }
+  }
+  if (ch.delay > 0 && b == 0 && J == NT - 1) {   // debug knob (expiry test): a late producer
+    for (int i = 0; i < ch.delay; ++i) __builtin_amdgcn_s_sleep(127);
   }
   chain_publish(flag_beta(ch, b, NT, J), ch.seq, ch.mode);
 
@@ -611,7 +625,7 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   }
   // F(b, 0): EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu, J ascending; then the fitness
   for (int K = 1; K < NT; ++K)
-    if (!chain_wait(flag_e(ch, b, NT, K), ch.seq, ch.err, sh, ch.mode)) {
+    if (!chain_wait(flag_e(ch, b, NT, K), ch, sh)) {
       if (t == 0) fit[b] = __builtin_nan("");
       return;
     }

@@ -191,6 +191,39 @@ class GpuBlupEngine:
             self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(flag)))
         return bool(flag.value)
 
+    def solve_error(self, stream_ptr=None):
+        """True if a chained-solve hand-off wait expired in a device-entry evaluation since the
+        last call (those fitnesses are invalid); synchronises the stream, clears the flag."""
+        self._settle()
+        flag = ctypes.c_int(0)
+        _native.check("tblup_solve_error", self._lib.tblup_solve_error(
+            self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(flag)))
+        return bool(flag.value)
+
+    def check_device_status(self, stream_ptr=None):
+        """Raise for a device-entry evaluation that failed: TblupIndexError for an index outside
+        [-P, P) (numpy's IndexError), TblupError for an expired chained-solve wait."""
+        if self.index_error(stream_ptr):
+            raise _native.TblupIndexError("tblup_eval_batch_device", _native.ERR_INDEX,
+                                          "an index is out of bounds for axis 1 with size %d" % self.n_snps)
+        if self.solve_error(stream_ptr):
+            raise _native.TblupError("tblup_eval_batch_device", _native.ERR_STATE, _native.CHAIN_EXPIRED)
+
+    def status_async(self, host_status, stream_ptr=None):
+        """Enqueue the copy of the device status words {index error, solve error} into the
+        page-locked int32 tensor `host_status` (and clear them); read it after the stream's event."""
+        _native.check("tblup_status_async", self._lib.tblup_status_async(
+            self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.c_void_p(host_status.data_ptr())))
+
+    @staticmethod
+    def raise_status(status, fn="tblup_eval_batch_device", n_snps=None):
+        """Raise for nonzero status words read through status_async."""
+        if int(status[0]):
+            raise _native.TblupIndexError(fn, _native.ERR_INDEX, "an index is out of bounds for axis 1"
+                                          + ("" if n_snps is None else " with size %d" % n_snps))
+        if int(status[1]):
+            raise _native.TblupError(fn, _native.ERR_STATE, _native.CHAIN_EXPIRED)
+
     def decode_randkey(self, keys, lengths):
         """RandomKeyIndividual.genome for a batch (individual.py:154-156) on the GPU:
         row i -> np.argsort(keys[i])[-int(lengths[i]):] (ascending key order; equal keys
@@ -293,8 +326,9 @@ class GpuBlupEngine:
     def eval_keys_async(self, keys, lengths, train, valid, h2):
         """RandomKey individuals' fitness straight from a device tensor of their keys (B x ld
         float64 on this context's device): decode (k_decode_topk) and evaluation enqueued on a
-        stream of this engine without waiting.  Returns (event, pinned host fitness tensor);
-        the result is valid once the event has completed.  Later calls on the engine wait for it."""
+        stream of this engine without waiting.  Returns (event, pinned host fitness tensor, pinned
+        status words); both are valid once the event has completed (raise_status(status) then
+        raises for a failed evaluation).  Later calls on the engine wait for it."""
         import torch
         self._settle()
         B, ld = keys.shape
@@ -317,10 +351,12 @@ class GpuBlupEngine:
                                  stream_ptr=st.cuda_stream)
             host = torch.empty(B, dtype=torch.float64, pin_memory=True)
             host.copy_(d_fit, non_blocking=True)
+            status = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+            self.status_async(status, st.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(st)
         self._pending = (ev, (keys, d_off, d_idx, d_fit, offsets))
-        return ev, host
+        return ev, host, status
 
     # --------------------------------------------------------------- profiling
     def set_profiling(self, enable=True):

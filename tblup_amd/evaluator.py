@@ -267,9 +267,9 @@ class BlupParallelEvaluator(ParallelEvaluator):
         if not all(1 <= k <= min(L, 8192) for k in lens) or keys.device.index != self.engine.device:
             return False
         train, valid = self.train_validation_indices(generation)
-        event, host = self.engine.eval_keys_async(keys, lens, train, valid, self.h2)
+        event, host, status = self.engine.eval_keys_async(keys, lens, train, valid, self.h2)
         self._spec = {"generation": generation, "keys": keys, "lens": lens, "event": event, "host": host,
-                      "inds": None}
+                      "status": status, "inds": None}
         return True
 
     def _spec_bind(self, children):
@@ -291,6 +291,7 @@ class BlupParallelEvaluator(ParallelEvaluator):
         if any(h is None or h[0] is not spec["keys"] or h[1] != i for i, h in enumerate(hits)):
             return None
         spec["event"].synchronize()
+        self.engine.raise_status(spec["status"].numpy(), n_snps=self.engine.n_snps)
         return spec["host"].numpy().copy()
 
     def evaluate(self, previous_population, next_population, generation):

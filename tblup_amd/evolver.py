@@ -257,6 +257,25 @@ class _RowBlocks:
     def __init__(self, keep=12):
         self.keep = keep
         self._reg = {}   # id(block) -> weakref(block)
+        self._reserved = set()
+
+    def keep_for(self, nbytes):
+        """Older blocks kept page-locked for blocks of nbytes (about 2 GiB in all)."""
+        return max(1, min(self.keep, (2 << 30) // max(nbytes, 1)))
+
+    def reserve(self, shape):
+        """Pre-size torch's caching host allocator for blocks of `shape`: the steady state holds
+        keep_for + 2 blocks at once (the kept older ones, the current population's, the one being
+        filled), so page-lock that many once now -- otherwise every generation until the pool is
+        full pins a fresh block (~10 ms per 100 MB)."""
+        key = tuple(int(x) for x in shape)
+        if key in self._reserved:
+            return
+        self._reserved.add(key)
+        import torch
+        n = self.keep_for(8 * int(np.prod(key))) + 2
+        bufs = [torch.empty(key, dtype=torch.float64, pin_memory=True) for _ in range(n)]
+        del bufs   # back to the caching allocator, page-locked
 
     def rows(self, block):
         import weakref
@@ -292,7 +311,7 @@ class _RowBlocks:
         few = max(1, len(individuals) // 64)
         # at most `keep` older blocks, fewer when they are large (about 2 GiB page-locked)
         big = max(r().nbytes for r in self._reg.values())
-        keep = max(1, min(self.keep, (2 << 30) // max(big, 1)))
+        keep = self.keep_for(big)
         drop = [k for i, k in enumerate(order) if len(users[k]) <= few or i < len(order) - keep]
         if not drop:
             return
@@ -399,6 +418,8 @@ class _GpuDEEvolver(Evolver):
                 # genomes (views: no host copy); otherwise chunks, each followed by an event, so the
                 # per-row copies of one chunk overlap the transfer of the next
                 block_rows = dtypes is None and n * L * 8 <= _BLOCK_MAX
+                if block_rows:
+                    _BLOCKS.reserve(children.shape)
                 host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
                 nchunk = 1 if block_rows else (8 if n >= 16 else 1)
                 rows = (n + nchunk - 1) // nchunk

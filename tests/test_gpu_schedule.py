@@ -4,12 +4,11 @@ target's in 1 / 2 block slices) redistribute the same MFMA chains over workgroup
 the two solve kernels (k_solve: one workgroup per individual; k_solve_chain: an individual's
 block rows and tiles over the chip, chosen for small batches) share one arithmetic, and the
 diagonal tile's last SYRK term runs the same MFMA chains whether the diagonal launch or the
-previous launch's tile (J, J-1) workgroup computes it, and the contractions over block column 0
-skip the SNP form's leading padding rows (exact zeros) or multiply them, and the diagonal
+previous launch's tile (J, J-1) workgroup computes it, and the diagonal
 target's partial sum runs in the off-diagonal launch or beside the diagonal one, so fitness
 and EBVs must be bit-identical under every setting, for both system forms and for system sizes
 from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS / TBLUP_SOLVE_CHAIN /
-TBLUP_LAST_TERM / TBLUP_PAD_SKIP / TBLUP_PAD_FIRST / TBLUP_DIAG_D are read when a context is created.)"""
+TBLUP_LAST_TERM / TBLUP_PAD_FIRST / TBLUP_DIAG_D are read when a context is created.)"""
 import os
 
 import numpy as np
@@ -30,7 +29,6 @@ SETTINGS = [
     {"TBLUP_SOLVE_CHAIN": "0"},                     # one solve workgroup per individual
     {"TBLUP_LAST_TERM": "1"},                       # diagonal's last SYRK term in the previous launch
     {"TBLUP_LAST_TERM": "0"},                       # ... in the diagonal launch
-    {"TBLUP_PAD_SKIP": "0"},                        # SNP form: leading padding rows multiplied, not skipped
     {"TBLUP_DIAG_D": "1"},                          # diagonal-target partials in the diagonal launches
     {"TBLUP_DIAG_D": "0"},                          # ... in the off-diagonal launches
 ]

@@ -1,0 +1,153 @@
+"""The batch shapes the benchmark actually runs, pinned as wholes, and the
+chained solve's failure mode.
+
+* Config 5 at pop 256: 3 traits, SNP-space form, B > 160, so the one-workgroup-per-individual
+  solve's multi-trait primal branch (k_solve<3>) -- oracle samples per trait at 1e-9 and bit
+  identity with the chained solve forced on (TBLUP_SOLVE_CHAIN=1).
+* Config 3's per-GPU shard at N = 8 (B = 128 at the config-2 shape) and N = 32 shards (B = 32):
+  every automatic small-batch policy at once (ahead P-units with makespan slicing, D-units beside
+  the diagonal, last-term mode at B <= 64, the chained solve) -- oracle samples and bit identity
+  with every policy off (TBLUP_AHEAD=0 TBLUP_SOLVE_CHAIN=0 TBLUP_DIAG_D=0 TBLUP_LAST_TERM=0).
+* A chained-solve hand-off wait that expires fails the call (TBLUP_ERR_STATE / TblupError) or
+  raises the device status word -- never a silent NaN -- and the next call on the same context is
+  clean (TBLUP_CHAIN_DEBUG forces one expiry: a lowered poll bound and a late producer unit).
+  Reference behaviour being replaced: a dead worker hangs its parent (tblup/evaluator.py:397-398).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import blup_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EBV_RTOL = 1e-9
+FIT_ATOL = 1e-9
+KNOBS_OFF = {"TBLUP_AHEAD": "0", "TBLUP_SOLVE_CHAIN": "0", "TBLUP_DIAG_D": "0", "TBLUP_LAST_TERM": "0"}
+
+
+def _relmax(a, b):
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+class _env:
+    """Temporarily set environment variables (read by tblup_ctx_create)."""
+
+    def __init__(self, env):
+        self.env = env
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.env}
+        os.environ.update(self.env)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def panel(gpu):
+    """BASELINE config-2 panel: 2000 animals x 50k SNPs, T 1280 / V 320, RandomKey genomes k = 1000."""
+    rng = np.random.default_rng(2)
+    n, P = 2000, 50_000
+    geno = O.synth_geno(rng, n, P)
+    pheno = rng.standard_normal(n)
+    perm = np.random.default_rng(3).permutation(n)
+    T, V = perm[:1280], perm[1280:1600]
+    keys = np.random.default_rng(4).uniform(size=(256, P))
+    genomes = [O.decode_randkeys(k, 1000) for k in keys]
+    Y = np.stack([pheno, rng.standard_normal(n), rng.standard_normal(n)], axis=1)
+    return dict(geno=geno, pheno=pheno, T=T, V=V, genomes=genomes, Y=Y)
+
+
+def _run(p, genomes, env=None, traits=False):
+    from tblup_amd.engine import GpuBlupEngine
+    with _env(env or {}):
+        with GpuBlupEngine(p["geno"], p["Y"] if traits else p["pheno"], device=0) as eng:
+            return eng.evaluate(genomes, p["T"], p["V"], 0.4, return_ebv=True)
+
+
+def test_config5_pop256_primal_multitrait_solve(panel):
+    """Config 5 as benchmarked: 256 individuals x 3 traits in one batch (k_solve<3>, SNP form)."""
+    p = panel
+    fit, ebv = _run(p, p["genomes"], traits=True)
+    assert ebv.shape == (256, 3, 320)
+    for i in (0, 97, 200, 255):
+        fs = []
+        for tr in range(3):
+            f, e = O.blup_grm_form(p["genomes"][i], p["T"], p["V"], p["geno"], p["Y"][:, tr], 0.4)
+            assert _relmax(ebv[i, tr], e) <= EBV_RTOL, (i, tr)
+            fs.append(f)
+        assert abs(fit[i] - np.mean(fs)) <= FIT_ATOL, i
+    chained = _run(p, p["genomes"], {"TBLUP_SOLVE_CHAIN": "1"}, traits=True)
+    np.testing.assert_array_equal(chained[0], fit)
+    np.testing.assert_array_equal(chained[1], ebv)
+
+
+@pytest.mark.parametrize("B", [128, 32])
+def test_config3_shard_auto_policies(panel, B):
+    """B individuals in one batch with every automatic schedule policy at once, against the
+    oracle and against every policy switched off, bit for bit."""
+    p = panel
+    genomes = p["genomes"][:B]
+    fit, ebv = _run(p, genomes)
+    off = _run(p, genomes, KNOBS_OFF)
+    np.testing.assert_array_equal(off[0], fit)
+    np.testing.assert_array_equal(off[1], ebv)
+    for i in sorted({0, B // 2, B - 1}):
+        f, e = O.blup_grm_form(genomes[i], p["T"], p["V"], p["geno"], p["pheno"], 0.4)
+        assert abs(fit[i] - f) <= FIT_ATOL, i
+        assert _relmax(ebv[i], e) <= EBV_RTOL, i
+
+
+def test_chain_sync_modes_bit_identical(panel):
+    """The chained solve's two hand-off protocols (sc1 loads/stores; acquire/release atomics,
+    TBLUP_CHAIN_SYNC=1) give the same bits."""
+    p = panel
+    genomes = p["genomes"][:24]
+    a = _run(p, genomes, {"TBLUP_SOLVE_CHAIN": "1", "TBLUP_CHAIN_SYNC": "0"})
+    b = _run(p, genomes, {"TBLUP_SOLVE_CHAIN": "1", "TBLUP_CHAIN_SYNC": "1"})
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_chained_solve_expiry_is_an_error(panel):
+    """TBLUP_CHAIN_DEBUG=spin,delay,shots: the next `shots` chained solves poll at most `spin`
+    times while one producer sleeps `delay` rounds, so a wait expires.  Host entry: TblupError
+    (TBLUP_ERR_STATE); device entry: the solve-error flag; then the same context is clean."""
+    import torch
+    from tblup_amd import _native
+    from tblup_amd.engine import GpuBlupEngine, concat_genomes
+    p = panel
+    genomes = p["genomes"][:8]                  # SNP form, B = 8 <= 160: the chained solve
+    ref = _run(p, genomes)
+    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,2"}):
+        eng = GpuBlupEngine(p["geno"], p["pheno"], device=0)
+    try:
+        with pytest.raises(_native.TblupError, match="chained solve") as ei:
+            eng.evaluate(genomes, p["T"], p["V"], 0.4)
+        assert ei.value.code == _native.ERR_STATE
+        # device entry: no synchronous failure, the status word is raised instead
+        sid = eng.split_id(p["T"], p["V"])
+        idx, off = concat_genomes(genomes)
+        d_idx, d_off = torch.from_numpy(idx).cuda(), torch.from_numpy(off).cuda()
+        d_fit = torch.empty(len(genomes), dtype=torch.float64, device="cuda")
+        s = torch.cuda.Stream()
+        eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(),
+                            stream_ptr=s.cuda_stream)
+        assert eng.solve_error(s.cuda_stream)
+        assert not eng.solve_error(s.cuda_stream)          # cleared by the read
+        # the debug shots are used up: the same context is clean again, host and device entries
+        fit, ebv = eng.evaluate(genomes, p["T"], p["V"], 0.4, return_ebv=True)
+        np.testing.assert_array_equal(fit, ref[0])
+        np.testing.assert_array_equal(ebv, ref[1])
+        eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(),
+                            stream_ptr=s.cuda_stream)
+        eng.check_device_status(s.cuda_stream)
+        np.testing.assert_array_equal(d_fit.cpu().numpy(), ref[0])
+    finally:
+        eng.close()

@@ -81,19 +81,22 @@ def main():
         print(f"{'diag' if is_diag else 'off '} J={J}: start +{(st - t0) * 1e6:8.1f} span {span * 1e6:7.1f} us "
               f"gap {gap * 1e6:5.1f} util {util:.2f}{first_tile} | " + "; ".join(parts))
     print(f"sum of launch spans {tot * 1e6:.1f} us, first start to last end {(prev_end - t0) * 1e6:.1f} us")
-    # phase stamps of diagonal workgroup 0 (tblup_internal.h DTR_RECS): per wave, 30 slots
-    NT, pos = 8, int(sysm.sum())
+    # phase stamps of diagonal workgroup 0 (tblup_internal.h DTR_RECS): per wave, 30 slots.  They
+    # follow the diagonal launch's own records (B x (1 + D-units beside it)), so locate them from
+    # the last diagonal record of launch J (the units per launch depend on the schedule policy)
+    NT = 8
     names = ["start", "pre-barrier", "post-barrier"] + [f"{x}{p}" for p in range(8) for x in ("a", "b", "w")] + [
         "xinv7", "post-xinv7", "dinv", "z", "syrk-issued", "-"] + [f"{x}{t}" for t in range(8) for x in
                                                                    ("stg-ready", "stg-go")] + ["syrk-done"] + [
         "f4-upd-done", "f4-x-init", "f4-steps", "f4-stored", "f4-branch"]
+    rkind = (raw[:, 2] >> np.uint64(56)).astype(np.int64)
+    rJ = (raw[:, 3] & np.uint64(0xFFFF)).astype(np.int64)
     for J in range(NT):
-        pos += pop
+        diag_rows = np.nonzero(((rkind == 1) | (rkind == 9)) & (rJ == J))[0]
+        if not len(diag_rows):
+            continue
+        pos = int(diag_rows.max()) + 1
         st = raw[pos:pos + 128].reshape(-1).reshape(8, 64).astype(np.int64)
-        pos += 128
-        nI = NT - J - 1
-        kjj = J == 0 and os.environ.get("TBLUP_SYS_TILES", "1") == "0"
-        pos += 0 if nI <= 0 else pop * nI + pop * (1 if (J >= 1 and J + 1 < NT) else 0) + (pop * (NT - 2) if kjj else 0)
         if J in (0, 3):
             base = st[0, 0]
             print(f"diag J={J} wg0 phase stamps (us from start), waves 0 / 1 / 4:")
