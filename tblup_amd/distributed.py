@@ -79,30 +79,36 @@ def shard_range(n_items, rank, world_size):
 def allgather_fitness(local, n_total, device=None):
     """All-gather the per-rank fitness blocks into the full float64 vector (rank order).
 
-    With nccl the buffers live on `device` (the evaluating engine's GPU; default the
-    current device), so each rank hands RCCL its own GPU's memory."""
+    `local` is this rank's shard_range block of n_total individuals: a vector, or an
+    (rows, block) matrix -- IntraGCV's per-fold fitnesses -- gathered in ONE collective into
+    (rows, n_total).  With nccl the buffers live on `device` (the evaluating engine's GPU; default
+    the current device), so each rank hands RCCL its own GPU's memory."""
     import torch
     import torch.distributed as dist
 
     rank, ws = world()
+    loc = np.asarray(local, dtype=np.float64)
     if ws == 1:
-        return np.asarray(local, dtype=np.float64)
+        return loc
+    rows = loc.shape[0] if loc.ndim == 2 else None
+    loc2 = loc.reshape(rows or 1, -1)
+    R = loc2.shape[0]
     sizes = [shard_range(n_total, r, ws) for r in range(ws)]
     maxc = max(hi - lo for lo, hi in sizes)
     if dist.get_backend() == "nccl":
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
     else:
         dev = torch.device("cpu")
-    buf = torch.full((maxc,), float("nan"), dtype=torch.float64, device=dev)
-    if len(local):
-        buf[:len(local)] = torch.as_tensor(np.asarray(local, dtype=np.float64), device=dev)
-    out = torch.empty(ws * maxc, dtype=torch.float64, device=dev)
-    allgather_device(out, buf)
-    out = out.cpu().numpy()
-    full = np.empty(n_total, dtype=np.float64)
+    buf = torch.full((R, maxc), float("nan"), dtype=torch.float64, device=dev)
+    if loc2.shape[1]:
+        buf[:, :loc2.shape[1]] = torch.as_tensor(loc2, device=dev)
+    out = torch.empty(ws * R * maxc, dtype=torch.float64, device=dev)
+    allgather_device(out, buf.reshape(-1))
+    out = out.cpu().numpy().reshape(ws, R, maxc)
+    full = np.empty((R, n_total), dtype=np.float64)
     for r, (lo, hi) in enumerate(sizes):
-        full[lo:hi] = out[r * maxc:r * maxc + hi - lo]
-    return full
+        full[:, lo:hi] = out[r, :, :hi - lo]
+    return full if rows is not None else full[0]
 
 
 def allgather_device(out, local):

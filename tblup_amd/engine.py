@@ -106,17 +106,23 @@ class GpuBlupEngine:
             p[0].synchronize()
 
     # ------------------------------------------------------------------ splits
-    def split_id(self, train, valid):
+    def split_id(self, train, valid, pinned=()):
+        """Device id of the (train, valid) split, registered on first use; the cache keeps the
+        MAX_SPLITS most recently used splits, never evicting the keys in `pinned` (the other
+        splits of the same call: evaluate_folds)."""
         self._settle()
         t = _as_int64(train)
         v = _as_int64(valid)
-        key = hashlib.sha1(t.tobytes() + b"|" + v.tobytes()).hexdigest()
+        key = self._split_key(t, v)
         hit = self._splits.get(key)
         if hit is not None:
             self._splits.move_to_end(key)
             return hit[0]
-        if len(self._splits) >= self.MAX_SPLITS:
-            _, (old_id, _) = self._splits.popitem(last=False)
+        while len(self._splits) >= self.MAX_SPLITS:
+            victim = next((k for k in self._splits if k not in pinned), None)
+            if victim is None:   # every cached split belongs to this call: let the cache grow
+                break
+            old_id, _ = self._splits.pop(victim)
             _native.check("tblup_drop_split", self._lib.tblup_drop_split(self._ctx, old_id))
         sid = self._next_split
         self._next_split += 1
@@ -124,6 +130,16 @@ class GpuBlupEngine:
             self._ctx, sid, _ptr(t, ctypes.c_int64), len(t), _ptr(v, ctypes.c_int64), len(v)))
         self._splits[key] = (sid, len(v))
         return sid
+
+    @staticmethod
+    def _split_key(train, valid):
+        return hashlib.sha1(_as_int64(train).tobytes() + b"|" + _as_int64(valid).tobytes()).hexdigest()
+
+    def split_ids(self, splits):
+        """split_id for every (train, valid) pair of one call; none of them evicts another, however
+        many there are (the cache shrinks back to MAX_SPLITS on later registrations)."""
+        pinned = {self._split_key(t, v) for t, v in splits}
+        return [self.split_id(t, v, pinned) for t, v in splits]
 
     # -------------------------------------------------------------- evaluation
     def evaluate(self, genomes, train, valid, h2, branch="auto", return_ebv=False):
@@ -149,7 +165,7 @@ class GpuBlupEngine:
         splits' evaluations back to back on the GPU, one round trip): (n_splits, B) fitness, row f
         bit-identical to evaluate(genomes, *splits[f]).  IntraGCV's k folds (evaluator.py:509-537)."""
         self._settle()
-        sids = np.array([self.split_id(t, v) for t, v in splits], dtype=np.int32)
+        sids = np.array(self.split_ids(splits), dtype=np.int32)
         idx, offsets = concat_genomes(genomes)
         B = len(genomes)
         fit = np.empty((len(sids), B), dtype=np.float64)

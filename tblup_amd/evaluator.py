@@ -252,11 +252,13 @@ class BlupParallelEvaluator(ParallelEvaluator):
         evaluate() takes the result only when it is asked for exactly these children,
         unchanged, at this generation; otherwise it is dropped and evaluate() runs as usual.
         Only where evaluate() is a pure function of the genomes: the fixed split or InterGCV
-        folds (no RNG draws), no SNP removal, one process, RandomKey individuals."""
+        folds (no RNG draws), no SNP removal, RandomKey individuals.  Under torch.distributed
+        every rank holds the same children (the DE step is replicated) and evaluates its own
+        shard of them; evaluate() all-gathers the shards, as _fitness does."""
         self._spec = None
         if self.engine is None or type(self) not in (BlupParallelEvaluator, InterGCVBlupParallelEvaluator):
             return False
-        if not hasattr(self.engine, "eval_keys_async") or world()[1] > 1 or not parents:
+        if not hasattr(self.engine, "eval_keys_async") or not parents:
             return False
         if self.snp_remover is not None and self.snp_remover.should_remove():
             return False
@@ -267,9 +269,14 @@ class BlupParallelEvaluator(ParallelEvaluator):
         if not all(1 <= k <= min(L, 8192) for k in lens) or keys.device.index != self.engine.device:
             return False
         train, valid = self.train_validation_indices(generation)
-        event, host, status = self.engine.eval_keys_async(keys, lens, train, valid, self.h2)
+        rank, ws = world()
+        lo, hi = shard_range(len(lens), rank, ws)
+        if hi > lo:
+            event, host, status = self.engine.eval_keys_async(keys[lo:hi], lens[lo:hi], train, valid, self.h2)
+        else:   # more ranks than children: nothing to evaluate here, the all-gather still runs
+            event, host, status = None, None, None
         self._spec = {"generation": generation, "keys": keys, "lens": lens, "event": event, "host": host,
-                      "status": status, "inds": None}
+                      "status": status, "inds": None, "shard": (lo, hi)}
         return True
 
     def _spec_bind(self, children):
@@ -290,9 +297,15 @@ class BlupParallelEvaluator(ParallelEvaluator):
         hits = DeviceKeyStore.get(self.engine.device).rows(inds)
         if any(h is None or h[0] is not spec["keys"] or h[1] != i for i, h in enumerate(hits)):
             return None
-        spec["event"].synchronize()
-        self.engine.raise_status(spec["status"].numpy(), n_snps=self.engine.n_snps)
-        return spec["host"].numpy().copy()
+        if spec["event"] is not None:
+            spec["event"].synchronize()
+            self.engine.raise_status(spec["status"].numpy(), n_snps=self.engine.n_snps)
+            local = spec["host"].numpy().copy()
+        else:
+            local = np.zeros(0, dtype=np.float64)
+        if world()[1] > 1:   # every rank takes the same decision here (replicated state): one all-gather
+            return allgather_fitness(local, len(inds), getattr(self.engine, "device", None))
+        return local
 
     def evaluate(self, previous_population, next_population, generation):
         """evaluator.py:359-378."""
@@ -380,9 +393,9 @@ class IntraGCVBlupParallelEvaluator(InterGCVBlupParallelEvaluator):
         if ws == 1:
             return folds(genomes, splits, self.h2)
         lo, hi = shard_range(len(genomes), rank, ws)
-        local = folds(genomes[lo:hi], splits, self.h2)
-        dev = getattr(self.engine, "device", None)
-        return np.array([allgather_fitness(local[k], len(genomes), dev) for k in range(self.n_folds)])
+        local = np.asarray(folds(genomes[lo:hi], splits, self.h2)).reshape(self.n_folds, hi - lo)
+        # every fold's block in one all-gather
+        return allgather_fitness(local, len(genomes), getattr(self.engine, "device", None))
 
     def _evaluate(self, population, to_evaluate, indices, generation):
         sums = {i: 0 for i in indices}

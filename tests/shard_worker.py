@@ -42,3 +42,40 @@ def run(rank, world, port, gp, pp, pop, k, out_dir):
     json.dump({"seen": seen, "group_after": dist.is_initialized(),
                "T": [int(x) for x in ev.training_indices], "V": [int(x) for x in ev.validation_indices]},
               open(os.path.join(out_dir, f"rank{rank}.json"), "w"))
+
+
+def run_main_gpu(rank, world, port, case, out_dir):
+    """main.py (tests/ga_driver.py) on a tests/golden/main_runs.npz case with the GPU drop-ins --
+    HIP evaluator, GPU DE evolver, speculative evaluation of the children -- as one of `world`
+    torchrun-style ranks on GPU 0 (gloo): the children's shard of this rank is evaluated on the
+    device while their genomes cross to the host, and evaluate() all-gathers the shards."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", TBLUP_DIST_BACKEND="gloo")
+    import numpy as np
+
+    from tblup_amd import evaluator as E
+    from tblup_amd import evolver as EV
+    from tblup_amd import local as LS
+    from tests import ga_driver as D
+
+    z = np.load(os.path.join(root, "tests", "golden", "main_runs.npz"))
+    gp, pp = os.path.join(out_dir, "geno.npy"), os.path.join(out_dir, "pheno.npy")
+    taken = []
+
+    def get_evaluator(args):
+        ev = E.get_evaluator(args)
+        orig = ev._take_spec
+
+        def spy(*a, **k):
+            r = orig(*a, **k)
+            taken.append(r is not None)
+            return r
+        ev._take_spec = spy
+        return ev
+
+    argv = list(z["base_argv"]) + ["--geno", gp, "--pheno", pp] + list(z[case + "_argv"])
+    run = D.run_main(argv, get_evaluator, EV.get_evolver, LS.get_local_search)
+    D.compare(run, z, case)
+    json.dump({"taken": taken}, open(os.path.join(out_dir, f"main_gpu_rank{rank}.json"), "w"))

@@ -52,7 +52,7 @@ def test_two_rank_gloo_matches_single_process(golden_dir, tmp_path):
     np.testing.assert_allclose(res[0]["testing"], flow["flow_testing"][:31], rtol=0, atol=1e-12)
 
 
-@pytest.mark.parametrize("case", ["rk_rand1", "removal_testing_knockout"])
+@pytest.mark.parametrize("case", ["rk_rand1", "removal_testing_knockout", "intracv"])
 def test_two_rank_main_flow_without_preinitialised_group(golden_dir, tmp_path, case):
     """torchrun-style main.py run on 2 ranks where nothing but the evaluator creates the
     process group (ParallelEvaluator.__enter__, the reference's worker start-up point,

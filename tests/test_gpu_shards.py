@@ -125,6 +125,31 @@ def test_bench_multi_rank_rehearsal(gpu, tmp_path):
     assert l1["fitness_checksum"] == l2["fitness_checksum"]
 
 
+@pytest.mark.parametrize("case", ["rk_rand1", "intercv"])
+def test_multi_rank_gpu_generations_reproduce_reference(gpu, golden_dir, tmp_path, case):
+    """The GPU generation path at world 2 (gloo, both ranks on this GPU): GPU DE step, each rank
+    evaluating ITS shard of the children speculatively while their genomes cross to the host,
+    one all-gather per generation -- every rank reproduces the reference's single-process main()
+    run (tests/golden/main_runs.npz), and the speculative results are the ones used."""
+    from tests import shard_worker
+    z = np.load(os.path.join(golden_dir, "main_runs.npz"))
+    np.save(tmp_path / "geno.npy", z["geno"].astype(np.float64))
+    np.save(tmp_path / "pheno.npy", z["pheno"])
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=shard_worker.run_main_gpu, args=(r, 2, port, case, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=400)
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+        assert p.exitcode == 0, f"rank process failed ({p.exitcode})"
+    taken = [json.load(open(tmp_path / f"main_gpu_rank{r}.json"))["taken"] for r in range(2)]
+    assert taken[0] == taken[1] and sum(taken[0]) >= 3     # both ranks took the speculative results
+
+
 RCCL_SNIPPET = r"""
 import os, sys
 import numpy as np
