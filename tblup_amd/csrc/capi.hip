@@ -326,7 +326,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add((size_t)B * d.nt * sd.ns * 8);                            // w
   add((size_t)B * d.nt * sd.ns * 8);                            // rhs
   add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // next diagonal tile (minus its last SYRK term)
-  add((size_t)B * sd.NT * 36 * 256 * 8);                        // diagonal GRM tiles
+  add((size_t)B * sd.NT * NPACK * BLKD * 8);                    // diagonal GRM tiles (or their int16 counts)
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
   add(any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
   if (use_chain(c, sd, B)) {                                    // chained solve: beta, c_{J->I}, EBV shares
@@ -410,6 +410,7 @@ FoldTab single_fold(const Split& sp, int64_t B) {
   ft.csT[0] = (const int32_t*)sp.colsumT.p;
   ft.xty[0] = (const double*)sp.xty.p;
   ft.yV[0] = (const double*)sp.yV.p;
+  ft.yT[0] = (const double*)sp.yT.p;
   ft.ymu[0] = (const double*)sp.ymu.p;
   return ft;
 }
@@ -439,17 +440,17 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* wv = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* rhs = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* Sp = cv.take<double>((size_t)B * TBLUP_NSLOT * 36 * 256);
-  double* Kdg = cv.take<double>((size_t)B * sd.NT * 36 * 256);
   const bool use_st = sys_tiles(d, sd) && stop_stage != 1;
+  // diagonal system tiles: exact int16 counts (k_sys_tiles) or fp64 K_JJ + lambda I (kernel form)
+  double* Kdg = use_st ? nullptr : cv.take<double>((size_t)B * sd.NT * NPACK * BLKD);
+  int16_t* kdb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * KD_TILE) : nullptr;
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
   double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
   double* Qb = use_last_term(c, sd, B) ? cv.take<double>((size_t)B * NPACK * BLKD) : nullptr;
   const bool fold_share = use_st && ft.nf > 1 && ft.share;   // k_sys_tiles_folds
-  int16_t* kcd = fold_share ? cv.take<int16_t>((size_t)B * sd.NT * KC_TILE) : nullptr;
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
   for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, AHEAD_SLOTS, c->diag_d);
-  const int32_t* csT = (const int32_t*)sp.colsumT.p;
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   int rc;
   rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
@@ -460,7 +461,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   if (sd.form == FORM_DUAL) {
     // primal rows are read in place from the split matrix: no gather
     rc = timed(c, s, KC_GATHER, 0.0, gather_bytes, [&] {
-      return launch_gather((const int8_t*)sp.geno.p, d_idx, d_off, pstride, B, csT, csA, scal, d, panel, u, s);
+      return launch_gather(ft, d_idx, d_off, pstride, B, csA, scal, d, panel, u, s);
     });
     if (rc) return rc;
   }
@@ -479,6 +480,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, panel, pstride, d_off, d_idx,
                 d.nRp, d.nRp / 4, ft, u, scal, c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
                 Pp, Qb};
+  cl.kd = kdb;
   cl.padskip = (sd.form == FORM_PRIMAL && sd.pad_first) ? 1 : 0;
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
@@ -499,13 +501,13 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     // every system tile (I >= J) in one int8 launch: int ops 2 x 128^2 x n_T per tile
     const double ntri = (double)sd.NT * (sd.NT + 1) / 2.0;
     const double fg = (double)B * ntri * 2.0 * 128.0 * 128.0 * cbar;
-    const double bg = (double)B * ((ntri - sd.NT) * KC_TILE * 2.0 + sd.NT * 36 * 256 * 8.0);
+    const double bg = (double)B * ((ntri - sd.NT) * KC_TILE * 2.0 + sd.NT * KD_TILE * 2.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
       c->wgt_used += B * sd.NT * (sd.NT + 1) / 2;
     }
     rc = timed(c, s, KC_GRM, fg, bg, [&] {
-      return fold_share ? launch_sys_tiles_folds(cl, kcd, s) : launch_sys_tiles(cl, s);
+      return fold_share ? launch_sys_tiles_folds(cl, s) : launch_sys_tiles(cl, s);
     });
     if (rc) return rc;
   } else {
@@ -981,7 +983,7 @@ static bool fold_fusable(const tblup_ctx* c, const std::vector<Split*>& sps, con
     if (sp->nT != sps[0]->nT || sp->nV != sps[0]->nV || sp->nTp != sps[0]->nTp || sp->nRp != sps[0]->nRp) return false;
   const EvalDims d = dims_of(c, *sps[0]);
   sd = choose_sys(c, d, h_off, B, branch, c->form_pref);
-  return sd.form == FORM_PRIMAL && sys_tiles(d, sd);
+  return true;   // either form: every system reads its own split through the FoldTab
 }
 
 // The fused chunk: the index lists replicated per fold (F x sum_k, device to device), the fused
@@ -1012,6 +1014,7 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
     ft.csT[f] = (const int32_t*)sps[f]->colsumT.p;
     ft.xty[f] = (const double*)sps[f]->xty.p;
     ft.yV[f] = (const double*)sps[f]->yV.p;
+    ft.yT[f] = (const double*)sps[f]->yT.p;
     ft.ymu[f] = (const double*)sps[f]->ymu.p;
   }
   return run_chunk(c, *sps[0], d, sd, s, idx_f, off_f, ho.data(), FB, h2, branch, cv, d_fit, nullptr, 0, nullptr,
@@ -1023,8 +1026,7 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
 static size_t fused_bytes(const tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd, int64_t B,
                           int64_t sum_k) {
   const int64_t F = (int64_t)sps.size();
-  return chunk_bytes(c, dims_of(c, *sps[0]), sd, F * B, F * sum_k, false) + (size_t)(sum_k + B + 1) * 8 +
-         (size_t)F * B * sd.NT * KC_TILE * 2 + 1024;   // + the diagonal tiles' counts (shared counts)
+  return chunk_bytes(c, dims_of(c, *sps[0]), sd, F * B, F * sum_k, false) + (size_t)(sum_k + B + 1) * 8 + 1024;
 }
 
 static int validate_splits(tblup_ctx* c, const int* split_ids, int n_splits, std::vector<Split*>& sps) {

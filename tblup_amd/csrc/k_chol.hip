@@ -268,7 +268,46 @@ struct CholArgs {
   FoldTab ft;               // each system's split (ymu, packed rows)
   int padskip;              // contractions over block column 0 skip the leading padding rows (SNP form)
   int padfirst;             // SNP form: padding rows lead (SC_PAD = ns - k)
+  int kdc;                  // Kd holds the diagonal tiles' exact int16 counts (k_sys_tiles: KD_TILE each),
+                            // not fp64 K_JJ + lambda I (one pointer field: the kernels are SGPR-bound)
+  __device__ __forceinline__ int16_t* kd() const { return kdc ? reinterpret_cast<int16_t*>(Kd) : nullptr; }
 };
+
+// K_JJ + lambda I (identity on padding rows) of packed lower block e of individual b's diagonal tile J,
+// from its exact counts (k_sys_tiles), minus sub (may be null), into the packed-block image dst: the
+// f64 MFMA C layout, element (16 q + (l >> 4) + 4 r, 16 s + (l & 15)) of the tile at
+// dst[pk(q, s) + bo((l >> 4) + 4 r, l & 15)], q / s the block's row / column.  cv: the block's
+// counts (int2 load issued by the caller).  (v - 0.0 == v exactly, so sub = 0 stores K itself.)
+__device__ __forceinline__ void kd_block(const CholArgs& a, int64_t b, int J, int e, int2 cv, v4d sub,
+                                         double* dst) {
+  const int l = threadIdx.x & 63;
+  const double* sc = a.scal + b * SCAL;
+  const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
+  const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
+  int q = 0;
+  while ((q + 1) * (q + 2) / 2 <= e) ++q;
+  const int sb = e - q * (q + 1) / 2;
+  const int64_t j0 = (int64_t)J * TILE;
+  const double* ub = a.u + b * a.prow + j0;
+  const int il = 16 * sb + (l & 15);
+  const int64_t gj = j0 + il;
+  const double uj = ub[il];
+  const int32_t c4[4] = {(int32_t)(int16_t)(cv.x & 0xffff), (int32_t)(int16_t)(cv.x >> 16),
+                         (int32_t)(int16_t)(cv.y & 0xffff), (int32_t)(int16_t)(cv.y >> 16)};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int cl = 16 * q + (l >> 4) + 4 * r;
+    const int64_t gi = j0 + cl;
+    const double kv = grm_value(c4[r], ub[cl], uj, sa, cN, invd, sm);
+    const double v = (sys_real(gi, pad, nrow) && sys_real(gj, pad, nrow)) ? kv + ((gi == gj) ? lam : 0.0)
+                                                                         : ((gi == gj) ? 1.0 : 0.0);
+    dst[pk(q, sb) + bo((l >> 4) + 4 * r, l & 15)] = v - sub[r];
+  }
+}
+__device__ __forceinline__ int2 kd_load(const CholArgs& a, int64_t b, int J, int e) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const int2*>(a.kd() + ((b * a.NT + J) * KD_TILE) + (e * 64 + l) * 4);
+}
 
 // Leading contraction rows of block column 0 that a GEMM1 / SYRK run starting at L = 0 skips:
 // individual b's leading padding rows (SC_PAD), rounded down to the MFMA's 4-row k-step.
@@ -738,14 +777,32 @@ __device__ __forceinline__ void store_syrk_blocks(double* dst, const double* bas
 }
 
 // S[b][Jt&1] = K_{Jt,Jt} - sum_{L < nterm} L_{Jt,L} L_{Jt,L}^T (packed blocks; the blocks of slice
-// sl only), 8 waves: the diagonal target's partial sum.
+// sl only), 8 waves: the diagonal target's partial sum.  K_{Jt,Jt} from Kd, or formed from the
+// exact counts (kd: their loads issued before the SYRK, whose first wait covers them).
 __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int Jt, int nterm, double* lds, int sl) {
+  const int w = threadIdx.x >> 6;
   v4d acc[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
+  int2 kv[5];
+  if (a.kdc) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int e = w + 8 * i;
+      kv[i] = (e < NPACK && ((slice_mask(sl) >> i) & 1)) ? kd_load(a, b, Jt, e) : int2{0, 0};
+    }
+  }
   if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc, sl, skip_rows(a, b));
-  store_syrk_blocks(a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD,
-                    a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD, acc, sl);
+  double* dst = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
+  if (!a.kdc) {
+    store_syrk_blocks(dst, a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD, acc, sl);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int e = w + 8 * i;
+    if (e < NPACK && ((slice_mask(sl) >> i) & 1)) kd_block(a, b, Jt, e, kv[i], acc[i], dst);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -849,7 +906,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       if (tr < nt) {
         const int64_t o = (b * nt + tr) * ns + gi;
         const double wv = (J > 0) ? a.w[o] : 0.0;
-        rv[tr] = ((a.form == FORM_PRIMAL) ? a.rhs[o] : a.yT[tr * a.ytp + gi] - muf * a.ft.ymu[0][tr]) - wv;
+        const int fo = fold_of(a.ft, b);   // the system's split (fold-fused batches)
+        rv[tr] = ((a.form == FORM_PRIMAL) ? a.rhs[o] : a.ft.yT[fo][tr * a.ytp + gi] - muf * a.ft.ymu[fo][tr]) - wv;
       }
     }
   }
@@ -860,10 +918,21 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
                                 : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
   {
+    if (L0 == 0 && a.kdc) {
+      // K_JJ + lambda I formed from the exact counts, wave w its packed blocks w + 8i (the lanes
+      // that later subtract the SYRK's accumulators from them)
+      int2 kv[5];
 #pragma unroll
-    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
-      const int chunk = (e * DW + w) * 64;
-      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
+      for (int i = 0; i < 5; ++i) kv[i] = (w + DW * i < NPACK) ? kd_load(a, b, J, w + DW * i) : int2{0, 0};
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        if (w + DW * i < NPACK) kd_block(a, b, J, w + DW * i, kv[i], v4d{0.0, 0.0, 0.0, 0.0}, Tp);
+    } else {
+#pragma unroll
+      for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
+        const int chunk = (e * DW + w) * 64;
+        __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
+      }
     }
     if (J > L0 && a.q != nullptr) {
       // last-term mode: Q = L_{J,J-1} L_{J,J-1}^T came with launch J-1's tile (J, J-1)
@@ -1413,14 +1482,30 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
 // stages through a 3-deep LDS-DMA ring (48 KiB, three workgroups per CU).  A rows are read
 // through pi(rho) so the counts land in the f64 accumulator layout.  Off-diagonal tiles store
 // the exact counts as int16 where the off-diagonal kernel's lanes read them (kc, see
-// tblup_internal.h); diagonal tiles store K_JJ + lambda I (identity on padding rows) as packed
-// fp64 blocks into Kd, exactly as k_diag_grm8 does.  (Rows stored as nibbles -- twice the bytes,
-// no unpack -- measured no faster: those loads then bound the launch.)
+// tblup_internal.h); diagonal tiles store the exact counts of their 36 lower blocks the same way
+// (kd: 18 KiB a tile instead of 72 KiB of fp64 K_JJ + lambda I -- the diagonal kernel and the
+// D-units form those values where they read them, kd_block).  (Rows stored as nibbles -- twice the
+// bytes, no unpack -- measured no faster: those loads then bound the launch.)
 // ===========================================================================
 constexpr int STW = 4;   // waves per system-tile workgroup
 
-__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
-                                       int l);
+// a diagonal tile's counts as int16 (diag): its 36 lower blocks (cb >= ib) only, packed block
+// e = cb (cb + 1) / 2 + ib, lane order of the f64 C layout (kd_load / kd_block read them); an
+// off-diagonal tile's: store_counts16's layout
+__device__ __forceinline__ void store_counts16_any(int16_t* kt, const v4f (&cnt)[4][4], int qr, int qc, int l,
+                                                   bool diag) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cb = 4 * qr + m, ib = 4 * qc + n;
+      if (diag && cb < ib) continue;
+      const v4f c = cnt[m][n];
+      const int2 packed = {(int)((uint32_t)((int)c[0] & 0xffff) | ((uint32_t)(int)c[1] << 16)),
+                           (int)((uint32_t)((int)c[2] & 0xffff) | ((uint32_t)(int)c[3] << 16))};
+      *reinterpret_cast<int2*>(kt + ((diag ? cb * (cb + 1) / 2 + ib : ib * 8 + cb) * 64 + l) * 4) = packed;
+    }
+}
 
 // two packed dwords (32 animals) -> one fp4 MFMA operand (even fields, odd fields of each): the
 // 2-bit code g lands in the low half of a nibble, e2m1 value g / 2 (0, 0.5 subnormal, 1.0), and
@@ -1433,7 +1518,6 @@ __device__ __forceinline__ v4i fp4_operand(uint32_t x0, uint32_t x1) {
 // the upper half unused by fp4 -- 32 more VGPRs and a zeroing move per operand)
 __device__ v4f mfma_fp4_16x16x128(v4i a, v4i b, v4f c, int cbsz, int blgp, int opsel_a, int scale_a, int opsel_b,
                                   int scale_b) __asm("llvm.amdgcn.mfma.scale.f32.16x16x128.f8f6f4.v4i32.v4i32");
-#define sys_diag_epilogue sys_diag_epilogue_impl
 
 __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* kc, int ntri) {
   constexpr int D = 3;                 // 64-B stages (256 animals) in the LDS ring (48 KiB: 3 workgroups per CU)
@@ -1512,94 +1596,11 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
       }
     }
   }
-  if (compute && I != J && !(a.skip & (1 << 16))) {
-    int16_t* kt = kc + ((b * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int cb = 4 * qr + m, ib = 4 * qc + n;
-        const v4f c = cnt[m][n];
-        const int2 packed = {(int)((uint32_t)((int)c[0] & 0xffff) | ((uint32_t)(int)c[1] << 16)),
-                             (int)((uint32_t)((int)c[2] & 0xffff) | ((uint32_t)(int)c[3] << 16))};
-        *reinterpret_cast<int2*>(kt + ((ib * 8 + cb) * 64 + l) * 4) = packed;
-      }
-  } else if (compute && I == J && !(a.skip & (1 << 17))) {
-    sys_diag_epilogue(a, cnt, b, J, qr, qc, l);
-  }
+  if (compute && !(a.skip & (I != J ? 1 << 16 : 1 << 17)))
+    store_counts16_any(I != J ? kc + ((b * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE
+                              : a.kd() + (b * a.NT + J) * KD_TILE,
+                       cnt, qr, qc, l, I == J);
   tr.done(WGT_SYS, J, I, b);
-}
-
-__device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr,
-                                                      int qc, int l) {
-  const double* sc = a.scal + b * SCAL;
-  const int64_t j0 = (int64_t)J * TILE;
-  const double sa_ = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
-  const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
-  const double* ub = a.u + b * a.prow + j0;
-  double* Kd = a.Kd + (b * a.NT + J) * (int64_t)NPACK * BLKD;
-  // every centring sum this lane needs, loaded before the first store (Kd and u are both double
-  // pointers: loads interleaved with the stores were issued one after another, ~47 us a launch)
-  double ur[4][4], uc[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ur[m][r] = ub[16 * (4 * qr + m) + (l >> 4) + 4 * r];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) uc[n] = ub[16 * (4 * qc + n) + (l & 15)];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int cb = 4 * qr + m, ib = 4 * qc + n;
-      if (cb < ib) continue;
-      const int il = 16 * ib + (l & 15);
-      const int64_t gj = j0 + il;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int cl = 16 * cb + (l >> 4) + 4 * r;
-        const int64_t gi = j0 + cl;
-        const double kv = grm_value((int32_t)cnt[m][n][r], ur[m][r], uc[n], sa_, cN, invd, sm);
-        const double v = (sys_real(gi, pad, nrow) && sys_real(gj, pad, nrow)) ? kv + ((gi == gj) ? lam : 0.0)
-                                                                              : ((gi == gj) ? 1.0 : 0.0);
-        Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
-      }
-    }
-}
-
-// a 128 x 128 count tile from the fp32 accumulators (exact integers) as int16, in the lane order
-// of the off-diagonal kernel's reads (see kc in tblup_internal.h)
-__device__ __forceinline__ void store_counts16(int16_t* kt, const v4f (&cnt)[4][4], int qr, int qc, int l) {
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int cb = 4 * qr + m, ib = 4 * qc + n;
-      const v4f c = cnt[m][n];
-      const int2 packed = {(int)((uint32_t)((int)c[0] & 0xffff) | ((uint32_t)(int)c[1] << 16)),
-                           (int)((uint32_t)((int)c[2] & 0xffff) | ((uint32_t)(int)c[3] << 16))};
-      *reinterpret_cast<int2*>(kt + ((ib * 8 + cb) * 64 + l) * 4) = packed;
-    }
-}
-
-// K_JJ + lambda I of system s from its diagonal tile's counts (k_sys_tiles_folds): the epilogue of
-// k_sys_tiles on the same lanes, one 4-wave workgroup per (system, J)
-__global__ __launch_bounds__(64 * STW) void k_sys_diag_counts(CholArgs a, const int16_t* kcd) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, qr = w >> 1, qc = w & 1;
-  const int64_t s = blockIdx.x / a.NT;
-  const int J = (int)(blockIdx.x % a.NT);
-  if (qr < qc) return;   // the upper quadrant is never read
-  const int16_t* kt = kcd + (s * a.NT + J) * KC_TILE;
-  v4f cnt[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int2 p = *reinterpret_cast<const int2*>(kt + (((4 * qc + n) * 8 + 4 * qr + m) * 64 + l) * 4);
-      cnt[m][n] = v4f{(float)(int16_t)(p.x & 0xffff), (float)(int16_t)(p.x >> 16), (float)(int16_t)(p.y & 0xffff),
-                      (float)(int16_t)(p.y >> 16)};
-    }
-  sys_diag_epilogue_inl(a, cnt, s, J, qr, qc, l);
 }
 
 // Fold-fused evaluation with shared counts (IntraGCV's folds, tblup_eval_folds*): when every fold's
@@ -1611,7 +1612,7 @@ __global__ __launch_bounds__(64 * STW) void k_sys_diag_counts(CholArgs a, const 
 // 3-deep LDS-DMA ring across these segments.  Every partial sum is an exact integer in fp32, so
 // the tiles equal k_sys_tiles' per-fold ones bit for bit; contraction (nRp + (2F - 1) nVp) / (F nTp)
 // of the per-fold launch's (config 2, 5 folds of 256: 14 stages of 256 animals instead of 20).
-__global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles_folds(CholArgs a, int16_t* kc, int16_t* kcd, int ntri) {
+__global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles_folds(CholArgs a, int16_t* kc, int ntri) {
   constexpr int D = 3;
   constexpr int TB = TILE * 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[D * 2 * TB];
@@ -1711,26 +1712,20 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles_folds(CholArgs a, int
     }
     if (!(k & 1) || !compute) continue;
     const int64_t s = (int64_t)((k - 1) >> 1) * bpf + b;   // C_{T_all} - C_{V_f}: system f * B + b
-    // off-diagonal tile: counts into kc; diagonal tile: counts into kcd (k_sys_diag_counts then
-    // forms K_JJ + lambda I: that epilogue beside the live accumulators spilled)
-    store_counts16(I != J ? kc + ((s * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE
-                          : kcd + (s * a.NT + J) * KC_TILE,
-                   cnt, qr, qc, l);
+    store_counts16_any(I != J ? kc + ((s * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE
+                              : a.kd() + (s * a.NT + J) * KD_TILE,
+                       cnt, qr, qc, l, I == J);
   }
   tr.done(WGT_SYS, J, I, b);
 }
 
 
-__device__ void sys_diag_epilogue_impl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
-                                       int l) {
-  sys_diag_epilogue_inl(a, cnt, b, J, qr, qc, l);
-}
-
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.idx, c.off, c.gpk_row, c.d.P, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
              c.wgt, nullptr, c.kc, c.part, c.q, c.B, c.ft, c.padskip,
-             (c.sd.form == FORM_PRIMAL && c.sd.pad_first) ? 1 : 0};
+             (c.sd.form == FORM_PRIMAL && c.sd.pad_first) ? 1 : 0, c.kd ? 1 : 0};
+  if (c.kd) a.Kd = reinterpret_cast<double*>(c.kd);
   return a;
 }
 
@@ -1741,13 +1736,10 @@ hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sys_tiles_folds(const CholLaunch& c, int16_t* kcd, hipStream_t s) {
+hipError_t launch_sys_tiles_folds(const CholLaunch& c, hipStream_t s) {
   CholArgs a = make_args(c, 0);
   const int ntri = c.sd.NT * (c.sd.NT + 1) / 2;
-  hipLaunchKernelGGL(k_sys_tiles_folds, dim3((unsigned)(c.ft.bpf * ntri)), dim3(64 * STW), 0, s, a, c.kc, kcd, ntri);
-  if (hipError_t e = hipGetLastError()) return e;
-  a.wgt = nullptr;
-  hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * c.sd.NT)), dim3(64 * STW), 0, s, a, (const int16_t*)kcd);
+  hipLaunchKernelGGL(k_sys_tiles_folds, dim3((unsigned)(c.ft.bpf * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
   return hipGetLastError();
 }
 

@@ -243,10 +243,9 @@ hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B,
 //   Each 64-SNP block: 64 gathered SNP rows x 128 animals staged in LDS
 //   (coalesced 16-B row-segment loads), then transposed by byte reads.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void k_gather(const int8_t* __restrict__ gs, const int64_t* __restrict__ idx,
+__global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __restrict__ idx,
                                                 const int64_t* __restrict__ off,
-                                                int64_t panel_stride,
-                                                const int32_t* __restrict__ csT, const int32_t* __restrict__ csA,
+                                                int64_t panel_stride, const int32_t* __restrict__ csA,
                                                 const double* __restrict__ scal, int64_t P, int64_t nRp,
                                                 int8_t* __restrict__ panel, double* __restrict__ u) {
   __shared__ __attribute__((aligned(16))) int8_t tile[KBLK][GATHER_ROWS];
@@ -257,7 +256,8 @@ __global__ __launch_bounds__(128) void k_gather(const int8_t* __restrict__ gs, c
   const int64_t r0 = (int64_t)blockIdx.x * GATHER_ROWS;
   const int64_t o0 = off[b], k = off[b + 1] - o0;
   const int mode = (int)scal[b * SCAL + SC_MODE];
-  const int32_t* cs = (mode == 1) ? csA : csT;
+  const int8_t* __restrict__ gs = ft.gs[fold_of(ft, b)];   // the system's split (fold-fused batches)
+  const int32_t* cs = (mode == 1) ? csA : ft.csT[fold_of(ft, b)];
   const int64_t nblk = (k + KBLK - 1) / KBLK;
   int8_t* pb = panel + b * panel_stride;
   int64_t uacc = 0;
@@ -308,11 +308,11 @@ __global__ __launch_bounds__(128) void k_gather(const int8_t* __restrict__ gs, c
   u[b * nRp + r0 + t] = (double)uacc;
 }
 
-hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int64_t* off, int64_t panel_stride,
-                         int64_t B, const int32_t* colsum_T, const int32_t* colsum_all, const double* scal,
-                         const EvalDims& d, int8_t* panel, double* u, hipStream_t s) {
+hipError_t launch_gather(const FoldTab& ft, const int64_t* idx, const int64_t* off, int64_t panel_stride, int64_t B,
+                         const int32_t* colsum_all, const double* scal, const EvalDims& d, int8_t* panel, double* u,
+                         hipStream_t s) {
   dim3 grid((unsigned)(d.nRp / GATHER_ROWS), (unsigned)B);
-  hipLaunchKernelGGL(k_gather, grid, dim3(GATHER_ROWS), 0, s, geno_split, idx, off, panel_stride, colsum_T, colsum_all,
+  hipLaunchKernelGGL(k_gather, grid, dim3(GATHER_ROWS), 0, s, ft, idx, off, panel_stride, colsum_all,
                      scal, d.P, d.nRp, panel, u);
   return hipGetLastError();
 }

@@ -124,6 +124,7 @@ struct FoldTab {
   const int32_t* csT[MAXF];    // train allele counts [P]
   const double* xty[MAXF];     // [nt][P]
   const double* yV[MAXF];      // [nt][nV]
+  const double* yT[MAXF];      // [nt][nTp] (kernel form: the right-hand sides y_T - mu on the fly)
   const double* ymu[MAXF];     // [nt]
 };
 __host__ __device__ __forceinline__ int fold_of(const FoldTab& ft, int64_t s) { return (int)(s / ft.bpf); }
@@ -143,10 +144,10 @@ hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B,
                               const int32_t* colsum_all, const EvalDims& d, const SysDims& sd,
                               int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
                               hipStream_t s);
-hipError_t launch_gather(const int8_t* geno_split, const int64_t* idx, const int64_t* off,
-                         int64_t panel_stride, int64_t B, const int32_t* colsum_T,
-                         const int32_t* colsum_all, const double* scal, const EvalDims& d,
-                         int8_t* panel, double* u, hipStream_t s);
+// kernel form: each system's animal-major panel from its split's rows (ft: fold of system b)
+hipError_t launch_gather(const FoldTab& ft, const int64_t* idx, const int64_t* off, int64_t panel_stride, int64_t B,
+                         const int32_t* colsum_all, const double* scal, const EvalDims& d, int8_t* panel, double* u,
+                         hipStream_t s);
 
 // ---- launchers (k_grm.hip) ----
 hipError_t launch_grm(const int8_t* panel, int64_t panel_stride, const int64_t* off, const double* u,
@@ -163,7 +164,7 @@ struct CholLaunch {
   double* w;             // [B][nt][ns] forward-substitution partial sums
   const double* rhs;     // [B][nt][ns] primal right-hand sides (dual: y_T - mu on the fly)
   double* S;             // [B][2][36*256] diagonal-tile preparation, slot J&1
-  double* Kd;            // [B][NT][36*256] GRM diagonal tiles
+  double* Kd;            // [B][NT][36*256] GRM diagonal tiles K_JJ + lambda I (kernel form / no system tiles)
   const double* yT;      // split phenotypes [nt][nTp] (kernel form: one split)
   const int8_t* panel;   // gathered genotypes
   int64_t pstride;       // panel bytes per individual
@@ -180,11 +181,15 @@ struct CholLaunch {
   double* part;          // [2][B][NT][128*128] partial sums of the next column's tiles (ahead schedule)
   double* q;             // last-term mode: [B][36*256] diagonal tile J's last SYRK term, from launch J-1
   int padskip;           // contractions over block column 0 skip the leading padding rows (SC_PAD)
+  int16_t* kd;           // SNP form with k_sys_tiles: the diagonal tiles' exact counts instead of Kd,
+                         // [B][NT][36 packed lower blocks][64 lanes][4] (KD_TILE int16 per tile); the
+                         // consumers form K_JJ + lambda I from them (kd_block, k_chol.hip)
 };
 // k_sys_tiles output: per individual NT(NT-1)/2 off-diagonal tiles (I > J, t = I(I-1)/2 + J) of
 // 128 x 128 int16 counts, in the order the off-diagonal kernel's lanes read them:
 // [column block ib][row block cb][lane][4].  Exact while n_T <= 8191 (counts <= 4 n_T).
 constexpr int64_t KC_TILE = (int64_t)TILE * TILE;
+constexpr int64_t KD_TILE = (int64_t)NPACK * BLKD;   // diagonal tile counts: the 36 lower 16x16 blocks
 constexpr int64_t KC_MAX_NT = 8191;
 // workgroup trace record (profiling only): {start, end, kind << 56 | I << 40 | b, J},
 // s_memrealtime ticks (100 MHz); kinds below
@@ -220,7 +225,10 @@ constexpr int64_t AHEAD_SLOTS = 256;
 // launches still grow); every J (TBLUP_DIAG_D=1): diagonal +100 us at pop 128
 constexpr int64_t DD_MIN_B = 64;
 constexpr int64_t DD_MAX_B = 128;
-constexpr int DD_MAX_J = 3;
+#ifndef TBLUP_AB_DD_MAX_J   // A/B builds only (tools/ab_build_defs.sh)
+#define TBLUP_AB_DD_MAX_J 3
+#endif
+constexpr int DD_MAX_J = TBLUP_AB_DD_MAX_J;
 OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs, int64_t slots = AHEAD_SLOTS,
                  int diag_d = 0, int dd_maxj = DD_MAX_J);
 inline int64_t offdiag_grid(const OffPlan& p, int64_t B) { return p.nI > 0 ? B * p.units() + p.n_kd : 0; }
@@ -230,14 +238,13 @@ hipError_t launch_chol_diag(const CholLaunch& c, int J, const OffPlan& p, hipStr
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s);
 // all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
-// SNP form: every (I >= J) system tile of the batch on int8 MFMA in one launch -- off-diagonal
-// counts into c.kc, diagonal tiles into Kd (replaces launch_diag_grm and the int8 phase of the
-// off-diagonal tiles)
+// SNP form: every (I >= J) system tile of the batch on FP4 MFMA in one launch -- off-diagonal
+// counts into c.kc, diagonal tiles' counts into c.kd (replaces launch_diag_grm and the int8 phase
+// of the off-diagonal tiles)
 hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s);
 // the same for a fold-fused chunk whose folds share their train + valid rows (FoldTab::share):
 // C_{R_f} = C_{T_all} - C_{V_f}, one workgroup per (individual, tile) for all F folds
-// (diagonal tiles through their counts in kcd [B][NT][KC_TILE] int16, then k_sys_diag_counts)
-hipError_t launch_sys_tiles_folds(const CholLaunch& c, int16_t* kcd, hipStream_t s);
+hipError_t launch_sys_tiles_folds(const CholLaunch& c, hipStream_t s);
 // Back substitution, prediction and fitness.  ch == null: one workgroup per individual
 // (k_solve); else (SNP form) the chained solve (k_solve_chain): an individual's block rows and
 // tile products spread over the chip, handing beta_J and the partial products on through

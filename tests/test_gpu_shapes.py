@@ -151,3 +151,29 @@ def test_chained_solve_expiry_is_an_error(panel):
         np.testing.assert_array_equal(d_fit.cpu().numpy(), ref[0])
     finally:
         eng.close()
+
+
+def test_kernel_form_folds_fused(panel):
+    """IntraGCV's folds in the kernel (GRM) form -- k > n (gblup) and n_T < k <= n (snp branch,
+    the kernel form because the fold's n_T = 1024 < k) -- run as ONE fused batch of 5 x B systems
+    (each system's panel gathered from its own fold's rows): bit-identical to the folds evaluated
+    split by split (TBLUP_FOLD_FUSE=0) and to each fold's own evaluation (SURVEY.md 8 f-2,
+    tblup/evaluator.py:509-537)."""
+    from tblup_amd.engine import GpuBlupEngine
+    from tblup_amd.evaluator import InterGCVBlupParallelEvaluator
+    p = panel
+    rng = np.random.default_rng(61)
+    genomes = [rng.choice(50_000, k, replace=False) for k in (2500, 1100, 2100, 1500, 2400, 1200)]
+    folds = InterGCVBlupParallelEvaluator.make_fold_indices(np.asarray(p["T"]), 5)
+    with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
+        fused = eng.evaluate_folds(genomes, folds, 0.4)
+        singles = [eng.evaluate(genomes, t, v, 0.4) for t, v in folds]
+    with _env({"TBLUP_FOLD_FUSE": "0"}):
+        with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
+            unfused = eng.evaluate_folds(genomes, folds, 0.4)
+    np.testing.assert_array_equal(fused, unfused)
+    for f in range(5):
+        np.testing.assert_array_equal(fused[f], singles[f])
+    for i in (0, 1):
+        fo, _ = O.blup_grm_form(genomes[i], folds[2][0], folds[2][1], p["geno"], p["pheno"], 0.4)
+        assert abs(fused[2][i] - fo) <= FIT_ATOL
