@@ -326,7 +326,8 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add((size_t)B * d.nt * sd.ns * 8);                            // w
   add((size_t)B * d.nt * sd.ns * 8);                            // rhs
   add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // next diagonal tile (minus its last SYRK term)
-  add((size_t)B * sd.NT * NPACK * BLKD * 8);                    // diagonal GRM tiles (or their int16 counts)
+  add((size_t)B * sd.NT * NPACK * BLKD * 8);                    // diagonal GRM tiles
+  add(sys_tiles(d, sd) ? (size_t)B * sd.NT * KD_TILE * 2 : 0);  // their int16 counts (k_sys_tiles)
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
   add(any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
   if (use_chain(c, sd, B)) {                                    // chained solve: beta, c_{J->I}, EBV shares
@@ -441,8 +442,9 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* rhs = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* Sp = cv.take<double>((size_t)B * TBLUP_NSLOT * 36 * 256);
   const bool use_st = sys_tiles(d, sd) && stop_stage != 1;
-  // diagonal system tiles: exact int16 counts (k_sys_tiles) or fp64 K_JJ + lambda I (kernel form)
-  double* Kdg = use_st ? nullptr : cv.take<double>((size_t)B * sd.NT * NPACK * BLKD);
+  // diagonal system tiles: fp64 K_JJ + lambda I (with k_sys_tiles: J < 2 only, the diagonal
+  // kernel's direct reads) and, with k_sys_tiles, the exact int16 counts of J >= 2 (the D-units')
+  double* Kdg = cv.take<double>((size_t)B * sd.NT * NPACK * BLKD);
   int16_t* kdb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * KD_TILE) : nullptr;
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
   double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
@@ -501,7 +503,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     // every system tile (I >= J) in one int8 launch: int ops 2 x 128^2 x n_T per tile
     const double ntri = (double)sd.NT * (sd.NT + 1) / 2.0;
     const double fg = (double)B * ntri * 2.0 * 128.0 * 128.0 * cbar;
-    const double bg = (double)B * ((ntri - sd.NT) * KC_TILE * 2.0 + sd.NT * KD_TILE * 2.0);
+    const double nd8 = std::min(sd.NT, 2);   // diagonal tiles stored as fp64 (the rest as int16 counts)
+    const double bg = (double)B * ((ntri - sd.NT) * KC_TILE * 2.0 + (sd.NT - nd8) * KD_TILE * 2.0 + nd8 * KD_TILE * 8.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
       c->wgt_used += B * sd.NT * (sd.NT + 1) / 2;

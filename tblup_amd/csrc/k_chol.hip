@@ -268,9 +268,9 @@ struct CholArgs {
   FoldTab ft;               // each system's split (ymu, packed rows)
   int padskip;              // contractions over block column 0 skip the leading padding rows (SNP form)
   int padfirst;             // SNP form: padding rows lead (SC_PAD = ns - k)
-  int kdc;                  // Kd holds the diagonal tiles' exact int16 counts (k_sys_tiles: KD_TILE each),
-                            // not fp64 K_JJ + lambda I (one pointer field: the kernels are SGPR-bound)
-  __device__ __forceinline__ int16_t* kd() const { return kdc ? reinterpret_cast<int16_t*>(Kd) : nullptr; }
+  int16_t* kd;              // SNP form with k_sys_tiles: the diagonal tiles' exact counts for J >= 2 (KD_TILE
+                            // each; the D-units form K_JJ + lambda I where they read it, kd_block); Kd then
+                            // holds J < 2 only (the diagonal kernel's direct reads)
 };
 
 // K_JJ + lambda I (identity on padding rows) of packed lower block e of individual b's diagonal tile J,
@@ -306,7 +306,7 @@ __device__ __forceinline__ void kd_block(const CholArgs& a, int64_t b, int J, in
 }
 __device__ __forceinline__ int2 kd_load(const CholArgs& a, int64_t b, int J, int e) {
   const int l = threadIdx.x & 63;
-  return *reinterpret_cast<const int2*>(a.kd() + ((b * a.NT + J) * KD_TILE) + (e * 64 + l) * 4);
+  return *reinterpret_cast<const int2*>(a.kd + ((b * a.NT + J) * KD_TILE) + (e * 64 + l) * 4);
 }
 
 // Leading contraction rows of block column 0 that a GEMM1 / SYRK run starting at L = 0 skips:
@@ -785,7 +785,7 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
 #pragma unroll
   for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
   int2 kv[5];
-  if (a.kdc) {
+  if (a.kd) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int e = w + 8 * i;
@@ -794,7 +794,7 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
   }
   if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc, sl, skip_rows(a, b));
   double* dst = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
-  if (!a.kdc) {
+  if (!a.kd) {
     store_syrk_blocks(dst, a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD, acc, sl);
     return;
   }
@@ -918,21 +918,10 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   const double* src = (L0 == 0) ? a.Kd + (b * NT + J) * (int64_t)NPACK * BLKD
                                 : a.S + (b * NSLOT + (J & 1)) * (int64_t)NPACK * BLKD;
   {
-    if (L0 == 0 && a.kdc) {
-      // K_JJ + lambda I formed from the exact counts, wave w its packed blocks w + 8i (the lanes
-      // that later subtract the SYRK's accumulators from them)
-      int2 kv[5];
 #pragma unroll
-      for (int i = 0; i < 5; ++i) kv[i] = (w + DW * i < NPACK) ? kd_load(a, b, J, w + DW * i) : int2{0, 0};
-#pragma unroll
-      for (int i = 0; i < 5; ++i)
-        if (w + DW * i < NPACK) kd_block(a, b, J, w + DW * i, kv[i], v4d{0.0, 0.0, 0.0, 0.0}, Tp);
-    } else {
-#pragma unroll
-      for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
-        const int chunk = (e * DW + w) * 64;
-        __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
-      }
+    for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
+      const int chunk = (e * DW + w) * 64;
+      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
     }
     if (J > L0 && a.q != nullptr) {
       // last-term mode: Q = L_{J,J-1} L_{J,J-1}^T came with launch J-1's tile (J, J-1)
@@ -1489,6 +1478,46 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
 // ===========================================================================
 constexpr int STW = 4;   // waves per system-tile workgroup
 
+// K_JJ + lambda I (identity on padding rows) from a diagonal tile's accumulators (exact counts in
+// fp32) as packed fp64 blocks into Kd: the tiles J < 2, which the diagonal kernel reads directly
+__device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr,
+                                                      int qc, int l) {
+  const double* sc = a.scal + b * SCAL;
+  const int64_t j0 = (int64_t)J * TILE;
+  const double sa_ = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
+  const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
+  const double* ub = a.u + b * a.prow + j0;
+  double* Kd = a.Kd + (b * a.NT + J) * (int64_t)NPACK * BLKD;
+  // every centring sum this lane needs, loaded before the first store (Kd and u are both double
+  // pointers: loads interleaved with the stores were issued one after another, ~47 us a launch)
+  double ur[4][4], uc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ur[m][r] = ub[16 * (4 * qr + m) + (l >> 4) + 4 * r];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) uc[n] = ub[16 * (4 * qc + n) + (l & 15)];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cb = 4 * qr + m, ib = 4 * qc + n;
+      if (cb < ib) continue;
+      const int il = 16 * ib + (l & 15);
+      const int64_t gj = j0 + il;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cl = 16 * cb + (l >> 4) + 4 * r;
+        const int64_t gi = j0 + cl;
+        const double kv = grm_value((int32_t)cnt[m][n][r], ur[m][r], uc[n], sa_, cN, invd, sm);
+        const double v = (sys_real(gi, pad, nrow) && sys_real(gj, pad, nrow)) ? kv + ((gi == gj) ? lam : 0.0)
+                                                                              : ((gi == gj) ? 1.0 : 0.0);
+        Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
+      }
+    }
+}
+__device__ void sys_diag_epilogue(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc, int l);
+
 // a diagonal tile's counts as int16 (diag): its 36 lower blocks (cb >= ib) only, packed block
 // e = cb (cb + 1) / 2 + ib, lane order of the f64 C layout (kd_load / kd_block read them); an
 // off-diagonal tile's: store_counts16's layout
@@ -1596,9 +1625,11 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
       }
     }
   }
-  if (compute && !(a.skip & (I != J ? 1 << 16 : 1 << 17)))
+  if (compute && I == J && J < 2 && !(a.skip & (1 << 17)))
+    sys_diag_epilogue(a, cnt, b, J, qr, qc, l);   // read directly by the diagonal kernel
+  else if (compute && !(a.skip & (I != J ? 1 << 16 : 1 << 17)))
     store_counts16_any(I != J ? kc + ((b * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE
-                              : a.kd() + (b * a.NT + J) * KD_TILE,
+                              : a.kd + (b * a.NT + J) * KD_TILE,
                        cnt, qr, qc, l, I == J);
   tr.done(WGT_SYS, J, I, b);
 }
@@ -1713,19 +1744,45 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles_folds(CholArgs a, int
     if (!(k & 1) || !compute) continue;
     const int64_t s = (int64_t)((k - 1) >> 1) * bpf + b;   // C_{T_all} - C_{V_f}: system f * B + b
     store_counts16_any(I != J ? kc + ((s * (a.NT * (a.NT - 1) / 2)) + I * (I - 1) / 2 + J) * KC_TILE
-                              : a.kd() + (s * a.NT + J) * KD_TILE,
+                              : a.kd + (s * a.NT + J) * KD_TILE,
                        cnt, qr, qc, l, I == J);
   }
   tr.done(WGT_SYS, J, I, b);
 }
 
 
+__device__ void sys_diag_epilogue(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc,
+                                  int l) {
+  sys_diag_epilogue_inl(a, cnt, b, J, qr, qc, l);
+}
+
+// fold-fused chunks (k_sys_tiles_folds stores every diagonal tile's counts): K_JJ + lambda I of the
+// tiles J < 2 into Kd, one 4-wave workgroup per (system, J)
+__global__ __launch_bounds__(64 * STW) void k_sys_diag_counts(CholArgs a) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, qr = w >> 1, qc = w & 1;
+  const int64_t s = blockIdx.x >> 1;
+  const int J = (int)(blockIdx.x & 1);
+  if (qr < qc || J >= a.NT) return;   // the upper quadrant is never read
+  const int16_t* kt = a.kd + (s * a.NT + J) * KD_TILE;
+  v4f cnt[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cb = 4 * qr + m, ib = 4 * qc + n;
+      int2 p = {0, 0};
+      if (cb >= ib) p = *reinterpret_cast<const int2*>(kt + ((cb * (cb + 1) / 2 + ib) * 64 + l) * 4);
+      cnt[m][n] = v4f{(float)(int16_t)(p.x & 0xffff), (float)(int16_t)(p.x >> 16), (float)(int16_t)(p.y & 0xffff),
+                      (float)(int16_t)(p.y >> 16)};
+    }
+  sys_diag_epilogue_inl(a, cnt, s, J, qr, qc, l);
+}
+
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.idx, c.off, c.gpk_row, c.d.P, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
              c.wgt, nullptr, c.kc, c.part, c.q, c.B, c.ft, c.padskip,
-             (c.sd.form == FORM_PRIMAL && c.sd.pad_first) ? 1 : 0, c.kd ? 1 : 0};
-  if (c.kd) a.Kd = reinterpret_cast<double*>(c.kd);
+             (c.sd.form == FORM_PRIMAL && c.sd.pad_first) ? 1 : 0, c.kd};
   return a;
 }
 
@@ -1740,6 +1797,9 @@ hipError_t launch_sys_tiles_folds(const CholLaunch& c, hipStream_t s) {
   CholArgs a = make_args(c, 0);
   const int ntri = c.sd.NT * (c.sd.NT + 1) / 2;
   hipLaunchKernelGGL(k_sys_tiles_folds, dim3((unsigned)(c.ft.bpf * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
+  if (hipError_t e = hipGetLastError()) return e;
+  a.wgt = nullptr;
+  hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a);
   return hipGetLastError();
 }
 
