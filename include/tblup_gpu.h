@@ -303,6 +303,13 @@ int tblup_solve_error(tblup_ctx* ctx, void* stream, int* flag);
  * that point (the caller's event). */
 int tblup_status_async(tblup_ctx* ctx, void* stream, int32_t* host_status);
 
+/* Page-lock `bytes` of existing host memory at `ptr` for DMA (hipHostRegister) / release it.  The
+ * multi-rank generation path registers the node-shared memory segments the ranks' shards of the
+ * children's genomes are copied into (tblup_amd/shmrows.py), so each rank's device-to-host copy of
+ * its shard runs as a DMA straight into the shared rows. */
+int tblup_host_register(void* ptr, int64_t bytes);
+int tblup_host_unregister(void* ptr);
+
 /* Device memory currently held by the context (bytes). */
 int tblup_mem_info(tblup_ctx* ctx, int64_t* bytes_in_use);
 

@@ -1568,6 +1568,20 @@ int tblup_status_async(tblup_ctx* c, void* stream, int32_t* host_status) {
   return 0;
 }
 
+int tblup_host_register(void* ptr, int64_t bytes) {
+  g_err.clear();
+  if (!ptr || bytes <= 0) return fail(TBLUP_ERR_ARG, "null pointer or non-positive size");
+  HIPCHK(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault));
+  return 0;
+}
+
+int tblup_host_unregister(void* ptr) {
+  g_err.clear();
+  if (!ptr) return fail(TBLUP_ERR_ARG, "null pointer");
+  HIPCHK(hipHostUnregister(ptr));
+  return 0;
+}
+
 int tblup_mem_info(tblup_ctx* c, int64_t* bytes) {
   if (int rc = check_ctx(c)) return rc;
   if (bytes) *bytes = c->mem_in_use;

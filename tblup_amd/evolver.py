@@ -29,7 +29,9 @@ from copy import deepcopy
 import numpy as np
 
 from . import _native
+from .distributed import shard_range, world
 from .keystore import DeviceKeyStore, track, work_stream
+from .shmrows import RING as _SHM
 
 
 def get_evolver(args):
@@ -418,26 +420,43 @@ class _GpuDEEvolver(Evolver):
                 # genomes (views: no host copy); otherwise chunks, each followed by an event, so the
                 # per-row copies of one chunk overlap the transfer of the next
                 block_rows = dtypes is None and n * L * 8 <= _BLOCK_MAX
-                if block_rows:
-                    _BLOCKS.reserve(children.shape)
-                host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
-                nchunk = 1 if block_rows else (8 if n >= 16 else 1)
-                rows = (n + nchunk - 1) // nchunk
-                events = []
-                for c in range(nchunk):
-                    lo, hi = c * rows, min(n, (c + 1) * rows)
+                # several ranks of one node: a node-shared block, each rank copying its shard's rows
+                shared = _SHM.acquire(children.shape, _BLOCKS.keep_for(n * L * 8)) if block_rows else None
+                if shared is not None:
+                    rank, ws = world()
+                    lo, hi = shard_range(n, rank, ws)
+                    host = torch.from_numpy(shared)
                     if lo < hi:
                         host[lo:hi].copy_(children[lo:hi], non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record()
-                    events.append(ev)
+                    events = [ev]
+                else:
+                    if block_rows:
+                        _BLOCKS.reserve(children.shape)
+                    host = torch.empty(children.shape, dtype=torch.float64, pin_memory=True)
+                    nchunk = 1 if block_rows else (8 if n >= 16 else 1)
+                    rows = (n + nchunk - 1) // nchunk
+                    events = []
+                    for c in range(nchunk):
+                        lo, hi = c * rows, min(n, (c + 1) * rows)
+                        if lo < hi:
+                            host[lo:hi].copy_(children[lo:hi], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record()
+                        events.append(ev)
             finally:
                 rng_done()   # numpy's global state after the step's np.random.rand draws
         t = _mark(t, "ev_transfer_issue")
         # the candidates (new uids, the parent's other attributes) while the transfer runs
         next_pop = [_copy_individual(population[i]) for i in range(n)]
         t = _mark(t, "ev_candidates")
-        if block_rows:
+        if shared is not None:
+            events[-1].synchronize()
+            import torch.distributed as dist
+            dist.barrier()   # every rank's shard of the rows has landed
+            arrays = _BLOCKS.rows(shared)
+        elif block_rows:
             events[-1].synchronize()
             arrays = _BLOCKS.rows(host.numpy())
         else:

@@ -51,8 +51,10 @@ def run_main_gpu(rank, world, port, case, out_dir):
     device while their genomes cross to the host, and evaluate() all-gathers the shards."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
+    # LOCAL_WORLD_SIZE: the ranks share one node, so the children's rows go through the node-shared
+    # ring (tblup_amd/shmrows.py: each rank copies its shard, page-locked /dev/shm segments)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", TBLUP_DIST_BACKEND="gloo")
+                      LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world), TBLUP_DIST_BACKEND="gloo")
     import numpy as np
 
     from tblup_amd import evaluator as E
@@ -76,6 +78,15 @@ def run_main_gpu(rank, world, port, case, out_dir):
         return ev
 
     argv = list(z["base_argv"]) + ["--geno", gp, "--pheno", pp] + list(z[case + "_argv"])
+    from tblup_amd.shmrows import RING
+    acquired = []
+    orig_acq = RING.acquire
+
+    def acq(*a, **k):
+        blk = orig_acq(*a, **k)
+        acquired.append(blk is not None)
+        return blk
+    RING.acquire = acq
     run = D.run_main(argv, get_evaluator, EV.get_evolver, LS.get_local_search)
     D.compare(run, z, case)
-    json.dump({"taken": taken}, open(os.path.join(out_dir, f"main_gpu_rank{rank}.json"), "w"))
+    json.dump({"taken": taken, "shared": acquired}, open(os.path.join(out_dir, f"main_gpu_rank{rank}.json"), "w"))

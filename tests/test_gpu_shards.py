@@ -128,9 +128,10 @@ def test_bench_multi_rank_rehearsal(gpu, tmp_path):
 @pytest.mark.parametrize("case", ["rk_rand1", "intercv"])
 def test_multi_rank_gpu_generations_reproduce_reference(gpu, golden_dir, tmp_path, case):
     """The GPU generation path at world 2 (gloo, both ranks on this GPU): GPU DE step, each rank
-    evaluating ITS shard of the children speculatively while their genomes cross to the host,
-    one all-gather per generation -- every rank reproduces the reference's single-process main()
-    run (tests/golden/main_runs.npz), and the speculative results are the ones used."""
+    evaluating ITS shard of the children speculatively while it copies ITS shard of their genomes
+    into the node-shared host rows (tblup_amd/shmrows.py), one all-gather per generation -- every
+    rank reproduces the reference's single-process main() run (tests/golden/main_runs.npz), and
+    the speculative results and the shared rows are the ones used."""
     from tests import shard_worker
     z = np.load(os.path.join(golden_dir, "main_runs.npz"))
     np.save(tmp_path / "geno.npy", z["geno"].astype(np.float64))
@@ -146,8 +147,10 @@ def test_multi_rank_gpu_generations_reproduce_reference(gpu, golden_dir, tmp_pat
         if p.exitcode is None:
             p.kill()
         assert p.exitcode == 0, f"rank process failed ({p.exitcode})"
-    taken = [json.load(open(tmp_path / f"main_gpu_rank{r}.json"))["taken"] for r in range(2)]
-    assert taken[0] == taken[1] and sum(taken[0]) >= 3     # both ranks took the speculative results
+    res = [json.load(open(tmp_path / f"main_gpu_rank{r}.json")) for r in range(2)]
+    assert res[0]["taken"] == res[1]["taken"] and sum(res[0]["taken"]) >= 3   # both took the speculative results
+    # the children's rows crossed through the node-shared ring (each rank copied its shard)
+    assert res[0]["shared"] == res[1]["shared"] and sum(res[0]["shared"]) >= 3
 
 
 RCCL_SNIPPET = r"""

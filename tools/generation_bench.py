@@ -16,7 +16,16 @@ sys.path.insert(0, ROOT)
 
 
 def main(n=2000, p=50000, k=1000, pop=256, gens=4):
-    import torch  # noqa: F401
+    # under torch.distributed.run (WORLD_SIZE > 1): one rank per process; more ranks than GPUs share
+    # them (gloo: RCCL needs one device per rank), each rank evaluating its shard of the children
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    import torch
+    if world > 1:
+        ndev = max(1, torch.cuda.device_count())
+        os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % ndev)
+        if ndev < world:
+            os.environ.setdefault("TBLUP_DIST_BACKEND", "gloo")
+        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
     from oracle import blup_oracle as O
     from oracle import de_oracle as D
     from tests.helpers import Pop
@@ -35,7 +44,7 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
     ev = BlupParallelEvaluator(os.path.join(tmp, "g.npy"), os.path.join(tmp, "y.npy"), 0.4)
     inds = [RandomKeyIndividual(k, p, genome=rng.uniform(size=p)) for _ in range(pop)]
     evo = DERandOneEvolver(p, 0.8, 0.5, False)
-    out = {"n": n, "p": p, "k": k, "pop": pop}
+    out = {"n": n, "p": p, "k": k, "pop": pop, "world": world}
     phase = {}
 
     def timed(obj, name):
@@ -90,6 +99,13 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
                     "gpu_generation_ms_mean_all": float(np.mean(allg)),
                     "gpu_generation_ms_mean_after_first": float(np.mean(allg[1:])) if len(allg) > 1 else None,
                     "gpu_generation_ms_all": [round(x, 2) for x in allg]})
+        if world > 1:
+            from tblup_amd.shmrows import RING
+            out["shared_rows"] = any(r is not None for r in RING._rings.values())
+            out["gpu_generation_ms_max_over_ranks"] = _max_over_ranks(out["gpu_generation_ms_median"])
+            if int(os.environ.get("RANK", "0")) == 0:
+                print(json.dumps(out))
+            return
         # host evolve (numpy restatement of the reference loop) + host decode, same population
         genomes = [x.get_internal_genome() for x in popn.population]
         t0 = time.perf_counter()
@@ -102,5 +118,15 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
     print(json.dumps(out))
 
 
+def _max_over_ranks(x):
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 if __name__ == "__main__":
-    main(gens=int(sys.argv[1]) if len(sys.argv) > 1 else 4)
+    # usage: python tools/generation_bench.py [GENS] [POP]   (torch.distributed.run for N > 1 ranks)
+    main(gens=int(sys.argv[1]) if len(sys.argv) > 1 else 4, pop=int(sys.argv[2]) if len(sys.argv) > 2 else 256)
