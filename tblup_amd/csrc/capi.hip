@@ -240,7 +240,11 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   // launch j computes the partial sums of column j + 1's tiles; auto: when the launch's P-units
   // (B x (NT - 2 - j)) fit in AHEAD_SLOTS workgroup slots, i.e. run beside its T-units in one wave
   auto ahead_at = [&](int j) {
+#ifdef TBLUP_AB_AHEAD_MASK   // A/B builds only (tools/ab_build_defs.sh): launches ahead by bit j
+    const bool on = ahead == 1 || (ahead < 0 && (B * (NT - 2 - j) < slots || ((TBLUP_AB_AHEAD_MASK >> j) & 1)));
+#else
     const bool on = ahead == 1 || (ahead < 0 && B * (NT - 2 - j) < slots);
+#endif
     return on && j >= 1 && j + 2 <= NT - 1;
   };
   p.nP = ahead_at(J) ? NT - 2 - J : 0;

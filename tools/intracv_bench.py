@@ -1,6 +1,6 @@
 """IntraGCV (k = 5 folds inside every fitness evaluation, evaluator.py:494-537) against one
-fold's evaluation on the GPU: config 1 (200 x 1000, k = 100, pop 32) and config 2 (2000 x 50k,
-k = 1000, pop 256).  Per config one JSON line with
+fold's evaluation on the GPU: config 1 (200 x 1000, k = 100, pop 32), config 2 (2000 x 50k,
+k = 1000, pop 256) and a config-4-shaped kernel-form case (5000 x 50k, k = 5000, pop 32; device only).  Per config one JSON line with
   * device-resident genomes (no host decode in the ratio): one fold's evaluate_device and the
     k folds' evaluate_folds_device (tblup_eval_folds_device: fold-fused, the k x pop systems as
     one batch through one launch sequence, system tiles from shared counts; beside it the same
@@ -40,7 +40,11 @@ def main():
     from oracle import blup_oracle as O
     from tests.ga_driver import RandomKeyIndividual
     from tblup_amd import evaluator as E
-    for name, n, p, k, pop in (("config1", 200, 1000, 100, 32), ("config2", 2000, 50000, 1000, 256)):
+    cases = (("config1", 200, 1000, 100, 32), ("config2", 2000, 50000, 1000, 256),
+             # the kernel (GRM) form: k = 5000 > each fold's n_T = 2560 (BASELINE config 4's animals and
+             # panel size on a 50k-SNP panel), device-resident only
+             ("config4shape", 5000, 50000, 5000, 32))
+    for name, n, p, k, pop in cases:
         rng = np.random.default_rng(3)
         geno = O.synth_geno(rng, n, p)
         tmp = tempfile.mkdtemp()
@@ -95,20 +99,23 @@ def main():
             assert np.array_equal(d_fit.cpu().numpy(), got)
             eng.close()
         seq_dev = alt["TBLUP_FOLD_FUSE"]
+        line = {"config": name, "pop": pop, "k": k,
+                "device_one_fold_ms": round(one_dev, 3), "device_k_folds_ms": round(folds_dev, 3),
+                "device_ratio": round(folds_dev / one_dev, 2),
+                "device_k_folds_unshared_ms": round(alt["TBLUP_FOLD_SHARE"], 3),
+                "device_k_folds_unfused_ms": round(seq_dev, 3),
+                "device_ratio_unfused": round(seq_dev / one_dev, 2)}
+        if name == "config4shape":
+            print(json.dumps(line), flush=True)
+            continue
         random.seed(1)
         np.random.seed(1)
         one = timed_evals(E.BlupParallelEvaluator(gp, pp, 0.4), make_pop, 5)
         random.seed(1)
         np.random.seed(1)
         intra = timed_evals(E.IntraGCVBlupParallelEvaluator(gp, pp, 0.4, n_folds=5), make_pop, 5)
-        print(json.dumps({"config": name, "pop": pop,
-                          "device_one_fold_ms": round(one_dev, 3), "device_k_folds_ms": round(folds_dev, 3),
-                          "device_ratio": round(folds_dev / one_dev, 2),
-                          "device_k_folds_unshared_ms": round(alt["TBLUP_FOLD_SHARE"], 3),
-                          "device_k_folds_unfused_ms": round(seq_dev, 3),
-                          "device_ratio_unfused": round(seq_dev / one_dev, 2),
-                          "one_split_ms": round(one, 3), "intragcv_ms": round(intra, 3),
-                          "ratio": round(intra / one, 2)}), flush=True)
+        line.update({"one_split_ms": round(one, 3), "intragcv_ms": round(intra, 3), "ratio": round(intra / one, 2)})
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
