@@ -234,17 +234,6 @@ bool use_last_term(const tblup_ctx* c, const SysDims& sd, int64_t B) {
   return sd.NT >= 2 && (c->last_term == 1 || (c->last_term < 0 && B <= LT_MAX_B));
 }
 
-// Column 0 inside the diagonal launch (k_chol.hip column0_units): each diagonal workgroup runs its
-// individual's column-0 tiles with X_0 still in its LDS, and the off-diagonal launch of column 0
-// goes.  SNP form with k_sys_tiles' counts only (the units read them), and not with the last-term
-// mode (its tile (1, 0) unit feeds diagonal 1).  Auto from FUSE0_MIN_B individuals: below it the
-// diagonal launch leaves CUs idle that the separate launch's units would use.
-constexpr int64_t FUSE0_MIN_B = 192;
-bool use_fuse_col0(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int64_t B) {
-  if (!sys_tiles(d, sd) || use_last_term(c, sd, B)) return false;
-  return c->fuse_col0 == 1 || (c->fuse_col0 < 0 && B >= FUSE0_MIN_B);
-}
-
 size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k,
                    bool with_ebv) {
   size_t s = 0;
@@ -415,15 +404,13 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
                 d.nRp, d.nRp / 4, ft, u, scal, c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
                 Pp, Qb};
   cl.kd = kdb;
-  const bool fuse0 = use_st && use_fuse_col0(c, d, sd, B);
-  if (fuse0) cl.skip |= FLAG_FUSE_COL0;
   cl.padskip = (sd.form == FORM_PRIMAL && sd.pad_first) ? 1 : 0;
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
   if (c->wg_trace) {
     int64_t nwg = 0;
-    for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + DTR_RECS + ((J == 0 && fuse0) ? 0 : offdiag_grid(plan[J], B));
+    for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
     if (use_chain(c, sd, B)) nwg += B * sd.NT * (sd.NT + 1) / 2;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
@@ -466,21 +453,16 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     // forward-substitution GEMV (the exact system tiles are counted under KC_GRM)
     const double lt_d = Qb ? 0.0 : std::min(jt, 1.0);   // the last SYRK term's share of this launch
     // (+ the D-units when they run in this launch: 128^3 per L < J, as in the off-diagonal launch)
-    double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt) + (p.ndd ? Bd * T3 * jt : 0.0);
-    double bd = Bd * (TILE * TILE * lt_d * 8.0 + 2.0 * TILE * TILE * 8.0) +
-                (p.ndd ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
-    const bool fused_units = (J == 0 && fuse0 && p.nI > 0);   // column 0's T-units run in this launch
-    if (fused_units) {
-      fd += Bd * p.nI * T3;                                   // GEMM2 (no GEMM1 at J = 0)
-      bd += Bd * p.nI * 2.0 * TILE * TILE * 8.0;
-    }
+    const double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt) + (p.ndd ? Bd * T3 * jt : 0.0);
+    const double bd = Bd * (TILE * TILE * lt_d * 8.0 + 2.0 * TILE * TILE * 8.0) +
+                      (p.ndd ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
       c->wgt_used += B * (1 + p.ndd) + DTR_RECS;
     }
     rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, p, s); });
     if (rc) return rc;
-    if (p.nI > 0 && !fused_units) {
+    if (p.nI > 0) {
       // T-units: GEMM1 over the L not summed ahead (2*128^3 each) + the triangular solve 128^3;
       // P-units: 2*128^3 per L < J; D-unit: 128^3 per L < J (lower half); the fused int8 GRM
       // tiles' int-ops are excluded
@@ -612,7 +594,6 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
-  if (const char* e = getenv("TBLUP_FUSE_COL0")) c->fuse_col0 = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;

@@ -97,7 +97,6 @@ struct tblup_ctx {
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
-  int fuse_col0 = -1;    // TBLUP_FUSE_COL0: column 0's tiles in the diagonal launch (-1 auto: use_fuse_col0)
   int fold_share = 1;    // TBLUP_FOLD_SHARE: 0 builds every fold's system tiles from its own rows
   // SNP form: the padding rows (ns - k) lead the system, so the contractions over block column 0
   // skip them (TBLUP_PAD_FIRST=0: trailing padding, equal up to rounding -- a test knob).

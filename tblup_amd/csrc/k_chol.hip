@@ -1087,12 +1087,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   dstamp(a, 29);
 }
 
-__device__ void column0_units(const CholArgs& a, int64_t b, double* lds);
-
 // Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
-// K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.  Column 0 (FLAG_FUSE_COL0):
-// the workgroup then runs its individual's column-0 tiles itself (column0_units), replacing the
-// off-diagonal launch of column 0.
+// K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
 __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
   __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
   __shared__ double rsh[MAXT][TILE];
@@ -1108,7 +1104,6 @@ __global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
   // individual b on the XCD that runs its off-diagonal tiles (same L2 for L, S, X, w)
   const int64_t b = xcd_remap(blockIdx.x, a.B);
   diag_tile(a, b, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
-  if (a.J == 0 && (a.skip & FLAG_FUSE_COL0)) column0_units(a, b, lds);
   tr.done(WGT_DIAG, a.J, a.J, b);
 }
 
@@ -1137,7 +1132,7 @@ __device__ __forceinline__ void kc_issue(const CholArgs& a, int64_t b, int I, in
   for (int cb = 0; cb < NCB; ++cb) kcv[cb] = *reinterpret_cast<const int2*>(kt + ((cb0 + cb) * 64 + l) * 4);
 }
 
-template <int NCB, bool WAIT_ALL = true>
+template <int NCB>
 __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int Jt, int cb0, const int2 (&kcv)[NCB],
                                       uint8_t* lds8, const double* uj_sh, const double* ui_sh, v4d (&acc)[NCB]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1148,9 +1143,8 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
   const int il = 16 * w + (l & 15);
   const bool ireal = sys_real(i0 + il, pad, nrow);
   if (a.kc) {
-    // counts issued before the u / z loads landed; exact ints -> fp64 K.  (WAIT_ALL = false: the
-    // compiler's own waits on the count registers only -- stores in flight stay in flight)
-    if constexpr (WAIT_ALL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // counts issued before the u / z loads landed; exact ints -> fp64 K
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
       const int32_t c4[4] = {(int32_t)(int16_t)(kcv[cb].x & 0xffff), (int32_t)(int16_t)(kcv[cb].x >> 16),
@@ -1225,54 +1219,6 @@ __device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, i
   }
 }
 
-// GEMM2, the L tile store and the forward-substitution update of tile (I, J) from its T^T
-// accumulators: out^T[jb] = sum_{cb<=jb} X[jb][cb] T^T[cb] (X = inv(L_JJ), xat(jb, cb, r, c) = element
-// (r, c) of X_{jb,cb}^T) -> Lt tile (I, J); w_I += L_IJ z_J.  Shared by the off-diagonal T-units
-// (X^T staged from Dinv) and the column-0 units the diagonal kernel runs itself (X in its LDS), so
-// both run the same MFMA chains.
-template <typename XAt>
-__device__ __forceinline__ void tile_finish(const CholArgs& a, int64_t b, int I, int J, const v4d (&acc)[8], XAt xat,
-                                            const double (*zj_sh)[TILE]) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int NT = a.NT;
-  const int64_t ns = a.ns, i0 = (int64_t)I * TILE;
-  double* Lout = a.L + b * (int64_t)NT * NT * TT + ((int64_t)I * NT + J) * TT;
-  double wacc[MAXT] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 1
-  for (int jb = 0; jb < NBLK; ++jb) {
-    v4d o = {0.0, 0.0, 0.0, 0.0};
-    if (!(a.skip & 128)) {
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) {
-        if (cb <= jb) {
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) o = mfma64(xat(jb, cb, 4 * kk + (l >> 4), l & 15), acc[cb][kk], o);
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int jl = 16 * jb + (l >> 4) + 4 * r, il = 16 * w + (l & 15);
-      Lout[jl * TILE + il] = o[r];
-#pragma unroll
-      for (int tr = 0; tr < MAXT; ++tr) wacc[tr] += o[r] * zj_sh[tr][jl];
-    }
-  }
-  // w_I[i] += sum_j L_IJ[i][j] z_J[j]: reduce the 4 lane groups that share a column i
-#pragma unroll
-  for (int tr = 0; tr < MAXT; ++tr) {
-    if (tr < a.nt) {
-      double v = wacc[tr];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if ((l >> 4) == 0) {
-        const int64_t gi = (b * a.nt + tr) * ns + i0 + 16 * w + l;
-        a.w[gi] = (J == 0) ? v : a.w[gi] + v;
-      }
-    }
-  }
-}
-
 // T-unit: tile (I, J).
 __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, int ahead_cur, double* lds,
                                           double* uj_sh, double* ui_sh, double (*zj_sh)[TILE]) {
@@ -1325,7 +1271,41 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  tile_finish(a, b, I, J, acc, [&](int jb, int cb, int r, int c) { return xl[pk(jb, cb) + bo(r, c)]; }, zj_sh);
+  double wacc[MAXT] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 1
+  for (int jb = 0; jb < NBLK; ++jb) {
+    v4d o = {0.0, 0.0, 0.0, 0.0};
+    if (!(a.skip & 128)) {
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        if (cb <= jb) {
+          const double* xb = xl + pk(jb, cb);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) o = mfma64(xb[bo(4 * kk + (l >> 4), l & 15)], acc[cb][kk], o);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int jl = 16 * jb + (l >> 4) + 4 * r, il = 16 * w + (l & 15);
+      Lout[jl * TILE + il] = o[r];
+#pragma unroll
+      for (int tr = 0; tr < MAXT; ++tr) wacc[tr] += o[r] * zj_sh[tr][jl];
+    }
+  }
+  // w_I[i] += sum_j L_IJ[i][j] z_J[j]: reduce the 4 lane groups that share a column i
+#pragma unroll
+  for (int tr = 0; tr < MAXT; ++tr) {
+    if (tr < a.nt) {
+      double v = wacc[tr];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if ((l >> 4) == 0) {
+        const int64_t gi = (b * a.nt + tr) * ns + i0 + 16 * w + l;
+        a.w[gi] = (J == 0) ? v : a.w[gi] + v;
+      }
+    }
+  }
   // last-term mode: the diagonal tile J+1's last SYRK term L_{J+1,J} L_{J+1,J}^T from the tile
   // just stored (read back through the same stage ring and MFMA chains the diagonal kernel would
   // run, so its T = S - Q is bit-identical)
@@ -1337,42 +1317,6 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
     for (int i = 0; i < 5; ++i) qa[i] = v4d{0.0, 0.0, 0.0, 0.0};
     syrk_lower8_32(Lout, 8, lds, qa, 0, J == 0 ? skip_rows(a, b) : 0);
     store_syrk_blocks(a.q + b * (int64_t)NPACK * BLKD, nullptr, qa, 0);
-  }
-}
-
-// Column 0 inside the diagonal launch (FLAG_FUSE_COL0, SNP form with k_sys_tiles' counts): the
-// tiles (I, 0), I = 1 .. NT-1, of individual b by the workgroup that has just factorised L_00 --
-// X_0 is still in its LDS (no staging), no GEMM1 (J = 0), the counts of tile I+1 in flight while
-// tile I runs; the same K values and MFMA chains as the off-diagonal kernel's T-units (k_acc,
-// tile_finish), so bit-identical.  The off-diagonal launch of column 0 is then skipped.  (Its
-// T-units are GEMM2 only, 28 us each at two workgroups per CU: the launch was bound by its
-// staging, stores and three-and-a-half rounds of units, and cost a launch boundary.)
-__device__ void column0_units(const CholArgs& a, int64_t b, double* lds) {
-  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
-  const int t = threadIdx.x;
-  const int NT = a.NT;
-  const double* Xp = lds + NPACK * BLKD;                       // X_0 = L_00^{-1}, packed blocks
-  uint8_t* scratch = reinterpret_cast<uint8_t*>(lds);          // (k_acc's int8 path only; unused with counts)
-  __syncthreads();   // z_0 (diag_z) stored
-  if (t < TILE) {
-    uj_sh[t] = a.u[b * a.prow + t];
-#pragma unroll
-    for (int tr = 0; tr < MAXT; ++tr) zj_sh[tr][t] = (tr < a.nt) ? a.z[(b * a.nt + tr) * a.ns + t] : 0.0;
-  }
-  int2 kcv[8], kcn[8];
-  kc_issue<8>(a, b, 1, 0, 0, kcv);
-#pragma unroll
-  for (int cb = 0; cb < 8; ++cb) kcn[cb] = int2{0, 0};
-  for (int I = 1; I < NT; ++I) {
-    if (t < TILE) ui_sh[t] = a.u[b * a.prow + (int64_t)I * TILE + t];
-    __syncthreads();
-    v4d acc[8];
-    k_acc<8, false>(a, b, I, 0, 0, kcv, scratch, uj_sh, ui_sh, acc);
-    if (I + 1 < NT) kc_issue<8>(a, b, I + 1, 0, 0, kcn);
-    tile_finish(a, b, I, 0, acc, [&](int jb, int cb, int r, int c) { return Xp[pk(jb, cb) + bo(c, r)]; }, zj_sh);
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) kcv[cb] = kcn[cb];
-    __syncthreads();   // ui_sh reused
   }
 }
 

@@ -72,7 +72,6 @@ __host__ __device__ __forceinline__ int64_t snp_col(int64_t p, int64_t P) {
   return p < 0 ? 0 : (p >= P ? P - 1 : p);
 }
 constexpr int FLAG_WRITE_LJJ = 1 << 16;   // CholLaunch::skip: also store L_JJ (debug readback only)
-constexpr int FLAG_FUSE_COL0 = 1 << 20;   // CholLaunch::skip: the diagonal launch J = 0 runs column 0's tiles
 
 // System dimensions of one chunk.
 struct SysDims {

@@ -5,11 +5,10 @@ the two solve kernels (k_solve: one workgroup per individual; k_solve_chain: an 
 block rows and tiles over the chip, chosen for small batches) share one arithmetic, and the
 diagonal tile's last SYRK term runs the same MFMA chains whether the diagonal launch or the
 previous launch's tile (J, J-1) workgroup computes it, and the diagonal
-target's partial sum runs in the off-diagonal launch or beside the diagonal one, and column 0's
-tiles run in their own launch or inside the diagonal launch (SNP form), so fitness
+target's partial sum runs in the off-diagonal launch or beside the diagonal one, so fitness
 and EBVs must be bit-identical under every setting, for both system forms and for system sizes
 from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS / TBLUP_SOLVE_CHAIN /
-TBLUP_LAST_TERM / TBLUP_PAD_FIRST / TBLUP_DIAG_D / TBLUP_FUSE_COL0 are read when a context is created.)"""
+TBLUP_LAST_TERM / TBLUP_PAD_FIRST / TBLUP_DIAG_D are read when a context is created.)"""
 import os
 
 import numpy as np
@@ -32,7 +31,6 @@ SETTINGS = [
     {"TBLUP_LAST_TERM": "0"},                       # ... in the diagonal launch
     {"TBLUP_DIAG_D": "1"},                          # diagonal-target partials in the diagonal launches
     {"TBLUP_DIAG_D": "0"},                          # ... in the off-diagonal launches
-    {"TBLUP_FUSE_COL0": "1", "TBLUP_LAST_TERM": "0"},   # column 0's tiles in the diagonal launch
 ]
 
 

@@ -24,8 +24,7 @@ pytestmark = pytest.mark.gpu
 
 EBV_RTOL = 1e-9
 FIT_ATOL = 1e-9
-KNOBS_OFF = {"TBLUP_AHEAD": "0", "TBLUP_SOLVE_CHAIN": "0", "TBLUP_DIAG_D": "0", "TBLUP_LAST_TERM": "0",
-             "TBLUP_FUSE_COL0": "0"}
+KNOBS_OFF = {"TBLUP_AHEAD": "0", "TBLUP_SOLVE_CHAIN": "0", "TBLUP_DIAG_D": "0", "TBLUP_LAST_TERM": "0"}
 
 
 def _relmax(a, b):
@@ -101,21 +100,6 @@ def test_config3_shard_auto_policies(panel, B):
     np.testing.assert_array_equal(off[1], ebv)
     for i in sorted({0, B // 2, B - 1}):
         f, e = O.blup_grm_form(genomes[i], p["T"], p["V"], p["geno"], p["pheno"], 0.4)
-        assert abs(fit[i] - f) <= FIT_ATOL, i
-        assert _relmax(ebv[i], e) <= EBV_RTOL, i
-
-
-def test_config2_pop256_fused_column0(panel):
-    """Config 2 as benchmarked (B = 256: column 0's tiles inside the diagonal launch, the automatic
-    policy from 192 individuals) against the separate column-0 launch (TBLUP_FUSE_COL0=0), bit for
-    bit, and against the oracle."""
-    p = panel
-    fit, ebv = _run(p, p["genomes"])
-    off = _run(p, p["genomes"], {"TBLUP_FUSE_COL0": "0"})
-    np.testing.assert_array_equal(off[0], fit)
-    np.testing.assert_array_equal(off[1], ebv)
-    for i in (3, 130, 254):
-        f, e = O.blup_grm_form(p["genomes"][i], p["T"], p["V"], p["geno"], p["pheno"], 0.4)
         assert abs(fit[i] - f) <= FIT_ATOL, i
         assert _relmax(ebv[i], e) <= EBV_RTOL, i
 
