@@ -268,21 +268,19 @@ class _RowBlocks:
     def reserve(self, shape):
         """Pre-size torch's caching host allocator for blocks of `shape`: the steady state holds
         keep_for + 2 blocks at once (the kept older ones, the current population's, the one being
-        filled), so page-lock that many once, in a background thread on the first generation --
-        otherwise every generation until the pool is full pins a fresh block (~10 ms per 100 MB)."""
+        filled), so page-lock that many once, on the first generation -- otherwise every
+        generation until the pool is full pins a fresh block (~10 ms per 100 MB).  Synchronously:
+        page-locking from a background thread (round 4) contended with the generation's own HIP
+        calls and made generations 2-12 slower (18 ms vs 12 ms at config 2) than pinning them
+        one by one."""
         key = tuple(int(x) for x in shape)
         if key in self._reserved:
             return
         self._reserved.add(key)
-        import threading
-
         import torch
         n = self.keep_for(8 * int(np.prod(key))) + 2
-
-        def pin():   # page-locking is host work: off the generation's critical path
-            bufs = [torch.empty(key, dtype=torch.float64, pin_memory=True) for _ in range(n)]
-            del bufs   # back to the caching allocator, page-locked
-        threading.Thread(target=pin, name="tblup-pin", daemon=True).start()
+        bufs = [torch.empty(key, dtype=torch.float64, pin_memory=True) for _ in range(n)]
+        del bufs   # back to the caching allocator, page-locked
 
     def rows(self, block):
         import weakref
