@@ -216,8 +216,9 @@ bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
 }
 
 // SNP-form solve: the chained kernel up to CHAIN_MAX_B individuals (measured at config 2: solve
-// 0.175 -> 0.078 ms at B = 32, 0.184 -> 0.102 at 64, 0.199 -> 0.166 at 128, even at 192, 0.238 ->
-// 0.305 at 256, where one workgroup per individual already streams L at the HBM rate)
+// 0.175 -> 0.071 ms at B = 32, 0.184 -> 0.092 at 64, 0.199 -> 0.151 at 128 (round 4's block-row
+// units; round 3's tile units: 0.078 / 0.102 / 0.162), even at 192 (round 3), 0.238 -> 0.274 at
+// 256, where one workgroup per individual already streams L near the HBM rate)
 constexpr int64_t CHAIN_MAX_B = 160;
 bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B) {
   return sd.form == FORM_PRIMAL && (c->solve_chain == 1 || (c->solve_chain < 0 && B <= CHAIN_MAX_B));
@@ -412,7 +413,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     int64_t nwg = 0;
     for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
-    if (use_chain(c, sd, B)) nwg += B * sd.NT * (sd.NT + 1) / 2;   // chained solve units
+    if (use_chain(c, sd, B)) nwg += B * sd.NT;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
     wgt = (uint64_t*)c->wgt.p;
@@ -515,7 +516,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     chp = &ch;
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
-      c->wgt_used += B * sd.NT * (sd.NT + 1) / 2;
+      c->wgt_used += B * sd.NT;
     }
   }
   rc = timed(c, s, KC_SOLVE, fs, bs, [&] { return launch_solve(cl, chp, d_fit, d_ebv, s); });

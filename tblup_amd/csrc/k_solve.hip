@@ -391,33 +391,39 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 
 
 // ===========================================================================
-// Chained back substitution (SNP form): an individual's solve spread over the chip.
-//   F(b, J)     block row J: v = z_J - sum_{K > J} c_{K->J} (K ascending), beta_J = X_J^T v
-//               (X_J's rows prefetched), beta_J published; then block J's share of the
-//               prediction, sum_{a in J} x_va beta_a; F(b, 0) finally adds the shares (J
-//               ascending) and forms the fitness
-//   T(b, J, I)  tile (J, I), I < J: c_{J->I} = L_JI^T beta_J, the tile in registers before
-//               beta_J arrives
+// Chained back substitution (SNP form): an individual's solve spread over the chip, one 512-thread
+// unit U(b, J) per block row J:
+//   while it waits: X_J (72 KiB) into LDS by LDS-DMA and tile (J, J-1) into registers;
+//   v = z_J - sum_{K > J} c_{K->J} (K ascending; c_{K->J} from unit K), beta_J = X_J^T v;
+//   c_{J->J-1} = L_{J,J-1}^T beta_J from the registers, published at once -- the chain's only
+//   hand-off per block row -- then the tiles (J, I), I = J-2 .. 0, streamed (each c_{J->I} published
+//   as it is done: unit I takes its terms in K order, and the nearest rows are needed first);
+//   then block J's share of the prediction, sum_{a in J} x_va beta_a, and of the centring term;
+//   U(b, 0) finally adds the shares (J ascending) and forms the fitness.
 // The one-workgroup-per-individual k_solve streams an individual's 4.7 MB (config 2) through one
-// CU at ~30 GB/s and waits out the block-row chain on top; here every tile is read by its own
-// workgroup and only the hand-offs stay on the chain.
-// Grid order: for J = NT-1 .. 0: F(., J), then T(., J, I < J).  A unit waits only on units with
-// smaller block ids (F(b, J) on T(b, K > J, J), T(b, J, I) on F(b, J), F(b, 0) on F(b, J > 0)),
-// and each XCD dispatches its share in block-id order, so the waits drain.  Argument: let u be the
-// smallest block id not yet dispatched.  u's XCD is full, and every block resident there has an
-// id < u, so the smallest waiting unit w anywhere has w < u: every unit it waits on (ids < w) is
-// dispatched, and, being smaller than w, is not waiting -- it runs to completion.  Workgroups of
-// other kernels (other streams, other processes) holding CU slots only delay dispatch; they end
-// on their own.  The one assumption is the per-XCD in-order dispatch of one kernel's blocks, an
-// observed hardware behaviour, not a documented guarantee -- hence the bound on every wait:
-// CHAIN_SPIN_MAX polls, after which the unit stores the call's seq into ch.err (every later wait
-// of the same call gives up at once), raises the context's sticky status word ch.expired, and
-// the host entries fail the call with TBLUP_ERR_STATE (device entries: tblup_solve_error /
-// tblup_status_async) -- an error, never a silent NaN fitness.  Every sum has a fixed order, so
-// the results do not depend on B, the timing or the grid.
+// CU at ~30 GB/s and waits out the block-row chain on top; here the tile stream of every block row
+// runs on its own CU beside the chain.  (Round 3's form -- a unit per tile, each holding its tile in
+// registers until beta_J arrived, and two hand-offs per block row (F -> T -> F) -- spent most of its
+// time with the chip's unit slots full of waiting tile units: 0.162 ms at pop 128.)
+// Grid order: level J = NT-1 .. 0, individuals within a level.  A unit waits only on units with
+// smaller block ids (U(b, J) on U(b, K > J)), and each XCD dispatches its share in block-id order, so
+// the waits drain.  Argument: let u be the smallest block id not yet dispatched.  u's XCD is full,
+// and every block resident there has an id < u, so the smallest waiting unit w anywhere has w < u:
+// every unit it waits on (ids < w) is dispatched, and, being smaller than w, is not waiting -- it
+// runs to completion.  Workgroups of other kernels (other streams, other processes) holding CU
+// slots only delay dispatch; they end on their own.  The one assumption is the per-XCD in-order
+// dispatch of one kernel's blocks, an observed hardware behaviour, not a documented guarantee --
+// hence the bound on every wait: CHAIN_SPIN_MAX polls, after which the unit stores the call's seq
+// into ch.err (every later wait of the same call gives up at once), raises the context's sticky
+// status word ch.expired, and the host entries fail the call with TBLUP_ERR_STATE (device
+// entries: tblup_solve_error / tblup_status_async) -- an error, never a silent NaN fitness.  Every
+// sum has a fixed order, the same as k_solve's, so the results do not depend on B, the timing or
+// the grid, and equal k_solve's bit for bit.  With 8 | B an individual's units share one XCD
+// (block id = level * B + b), so its hand-offs stay in one L2.
 // ===========================================================================
 constexpr int CTH = 512;
-enum { WGT_SROW = 7, WGT_STILE = 8 };
+enum { WGT_SROW = 7 };
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // profiling only (TBLUP_WG_TRACE): {start, end, kind << 56 | I << 40 | b, J | (first wait done - start) << 16}
 struct ChainTrace {
@@ -444,9 +450,6 @@ struct ChainTrace {
   }
 };
 
-__device__ __forceinline__ int32_t* flag_beta(const SolveChain& ch, int64_t b, int NT, int J) {
-  return ch.flags + b * chain_flags(NT) + J;
-}
 __device__ __forceinline__ int32_t* flag_part(const SolveChain& ch, int64_t b, int NT, int I, int J) {
   return ch.flags + b * chain_flags(NT) + NT + I * NT + J;
 }
@@ -458,8 +461,10 @@ __device__ __forceinline__ int32_t* flag_e(const SolveChain& ch, int64_t b, int 
 // stores have completed (s_waitcnt vmcnt(0) + barrier), the flag; the consumer polls the flag
 // and reads the data with sc1 loads.  No acquire/release fences: on gfx950 those are an L2
 // invalidate (buffer_inv sc1) per poll and an L2 write-back (buffer_wbl2 sc1) per publish, which
-// measured 25 us per hand-off and slowed every other workgroup of the XCD.
-// mode (TBLUP_CHAIN_SYNC): 0 = this, 1 = acquire/release atomics on the flag (reference).
+// measured 25 us per hand-off and slowed every other workgroup of the XCD.  This relies on the
+// gfx950 (CDNA3/4) coherence of sc1 accesses, so the library is built for gfx950 only (Makefile);
+// mode (TBLUP_CHAIN_SYNC): 0 = this, 1 = acquire/release atomics on the flag (reference;
+// tests/test_gpu_shapes.py checks the two bit for bit).
 template <typename T>
 __device__ __forceinline__ T cload(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -508,22 +513,23 @@ __device__ __forceinline__ void chain_publish(int32_t* f, int32_t seq, int mode)
   }
 }
 
-template <int NTR>
-__device__ void chain_tile(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, int I, double (*bsh)[TILE],
-                           int* sh, ChainTrace& tr_) {
-  const int t = threadIdx.x, rc = t >> 3, seg = t & 7;   // rows rc and rc + 64, 8 threads per row
+// rows rc and rc + 64 of tile (J, I) (transposed storage: row r = column 128 I + r of L, block J),
+// 16 contiguous doubles at 16 seg each
+__device__ __forceinline__ void chain_tile_load(const CholLaunch& c, int64_t b, int J, int I, int rc, int seg,
+                                                v2d (&x)[2][8]) {
   const int NT = c.sd.NT;
-  const int64_t ns = c.sd.ns;
   const double* tile = c.L + ((b * NT + J) * (int64_t)NT + I) * TILE * TILE + 16 * seg;
-  v2d x[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[h][e] = *reinterpret_cast<const v2d*>(tile + (rc + 64 * h) * TILE + 2 * e);
-  if (!chain_wait(flag_beta(ch, b, NT, J), ch, sh)) return;
-  tr_.waited();
-  for (int i = t; i < NTR * TILE; i += CTH) bsh[i / TILE][i % TILE] = cload(ch.beta + (b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE);
-  __syncthreads();
+}
+
+// c_{J->I} = L_JI^T beta_J (beta_J in bsh) -> cpart, then its flag
+template <int NTR>
+__device__ __forceinline__ void chain_tile_publish(const SolveChain& ch, int64_t b, int NT, int J, int I,
+                                                   const v2d (&x)[2][8], const double (*bsh)[TILE], int rc,
+                                                   int seg) {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     double p[NTR];
@@ -533,18 +539,17 @@ __device__ void chain_tile(const CholLaunch& c, const SolveChain& ch, int64_t b,
       if (seg == 0) cstore(ch.cpart + (((b * NT + I) * NT + J) * NTR + tr) * TILE + rc + 64 * h, p[tr]);
   }
   chain_publish(flag_part(ch, b, NT, I, J), ch.seq, ch.mode);
-  tr_.done(WGT_STILE, J, I, b);
 }
 
+// The unit of block row J.  xl: 72 KiB of LDS -- X_J, then (U(b, 0)) the EBVs.
 template <int NTR>
-__device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, double* fit, double* ebv,
-                          double* eall, int* sh, ChainTrace& tr_) {
-  __shared__ double zsh[NTR][TILE];
-  __shared__ double vsh[NTR][TILE];
-  __shared__ double bsh[NTR][TILE];
+__device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, double* fit, double* ebv,
+                           double* xl, int* sh, ChainTrace& tr_) {
+  __shared__ double vsh[NTR][TILE];   // z_J, then v
+  __shared__ double bsh[NTR][TILE];   // beta_J
   __shared__ int32_t rowp[TILE];
   __shared__ double red[4 * 16];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int NT = c.sd.NT;
   const int64_t ns = c.sd.ns, nV = c.d.nV, nTp = c.d.nTp;
   const double* sc = c.scal + b * SCAL;
@@ -552,49 +557,63 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
   // rows of block J up to the last real one (system row r holds selected SNP r - pad; the leading
   // padding rows read the zero split row P)
   const int nr = (int)max((int64_t)0, min((int64_t)TILE, pad + kk - (int64_t)J * TILE));
-  for (int i = t; i < NTR * TILE; i += CTH) zsh[i / TILE][i % TILE] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
+  const int rc = t >> 3, seg = t & 7;   // rows rc and rc + 64, 8 threads per row
+  // X_J (packed lower blocks, each transposed: Dinv's layout) into LDS, 9 x 16 B per thread
+  {
+    const double* Dj = c.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
+#pragma unroll
+    for (int e = 0; e < NPACK * BLKD / 2 / CTH; ++e) {
+      const int chunk = (e * (CTH / 64) + w) * 64;
+      __builtin_amdgcn_global_load_lds(Dj + 2 * (chunk + l), (lds_ptr_t)(xl + 2 * chunk), 16, 0, 0);
+    }
+  }
+  v2d x[2][8];
+  if (J > 0) chain_tile_load(c, b, J, J - 1, rc, seg, x);
+  for (int i = t; i < NTR * TILE; i += CTH) vsh[i / TILE][i % TILE] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
   for (int r = t; r < nr; r += CTH) {
     const int64_t g = (int64_t)J * TILE + r;
     rowp[r] = (g < pad) ? (int32_t)c.d.P : (int32_t)snp_col(c.idx[o0 + g - pad], c.d.P);
   }
-  // X_J's rows rc and rc + 64 before the wait
-  const int rc = t >> 3, seg = t & 7;
-  const double* Dj = c.Dinv + (b * NT + J) * (int64_t)NPACK * BLKD;
-  v2d xr[2][8];
-  bool xok[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) xok[h] = xrow_load(Dj, rc + 64 * h, seg, xr[h]);
   for (int K = J + 1; K < NT; ++K)
     if (!chain_wait(flag_part(ch, b, NT, J, K), ch, sh)) {
       if (J == 0 && t == 0) fit[b] = __builtin_nan("");
       return;
     }
   tr_.waited();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X_J in LDS, z_J, the row table
   __syncthreads();
   for (int i = t; i < NTR * TILE; i += CTH) {   // v = z_J - sum_{K > J} c_{K->J}, K ascending
     const int tr = i / TILE, cc = i % TILE;
     double acc = 0.0;
     for (int K = J + 1; K < NT; ++K) acc += cload(ch.cpart + (((b * NT + J) * NT + K) * NTR + tr) * TILE + cc);
-    vsh[tr][cc] = zsh[tr][cc] - acc;
+    vsh[tr][cc] = vsh[tr][cc] - acc;
   }
   __syncthreads();
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < 2; ++h) {   // beta_J = X_J^T v
+    v2d xr[8];
+    const bool ok = xrow_load(xl, rc + 64 * h, seg, xr);
     double s2[NTR];
-    xrow_apply<NTR>(xr[h], xok[h], rc + 64 * h, seg, vsh, s2);
+    xrow_apply<NTR>(xr, ok, rc + 64 * h, seg, vsh, s2);
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr)
-      if (seg == 0) {
-        cstore(ch.beta + (b * NTR + tr) * ns + (int64_t)J * TILE + rc + 64 * h, s2[tr]);
-        bsh[tr][rc + 64 * h] = s2[tr];
-      }
+      if (seg == 0) bsh[tr][rc + 64 * h] = s2[tr];
   }
-  if (ch.delay > 0 && b == 0 && J == NT - 1) {   // debug knob (expiry test): a late producer
-    for (int i = 0; i < ch.delay; ++i) __builtin_amdgcn_s_sleep(127);
+  __syncthreads();
+  if (J > 0) {
+    if (ch.delay > 0 && b == 0 && J == NT - 1) {   // debug knob (expiry test): a late producer
+      for (int i = 0; i < ch.delay; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+    chain_tile_publish<NTR>(ch, b, NT, J, J - 1, x, bsh, rc, seg);
+    for (int I = J - 2; I >= 0; --I) {
+      chain_tile_load(c, b, J, I, rc, seg, x);
+      chain_tile_publish<NTR>(ch, b, NT, J, I, x, bsh, rc, seg);
+    }
   }
-  chain_publish(flag_beta(ch, b, NT, J), ch.seq, ch.mode);
 
-  // block J's share of the prediction and of the centring term, every trait in one pass
+  // block J's share of the prediction and of the centring term, every trait in one pass: units
+  // J > 0 to epart, U(b, 0) into LDS (X_0 is done with)
+  double* eall = xl;
   const int rg = t & 7;
   const int64_t nq = (nV + 3) / 4;
   for (int64_t qd = t >> 3; qd < nq; qd += CTH / 8) {
@@ -606,8 +625,10 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
       for (int j = 0; j < 4; ++j) {
         const int64_t v = 4 * qd + j;
         if (rg == 0 && v < nV) {
-          eall[tr * nV + v] = acc[tr][j];
-          if (J > 0) cstore(ch.epart + ((b * NT + J) * NTR + tr) * nV + v, acc[tr][j]);
+          if (J > 0)
+            cstore(ch.epart + ((b * NT + J) * NTR + tr) * nV + v, acc[tr][j]);
+          else
+            eall[tr * nV + v] = acc[tr][j];
         }
       }
   }
@@ -623,7 +644,7 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
     tr_.done(WGT_SROW, J, 0, b);
     return;
   }
-  // F(b, 0): EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu, J ascending; then the fitness
+  // U(b, 0): EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu, J ascending; then the fitness
   for (int K = 1; K < NT; ++K)
     if (!chain_wait(flag_e(ch, b, NT, K), ch, sh)) {
       if (t == 0) fit[b] = __builtin_nan("");
@@ -653,22 +674,17 @@ __device__ void chain_row(const CholLaunch& c, const SolveChain& ch, int64_t b, 
 template <int NTR>
 __global__ __launch_bounds__(CTH) void k_solve_chain(CholLaunch c, SolveChain ch, double* __restrict__ fit,
                                                      double* __restrict__ ebv) {
-  extern __shared__ double eall[];   // [NTR][nV]: the block's prediction share, then (F(b, 0)) the EBVs
-  __shared__ double bsh[NTR][TILE];
+  __shared__ __attribute__((aligned(16))) double xl[NPACK * BLKD];   // X_J, then (U(b, 0)) the EBVs
   __shared__ int sh;
   const int NT = c.sd.NT;
-  const int64_t B = c.B;
-  int64_t g = blockIdx.x;
-  int J = NT - 1;
-  for (; J > 0 && g >= B * (1 + J); --J) g -= B * (1 + J);
+  const int64_t g = blockIdx.x;
+  const int J = NT - 1 - (int)(g / c.B);
   ChainTrace tr(c.wgt);
-  if (g < B) {
-    chain_row<NTR>(c, ch, g, J, fit, ebv, eall, &sh, tr);
-  } else {
-    g -= B;
-    chain_tile<NTR>(c, ch, g / J, J, (int)(g % J), bsh, &sh, tr);
-  }
+  chain_unit<NTR>(c, ch, g % c.B, J, fit, ebv, xl, &sh, tr);
 }
+
+// whether the chained solve can run this batch: the EBVs of U(b, 0) fit its 72 KiB of LDS
+bool chain_fits(const CholLaunch& c) { return (int64_t)c.d.nt * c.d.nV <= (int64_t)NPACK * BLKD; }
 
 hipError_t launch_solve(const CholLaunch& c, const SolveChain* ch, double* fitness, double* ebv, hipStream_t s) {
   const size_t shm = (size_t)c.d.nt * (size_t)(c.sd.ns + c.d.nV) * sizeof(double) + (size_t)((c.sd.ns + 1) / 2) * sizeof(double);
@@ -680,22 +696,17 @@ hipError_t launch_solve(const CholLaunch& c, const SolveChain* ch, double* fitne
     hipLaunchKernelGGL(kernel, dim3((unsigned)c.B), dim3(NTH), shm, s, c, fitness, ebv);
     return hipGetLastError();
   };
-  if (ch != nullptr && c.sd.form == FORM_PRIMAL) {
-    const size_t eshm = (size_t)c.d.nt * (size_t)c.d.nV * sizeof(double);
-    const dim3 grid((unsigned)(c.B * c.sd.NT * (c.sd.NT + 1) / 2));
-    auto launch_chain = [&](const void* fn, auto kernel) -> hipError_t {
-      if (eshm > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eshm);
-        if (e != hipSuccess) return e;
-      }
-      hipLaunchKernelGGL(kernel, grid, dim3(CTH), eshm, s, c, *ch, fitness, ebv);
+  if (ch != nullptr && c.sd.form == FORM_PRIMAL && chain_fits(c)) {
+    const dim3 grid((unsigned)(c.B * c.sd.NT));
+    auto launch_chain = [&](auto kernel) -> hipError_t {
+      hipLaunchKernelGGL(kernel, grid, dim3(CTH), 0, s, c, *ch, fitness, ebv);
       return hipGetLastError();
     };
     switch (c.d.nt) {
-      case 1: return launch_chain((const void*)k_solve_chain<1>, k_solve_chain<1>);
-      case 2: return launch_chain((const void*)k_solve_chain<2>, k_solve_chain<2>);
-      case 3: return launch_chain((const void*)k_solve_chain<3>, k_solve_chain<3>);
-      case 4: return launch_chain((const void*)k_solve_chain<4>, k_solve_chain<4>);
+      case 1: return launch_chain(k_solve_chain<1>);
+      case 2: return launch_chain(k_solve_chain<2>);
+      case 3: return launch_chain(k_solve_chain<3>);
+      case 4: return launch_chain(k_solve_chain<4>);
       default: return hipErrorInvalidValue;
     }
   }

@@ -251,7 +251,7 @@ hipError_t launch_sys_tiles_folds(const CholLaunch& c, hipStream_t s);
 // per-call flags (SolveChain).
 struct SolveChain {
   int32_t* flags;   // [B][chain_flags(NT)], compared with seq (never reset)
-  double* beta;     // [B][nt][ns]
+  double* beta;     // [B][nt][ns] (unused since the block-row units keep beta_J in LDS)
   double* cpart;    // [B][NT (row I)][NT (tile J)][nt][128]: L_JI^T beta_J
   double* epart;    // [B][NT][nt][nV]: block J's share of X_V beta
   double* mbpart;   // [B][NT][nt]: block J's share of sum_a s_a beta_a
@@ -261,7 +261,7 @@ struct SolveChain {
   int32_t seq;      // this call's flag value
   int32_t mode;     // TBLUP_CHAIN_SYNC (k_solve.hip)
   int32_t spin_max; // polls before a wait gives up (CHAIN_SPIN_MAX; lowered only by the debug knob)
-  int32_t delay;    // debug knob only: F(0, NT-1) sleeps this many s_sleep(127) rounds before
+  int32_t delay;    // debug knob only: U(0, NT-1) sleeps this many s_sleep(127) rounds before
                     // publishing, so its consumers' waits expire (0 in production)
 };
 // Bound on a hand-off wait: 2^20 polls (an sc1 load round trip each plus s_sleep 2: ~0.5-1 s).

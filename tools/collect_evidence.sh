@@ -16,6 +16,7 @@ cp $(find $O/pmcs_$T -name "*counter_collection.csv" | head -1) $P/${T}_pmc_stal
 cp $O/pmc_traffic_$T.json $P/pmc_traffic.json
 cp $O/pmc_mfma_$T.json $P/pmc_mfma.json
 tail -1 $O/generation_$T.log > $P/${T}_generation.json
+for f in $O/generation_w*_$T.log; do [ -f $f ] && grep '^{' $f | tail -1; done > $P/${T}_generation_ranks.jsonl
 grep config $O/intracv_$T.log > $P/${T}_intracv.jsonl
 [ -f $O/knockout_$T.log ] && tail -1 $O/knockout_$T.log > $P/${T}_knockout.json
 cp $O/wg_trace_$T.txt $P/${T}_wg_trace.txt

@@ -26,6 +26,12 @@ timeout -k 10 400 python bench.py --steps 20 --warmup 5 --pmc-json $O/pmc_traffi
 tail -1 $O/bench_$TAG.log | cut -c1-300
 timeout -k 10 300 python tools/generation_bench.py 24 > $O/generation_$TAG.log 2>&1 || { tail -20 $O/generation_$TAG.log; exit 1; }
 tail -1 $O/generation_$TAG.log
+# the multi-rank generation path on this one GPU (gloo): 2 and 4 ranks, config 2 and config 3 populations
+for POP in 256 1024; do for W in 2 4; do
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $W --master-addr 127.0.0.1 --master-port $((29600 + W)) tools/generation_bench.py 16 $POP > $O/generation_w${W}_${POP}_$TAG.log 2>&1 || { tail -30 $O/generation_w${W}_${POP}_$TAG.log; exit 1; }
+  grep '^{' $O/generation_w${W}_${POP}_$TAG.log | tail -1 | cut -c1-300
+done; done
+timeout -k 10 300 python tools/generation_bench.py 16 1024 > $O/generation_w1_1024_$TAG.log 2>&1 || { tail -20 $O/generation_w1_1024_$TAG.log; exit 1; }
 timeout -k 10 300 python tools/intracv_bench.py > $O/intracv_$TAG.log 2>&1 || { tail -20 $O/intracv_$TAG.log; exit 1; }
 grep config $O/intracv_$TAG.log
 timeout -k 10 300 python tools/knockout_bench.py > $O/knockout_$TAG.log 2>&1 || { tail -20 $O/knockout_$TAG.log; exit 1; }

@@ -1,6 +1,6 @@
 """Timeline of the chained solve (k_solve_chain) of one config-2 evaluation (TBLUP_WG_TRACE=1):
-per group J (F units = block rows, T units = tiles (J, I)) the start / wait-done / end spread
-and the mean unit time, and the overall span.   usage: python tools/solve_trace.py [--pop N]"""
+per block row J (one unit each per individual) the start / wait-done / end spread and the mean
+unit time, and the overall span.   usage: python tools/solve_trace.py [--pop N]"""
 import os
 import sys
 
@@ -28,7 +28,7 @@ def main():
         eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(), stream_ptr=s.cuda_stream)
     torch.cuda.synchronize()
     rec = eng.wg_trace()
-    r = rec[(rec["kind"] == 7) | (rec["kind"] == 8)]
+    r = rec[rec["kind"] == 7]
     if not len(r):
         print("no chained-solve records")
         return
@@ -36,7 +36,7 @@ def main():
     us = lambda x: (x - t0) * 1e6
     print(f"pop {pop}: {len(r)} units, span {us(r['end'].max()):.1f} us")
     for J in sorted(set(r["J"].tolist()), reverse=True):
-        for kind, name in ((7, "F"), (8, "T")):
+        for kind, name in ((7, "U"),):
             m = r[(r["J"] == J) & (r["kind"] == kind)]
             if not len(m):
                 continue
