@@ -1,0 +1,6 @@
+# round 4: GEMM1 with the next k-step's A fragments interleaved with the MFMAs (scheduling groups):
+# schedule / shape tests, then A/B against HEAD at pop 256 / 128
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_schedule.py tests/test_gpu_shapes.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest_r04_sg.log 2>&1
+rc=$?; tail -3 gpurun_out/gputest_r04_sg.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/gputest_r04_sg.log | head -20; exit 1; }
+POPS="256 128" bash tools/ab_env.sh 3 "base=" "var=" 2>&1 | tee gpurun_out/r04_sg_ab.txt
