@@ -666,29 +666,40 @@ __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const 
   __syncthreads();
 }
 
-// SYRK of Lt stages restricted to the 36 lower blocks, 8 waves: wave W takes blocks
-// W + 8i (5 blocks for W < 4, 4 for W >= 4); only the i in MASK (a diagonal-target slice).
+// The 36 lower blocks over 8 waves, by block-row pairs (q, 7 - q), q = W & 3: the pair's 9 blocks
+// (7-q, 0 .. 7-q), (q, 0 .. q) in that order, the first 5 to wave q, the other 4 to wave q + 4 -- a
+// wave's blocks share their rows, so it reads 4-6 of the 8 A fragments per k-step instead of all 8
+// (round 4: the D-units' LDS reads per MFMA 1.78 -> 1.08; each block keeps its MFMA chain, so the
+// sums are unchanged bit for bit).  syrk_e(W, i): packed index of wave W's i-th block, i < syrk_nb(W).
+__host__ __device__ constexpr int syrk_nb(int W) { return W < 4 ? 5 : 4; }
+__host__ __device__ constexpr int syrk_e(int W, int i) {
+  const int q = W & 3, j = (W < 4) ? i : 5 + i, r1 = 8 - q;   // r1: blocks in row 7 - q
+  return (j < r1) ? (7 - q) * (8 - q) / 2 + j : q * (q + 1) / 2 + (j - r1);
+}
+
+// SYRK of Lt stages restricted to the 36 lower blocks, 8 waves: wave W takes blocks syrk_e(W, i),
+// i < syrk_nb(W); only the i in MASK (a diagonal-target slice).
 // PART: from k-step ks on (the first stage of a run that starts past padding rows).
 template <int W, int MASK, bool PART = false>
 __device__ __forceinline__ void syrk_stage8(const double* As, v4d (&acc)[5], int l, int ks = 0) {
-  constexpr int NBW = (W < 4) ? 5 : 4;
+  constexpr int NBW = syrk_nb(W);
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     if (PART && kk < ks) continue;
     const int k = 4 * kk + (l >> 4);
-    double a8[8];
+    double a8[8];   // the fragments no block of this wave uses are never loaded (dead)
 #pragma unroll
     for (int q = 0; q < 8; ++q) a8[q] = As[lt_off(k, 16 * q + (l & 15))];
 #pragma unroll
     for (int i = 0; i < NBW; ++i)
-      if ((MASK >> i) & 1) acc[i] = mfma64(a8[tri_q(W + 8 * i)], a8[tri_s(W + 8 * i)], acc[i]);
+      if ((MASK >> i) & 1) acc[i] = mfma64(a8[tri_q(syrk_e(W, i))], a8[tri_s(syrk_e(W, i))], acc[i]);
   }
 }
 
 // block masks of the diagonal-target slices: all blocks; even i; odd i
 __host__ __device__ constexpr int slice_mask(int sl) { return sl == 0 ? 0x1F : sl == 1 ? 0x15 : 0x0A; }
 
-// SYRK of Lt rows restricted to the 36 lower blocks, 8 waves (wave W takes blocks W + 8i, i in
+// SYRK of Lt rows restricted to the 36 lower blocks, 8 waves (wave W takes blocks syrk_e(W, i), i in
 // slice_mask(sl)), on 32-row stages through a 2 x 32 KiB LDS-DMA ring: one barrier per 32 k rows.
 // r0 (a multiple of 4): leading rows skipped, as in gemm1_a32 (zero padding columns of block
 // column 0): whole stages, then the first stage computed from k-step (r0 & 31) / 4.
@@ -764,8 +775,8 @@ __device__ __forceinline__ void store_syrk_blocks(double* dst, const double* bas
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    const int e = w + 8 * i;
-    if (e < NPACK && ((slice_mask(sl) >> i) & 1)) {
+    const int e = syrk_e(w, i);
+    if (i < syrk_nb(w) && ((slice_mask(sl) >> i) & 1)) {
       const int q = tri_q_rt(e), sb = e - q * (q + 1) / 2;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -788,8 +799,8 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
   if (a.kd) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-      const int e = w + 8 * i;
-      kv[i] = (e < NPACK && ((slice_mask(sl) >> i) & 1)) ? kd_load(a, b, Jt, e) : int2{0, 0};
+      const int e = syrk_e(w, i);
+      kv[i] = (i < syrk_nb(w) && ((slice_mask(sl) >> i) & 1)) ? kd_load(a, b, Jt, e) : int2{0, 0};
     }
   }
   if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc, sl, skip_rows(a, b));
@@ -800,8 +811,8 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
   }
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    const int e = w + 8 * i;
-    if (e < NPACK && ((slice_mask(sl) >> i) & 1)) kd_block(a, b, Jt, e, kv[i], acc[i], dst);
+    const int e = syrk_e(w, i);
+    if (i < syrk_nb(w) && ((slice_mask(sl) >> i) & 1)) kd_block(a, b, Jt, e, kv[i], acc[i], dst);
   }
 }
 
@@ -944,8 +955,8 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       syrk_lower8_32(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const int e = w + DW * i;
-        if (e < NPACK) {
+        const int e = syrk_e(w, i);
+        if (i < syrk_nb(w)) {
           const int q = tri_q_rt(e);
           double* blk = Tp + pk(q, e - q * (q + 1) / 2);
 #pragma unroll
