@@ -676,6 +676,19 @@ __host__ __device__ constexpr int syrk_e(int W, int i) {
   const int q = W & 3, j = (W < 4) ? i : 5 + i, r1 = 8 - q;   // r1: blocks in row 7 - q
   return (j < r1) ? (7 - q) * (8 - q) / 2 + j : q * (q + 1) / 2 + (j - r1);
 }
+// every lower block exactly once
+constexpr bool syrk_map_ok() {
+  int seen[NPACK] = {};
+  for (int W = 0; W < 8; ++W)
+    for (int i = 0; i < syrk_nb(W); ++i) {
+      const int e = syrk_e(W, i);
+      if (e < 0 || e >= NPACK || seen[e]++) return false;
+    }
+  for (int e = 0; e < NPACK; ++e)
+    if (seen[e] != 1) return false;
+  return true;
+}
+static_assert(syrk_map_ok(), "SYRK block map must cover the 36 lower blocks once");
 
 // SYRK of Lt stages restricted to the 36 lower blocks, 8 waves: wave W takes blocks syrk_e(W, i),
 // i < syrk_nb(W); only the i in MASK (a diagonal-target slice).
