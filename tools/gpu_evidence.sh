@@ -39,9 +39,9 @@ tail -1 $O/knockout_$TAG.log
 timeout -k 10 200 python tools/wg_trace.py $O/wg_trace_$TAG.npy > $O/wg_trace_$TAG.txt 2>&1 || { tail -20 $O/wg_trace_$TAG.txt; exit 1; }
 timeout -k 10 200 python tools/wg_trace.py $O/wg_trace128_$TAG.npy --pop 128 > $O/wg_trace128_$TAG.txt 2>&1 || { tail -20 $O/wg_trace128_$TAG.txt; exit 1; }
 timeout -k 10 400 python bench.py --config config4 --steps 5 --warmup 2 > $O/bench_config4_$TAG.log 2> $O/bench_config4_$TAG.err || { tail -20 $O/bench_config4_$TAG.err; exit 1; }
-timeout -k 10 300 python bench.py --config config5 --steps 10 --warmup 3 > $O/bench_config5_$TAG.log 2> $O/bench_config5_$TAG.err || { tail -20 $O/bench_config5_$TAG.err; exit 1; }
+timeout -k 10 300 python bench.py --config config5 --steps 20 --warmup 5 > $O/bench_config5_$TAG.log 2> $O/bench_config5_$TAG.err || { tail -20 $O/bench_config5_$TAG.err; exit 1; }
 for P in 32 64 128; do
-timeout -k 10 300 python bench.py --pop $P --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_pop${P}_$TAG.log 2> $O/bench_pop${P}_$TAG.err || { tail -20 $O/bench_pop${P}_$TAG.err; exit 1; }
+timeout -k 10 300 python bench.py --pop $P --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_pop${P}_$TAG.log 2> $O/bench_pop${P}_$TAG.err || { tail -20 $O/bench_pop${P}_$TAG.err; exit 1; }
 done
 timeout -k 10 300 python bench.py --config config3 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_config3_$TAG.log 2> $O/bench_config3_$TAG.err || { tail -20 $O/bench_config3_$TAG.err; exit 1; }
 for c in config3 config4 config5 pop32 pop64 pop128; do tail -1 $O/bench_${c}_$TAG.log | cut -c1-200; done
