@@ -172,23 +172,24 @@ __device__ __forceinline__ void xrow_apply(const v2d (&xr)[8], bool ok, int row,
 }
 
 // block J's share of the SNP-form prediction for animals 4 qd .. 4 qd + 3, every trait: sum over
-// the block's rows r = rg, rg + 8, .. < nr of x_va beta_r (int8 split rows, V animals from byte
-// nTp; beta[tr * bstride + r]), then xor-reduced over the 8 row groups
+// the block's rows r = rg, rg + 8, .. < nr of x_va beta_r (the 2-bit packed split rows: one byte
+// holds the four animals, animal 4q + i at bits 2i; V animals from byte nTp / 4 -- a quarter of the
+// int8 rows' bytes; beta[tr * bstride + r]), then xor-reduced over the 8 row groups
 template <int NTR>
-__device__ __forceinline__ void pred_share(const int8_t* gs, int64_t gs_row, const int32_t* rowp, const double* beta,
-                                           int64_t bstride, int nr, int64_t off, int rg, double (&acc)[NTR][4]) {
+__device__ __forceinline__ void pred_share(const uint8_t* gp, int64_t gp_row, const int32_t* rowp, const double* beta,
+                                           int64_t bstride, int nr, int64_t qoff, int rg, double (&acc)[NTR][4]) {
 #pragma unroll
   for (int tr = 0; tr < NTR; ++tr)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[tr][j] = 0.0;
 #pragma unroll 4
   for (int r = rg; r < nr; r += 8) {
-    const uint32_t xw = *reinterpret_cast<const uint32_t*>(gs + (int64_t)rowp[r] * gs_row + off);
+    const uint32_t xb = gp[(int64_t)rowp[r] * gp_row + qoff];
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr) {
       const double bv = beta[tr * bstride + r];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[tr][j] = __builtin_fma((double)((xw >> (8 * j)) & 0xff), bv, acc[tr][j]);
+      for (int j = 0; j < 4; ++j) acc[tr][j] = __builtin_fma((double)((xb >> (2 * j)) & 3u), bv, acc[tr][j]);
     }
   }
 #pragma unroll
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       const int nr = (int)max((int64_t)0, min((int64_t)TILE, kk - (int64_t)J * TILE));
       for (int64_t qd = t >> 3; qd < ((c.skip & 2048) ? 0 : nq); qd += NTH / 8) {
         double acc[NTR][4];
-        pred_share<NTR>(c.ft.gs[fo], c.gs_row, rowp + J * TILE, alpha + J * TILE, ns, nr, nTp + 4 * qd, rg8, acc);
+        pred_share<NTR>(c.ft.gpk[fo], c.gpk_row, rowp + J * TILE, alpha + J * TILE, ns, nr, nTp / 4 + qd, rg8, acc);
 #pragma unroll
         for (int tr = 0; tr < NTR; ++tr)
 #pragma unroll
@@ -618,7 +619,7 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
   const int64_t nq = (nV + 3) / 4;
   for (int64_t qd = t >> 3; qd < nq; qd += CTH / 8) {
     double acc[NTR][4];
-    pred_share<NTR>(c.ft.gs[fold_of(c.ft, b)], c.gs_row, rowp, &bsh[0][0], TILE, nr, nTp + 4 * qd, rg, acc);
+    pred_share<NTR>(c.ft.gpk[fold_of(c.ft, b)], c.gpk_row, rowp, &bsh[0][0], TILE, nr, nTp / 4 + qd, rg, acc);
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr)
 #pragma unroll
