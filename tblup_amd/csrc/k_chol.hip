@@ -304,9 +304,19 @@ __device__ __forceinline__ void kd_block(const CholArgs& a, int64_t b, int J, in
     dst[pk(q, sb) + bo((l >> 4) + 4 * r, l & 15)] = v - sub[r];
   }
 }
+// The exact count tiles are written once (k_sys_tiles) and read once (the unit that forms their K):
+// non-temporal accesses, so that 235 MB of them a step do not push the Lt tiles out of the caches
+__device__ __forceinline__ int2 nt_load2(const int16_t* p) {
+  const long long v = __builtin_nontemporal_load(reinterpret_cast<const long long*>(p));
+  return int2{(int)(unsigned)(v & 0xffffffffll), (int)(v >> 32)};
+}
+__device__ __forceinline__ void nt_store2(int16_t* p, int2 v) {
+  __builtin_nontemporal_store((long long)(((unsigned long long)(unsigned)v.y << 32) | (unsigned)v.x),
+                              reinterpret_cast<long long*>(p));
+}
 __device__ __forceinline__ int2 kd_load(const CholArgs& a, int64_t b, int J, int e) {
   const int l = threadIdx.x & 63;
-  return *reinterpret_cast<const int2*>(a.kd + ((b * a.NT + J) * KD_TILE) + (e * 64 + l) * 4);
+  return nt_load2(a.kd + ((b * a.NT + J) * KD_TILE) + (e * 64 + l) * 4);
 }
 
 // Leading contraction rows of block column 0 that a GEMM1 / SYRK run starting at L = 0 skips:
@@ -1153,7 +1163,7 @@ __device__ __forceinline__ void kc_issue(const CholArgs& a, int64_t b, int I, in
   const int NT = a.NT;
   const int16_t* kt = a.kc + ((b * (NT * (NT - 1) / 2)) + I * (I - 1) / 2 + Jt) * KC_TILE + w * 8 * 64 * 4;
 #pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) kcv[cb] = *reinterpret_cast<const int2*>(kt + ((cb0 + cb) * 64 + l) * 4);
+  for (int cb = 0; cb < NCB; ++cb) kcv[cb] = nt_load2(kt + ((cb0 + cb) * 64 + l) * 4);
 }
 
 template <int NCB>
@@ -1556,7 +1566,7 @@ __device__ __forceinline__ void store_counts16_any(int16_t* kt, const v4f (&cnt)
       const v4f c = cnt[m][n];
       const int2 packed = {(int)((uint32_t)((int)c[0] & 0xffff) | ((uint32_t)(int)c[1] << 16)),
                            (int)((uint32_t)((int)c[2] & 0xffff) | ((uint32_t)(int)c[3] << 16))};
-      *reinterpret_cast<int2*>(kt + ((diag ? cb * (cb + 1) / 2 + ib : ib * 8 + cb) * 64 + l) * 4) = packed;
+      nt_store2(kt + ((diag ? cb * (cb + 1) / 2 + ib : ib * 8 + cb) * 64 + l) * 4, packed);
     }
 }
 
