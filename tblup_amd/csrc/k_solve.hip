@@ -113,6 +113,24 @@ __device__ __forceinline__ double pearson_abs(const double* e, const double* yV,
 }
 
 
+// Sum over the 8 lanes 8m .. 8m + 7 (every lane gets it), by DPP instead of ds_bpermute: xor 1 and xor 2
+// by quad_perm, then each lane adds the other quad's sum through row_half_mirror (lane i <-> 7 - i of
+// each 8): the same two quad sums the xor-4 butterfly adds, so the same bits; DPP moves 32 bits, so a
+// double crosses in two halves.
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double sum8(double v) {
+  v += dpp64<0xB1>(v);    // quad_perm [1, 0, 3, 2]: xor 1
+  v += dpp64<0x4E>(v);    // quad_perm [2, 3, 0, 1]: xor 2
+  v += dpp64<0x141>(v);   // row_half_mirror
+  return v;
+}
+
 // ---- arithmetic shared by k_solve and k_solve_chain (the SNP-form results of the two are
 // bit-identical, so the launcher may pick either per batch) ----
 constexpr int PCTH = 512;   // Pearson / centring-term reductions as over 512 threads
@@ -132,9 +150,7 @@ __device__ __forceinline__ void tile_row_partial(const v2d (&x)[8], const double
                             __builtin_fma(x[e][0], beta[tr * stride + 16 * seg + 2 * e], p[tr]));
 #pragma unroll
   for (int tr = 0; tr < NTR; ++tr) {
-    p[tr] += __shfl_xor(p[tr], 1);
-    p[tr] += __shfl_xor(p[tr], 2);
-    p[tr] += __shfl_xor(p[tr], 4);
+    p[tr] = sum8(p[tr]);
   }
 }
 
@@ -165,9 +181,7 @@ __device__ __forceinline__ void xrow_apply(const v2d (&xr)[8], bool ok, int row,
   }
 #pragma unroll
   for (int tr = 0; tr < NTR; ++tr) {
-    s2[tr] += __shfl_xor(s2[tr], 1);
-    s2[tr] += __shfl_xor(s2[tr], 2);
-    s2[tr] += __shfl_xor(s2[tr], 4);
+    s2[tr] = sum8(s2[tr]);
   }
 }
 
@@ -196,9 +210,7 @@ __device__ __forceinline__ void pred_share(const uint8_t* gp, int64_t gp_row, co
   for (int tr = 0; tr < NTR; ++tr)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      acc[tr][j] += __shfl_xor(acc[tr][j], 1);
-      acc[tr][j] += __shfl_xor(acc[tr][j], 2);
-      acc[tr][j] += __shfl_xor(acc[tr][j], 4);
+      acc[tr][j] = sum8(acc[tr][j]);
     }
 }
 
