@@ -405,6 +405,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
                 d.nRp, d.nRp / 4, ft, u, scal, c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
                 Pp, Qb};
   cl.kd = kdb;
+  cl.sys_st = c->sys_st;
   cl.padskip = (sd.form == FORM_PRIMAL && sd.pad_first) ? 1 : 0;
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
@@ -429,7 +430,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     const double bg = (double)B * ((ntri - sd.NT) * KC_TILE * 2.0 + (sd.NT - nd8) * KD_TILE * 2.0 + nd8 * KD_TILE * 8.0);
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
-      c->wgt_used += B * sd.NT * (sd.NT + 1) / 2;
+      const int64_t sg = fold_share ? -(B * sd.NT * (sd.NT + 1) / 2) : sys_tiles_grid(cl);
+      c->wgt_used += sg > 0 ? sg : -sg;
     }
     rc = timed(c, s, KC_GRM, fg, bg, [&] {
       return fold_share ? launch_sys_tiles_folds(cl, s) : launch_sys_tiles(cl, s);
@@ -595,6 +597,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
+  if (const char* e = getenv("TBLUP_SYS_ST")) c->sys_st = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;

@@ -98,6 +98,8 @@ struct tblup_ctx {
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
   int fold_share = 1;    // TBLUP_FOLD_SHARE: 0 builds every fold's system tiles from its own rows
+  int sys_st = -1;       // TBLUP_SYS_ST: system tiles by the persistent super-tile kernel (k_sys_tiles_st):
+                         // -1 auto (sys_tiles_grid), 0 never, 1 whenever it applies -- the same exact counts
   // SNP form: the padding rows (ns - k) lead the system, so the contractions over block column 0
   // skip them (TBLUP_PAD_FIRST=0: trailing padding, equal up to rounding -- a test knob).
   int pad_first = 1;

@@ -50,6 +50,24 @@ constexpr int NSLOT = TBLUP_NSLOT;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// LDS-DMA of 16 B per lane (lane i -> lds + 16 i) as inline asm, for the stage rings.  The compiler
+// sees __builtin_amdgcn_global_load_lds as an LDS write in flight and waits vmcnt(0) before the
+// next LDS read of ANY address (ROCm 7.2, checked in the emitted code): in a ring that issues
+// stage s + 1 and then reads stage s, that wait drained the prefetch, so every stage's load
+// latency was exposed.  Hidden from the compiler, the DMA is ordered by the ring's own counted
+// s_waitcnt + barrier, which every reader of a stage sits behind.  (No other code in these kernels
+// uses m0: the emitted code has no m0 reader besides the LDS-DMA instructions.)
+__device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory");
+}
+#ifndef TBLUP_AB_ASM_SYRK   // A/B builds only (tools/ab_build_defs.sh): the SYRK ring's DMA as inline asm
+#define TBLUP_AB_ASM_SYRK 1
+#endif
+#ifndef TBLUP_AB_ASM_GEMM1   // the GEMM1 ring's DMA as inline asm
+#define TBLUP_AB_ASM_GEMM1 1
+#endif
+
 // Stage image [16 k][128 x] of an Lt tile: 16-B chunk p of row k holds source chunk
 // p ^ 8(k&1), so the fragment pattern (16 x in one k row, the next k in lanes 16-31)
 // covers all 64 banks.  One LDS-DMA instruction moves one 1 KiB k row.
@@ -620,8 +638,11 @@ __device__ __forceinline__ void gemm1_a32(const double* __restrict__ ltJ, const 
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = 4 * w + e;
-      __builtin_amdgcn_global_load_lds(ltJ + src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(slot + k * TILE), 16,
-                                       0, 0);
+      if constexpr (TBLUP_AB_ASM_GEMM1)
+        glds16_asm(ltJ + src + k * TILE + 2 * (l ^ (8 * (k & 1))), slot + k * TILE);
+      else
+        __builtin_amdgcn_global_load_lds(ltJ + src + k * TILE + 2 * (l ^ (8 * (k & 1))), (lds_ptr_t)(slot + k * TILE),
+                                         16, 0, 0);
     }
   };
   const double* bcol = ltI + 16 * w + (l & 15) + (l >> 4) * TILE;
@@ -738,8 +759,11 @@ __device__ __forceinline__ void syrk_lower8_32(const double* __restrict__ src, i
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = 4 * w + e;
-      __builtin_amdgcn_global_load_lds(src + (int64_t)s * AS + k * TILE + 2 * (l ^ (8 * (k & 1))),
-                                       (lds_ptr_t)(slot + k * TILE), 16, 0, 0);
+      if constexpr (TBLUP_AB_ASM_SYRK)
+        glds16_asm(src + (int64_t)s * AS + k * TILE + 2 * (l ^ (8 * (k & 1))), slot + k * TILE);
+      else
+        __builtin_amdgcn_global_load_lds(src + (int64_t)s * AS + k * TILE + 2 * (l ^ (8 * (k & 1))),
+                                         (lds_ptr_t)(slot + k * TILE), 16, 0, 0);
     }
   };
   issue(s0);
@@ -1668,6 +1692,218 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
   tr.done(WGT_SYS, J, I, b);
 }
 
+// Persistent super-tile form of k_sys_tiles (large batches, sys_tiles_grid): one 8-wave workgroup
+// per CU walks a contiguous run of units, a unit being a 256 x 256 super-tile = the 2 x 2 tiles
+// (I0 + ti, J0 + tj), I0 = 2 SI, J0 = 2 SJ, SI >= SJ, of one individual (10 units at NT = 8 instead
+// of 36 tile workgroups).  Per 256-animal stage a unit loads 2 x 256 rows (32 KiB: half the bytes
+// per tile of the single-tile form) and runs 64 MFMAs per wave: wave (tj, qr, qc) accumulates
+// quadrant (qr, qc) of tiles (I0, J0 + tj) and (I0 + 1, J0 + tj) (A fragments shared).  The
+// 3-deep LDS-DMA ring runs on across unit boundaries (the next unit's first stages load while
+// this one's last stage computes and its counts are stored), so the per-tile prologue and store
+// latency of 36 short workgroups is paid once per run.  Row addresses come from a per-individual
+// row table in LDS (no global load whose use would drain the ring).  The same exact fp32 counts as
+// k_sys_tiles (every partial sum an integer below 2^24), stored to the same places.
+constexpr int SPW = 8;                 // waves per super-tile workgroup
+constexpr int SP_MAXIND = 64;          // individuals in one workgroup's run (sys_tiles_grid checks)
+
+#ifndef TBLUP_AB_SYS_ST_MIN   // A/B builds only (tools/ab_build_defs.sh)
+#define TBLUP_AB_SYS_ST_MIN 4
+#endif
+#ifndef TBLUP_AB_SP_D
+#define TBLUP_AB_SP_D 3
+#endif
+static_assert(TBLUP_AB_SP_D >= 3 && TBLUP_AB_SP_D <= 4, "ring waits are written for 1-2 stages ahead");
+constexpr int64_t SYS_ST_MIN = TBLUP_AB_SYS_ST_MIN;   // auto: at least this many units per CU
+
+__global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_t* kc, int nsu, int nunits) {
+  constexpr int D = TBLUP_AB_SP_D;     // stages in the ring
+  constexpr int TB2 = 2 * TILE * 64;   // one 256-row operand image of a stage: 16 KiB
+  __shared__ __attribute__((aligned(16))) uint8_t lds[D * 2 * TB2];   // 96 KiB at D = 3
+  __shared__ int32_t rowtab[SP_ROWTAB];
+  __shared__ int32_t cblk_tab[SP_MAXIND];   // contraction blocks of the run's individuals (no global
+                                            // load inside the ring: its use would wait vmcnt(0))
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int tj = w >> 2, qr = (w >> 1) & 1, qc = w & 1;
+  const int NT = a.NT;
+  WgTrace tr(a.wgt);
+  const int u0 = (int)((int64_t)blockIdx.x * nunits / gridDim.x), u1 = (int)((int64_t)(blockIdx.x + 1) * nunits / gridDim.x);
+  const int b_first = u0 / nsu;
+  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
+  const int pos = l & 3;
+  // super-tile s of the lower triangle (row-major): SI, SJ
+  auto unit_tiles = [&](int u, int& b, int& I0, int& J0) __attribute__((always_inline)) {
+    b = __builtin_amdgcn_readfirstlane(u / nsu);
+    const int s = __builtin_amdgcn_readfirstlane(u % nsu);
+    int SI = 0;
+    while ((SI + 1) * (SI + 2) / 2 <= s) ++SI;
+    I0 = 2 * SI;
+    J0 = 2 * (s - SI * (SI + 1) / 2);
+  };
+  // the row table of individual b: packed row index of each of its ns system rows (row P: zero)
+  int tab_b = -1;
+  auto load_rowtab = [&](int b) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
+    const int64_t pad = a.padfirst ? a.ns - k : 0;
+    const int nrt = 2 * TILE * ((NT + 1) / 2);   // rows a super-tile reads (ns rounded up to 256)
+    for (int r = t; r < nrt; r += 64 * SPW)
+      rowtab[r] = (int32_t)(r < a.ns && sys_real(r, pad, k) ? snp_col(a.idx[o0 + r - pad], a.P) : a.P);
+    __syncthreads();
+    tab_b = b;
+  };
+  // issue cursor: the unit and stage whose loads go out next, and its row pointers
+  int iu = u0, ib = 0;
+  int ist = 0, inst = 0;
+  int ra[2], rb[2];                    // packed rows of this lane's A / B loads (h = 0, 1)
+  const uint8_t* gbase = nullptr;
+  const int64_t gsr = a.gs_row;
+  const int offa[2] = {16 * (pos ^ (((l >> 2) >> 2) & 3)), 16 * (pos ^ (((16 + (l >> 2)) >> 2) & 3))};
+  const int offb[2] = {16 * (pos ^ (((l >> 2) >> 2) & 2)), 16 * (pos ^ (((16 + (l >> 2)) >> 2) & 2))};
+  auto setup_issue = [&]() __attribute__((always_inline)) {
+    int I0, J0;
+    unit_tiles(iu, ib, I0, J0);
+    if (ib != tab_b) load_rowtab(ib);
+    inst = (cblk_tab[ib - b_first] + 3) >> 2;
+    gbase = a.ft.gpk[fold_of(a.ft, ib)];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 16 * (2 * w + h) + (l >> 2);
+      ra[h] = rowtab[J0 * TILE + row];
+      rb[h] = rowtab[I0 * TILE + row];
+    }
+    ist = 0;
+  };
+  // issue one stage into ring slot g % D and advance the cursor (false: nothing left)
+  auto issue = [&](int g) __attribute__((always_inline)) {
+    if (iu >= u1) return;
+    uint8_t* slot = lds + (g % D) * 2 * TB2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      glds16_asm(gbase + (int64_t)ra[h] * gsr + (offa[h] + ist * 64), slot + (2 * w + h) * 1024);
+      glds16_asm(gbase + (int64_t)rb[h] * gsr + (offb[h] + ist * 64), slot + TB2 + (2 * w + h) * 1024);
+    }
+    if (++ist == inst && ++iu < u1) setup_issue();
+  };
+  if (u0 >= u1) return;
+  const int nind = (u1 - 1) / nsu - b_first + 1;
+  if (t < nind) cblk_tab[t] = (int32_t)a.scal[(int64_t)(b_first + t) * SCAL + SC_CBLK];
+  __syncthreads();
+  setup_issue();
+  // total stages of the run (the units of one individual share its stage count)
+  int nstages = 0;
+  for (int u = u0; u < u1;) {
+    const int b = u / nsu, ue = min(u1, (b + 1) * nsu);
+    nstages += (ue - u) * ((cblk_tab[b - b_first] + 3) >> 2);
+    u = ue;
+  }
+  for (int g = 0; g < D - 1; ++g) issue(g);
+
+  v4f cnt[2][4][4];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) cnt[ti][m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+  // compute cursor
+  int cu = u0, cb_ = 0;
+  int cI0 = 0, cJ0 = 0, cst = 0;
+  unit_tiles(cu, cb_, cI0, cJ0);
+  int cnblk = cblk_tab[cb_ - b_first];
+  int cnst = (int)((cnblk + 3) >> 2);
+  bool stored_full = false;   // the previous stage ended a unit whose every wave stored 32 count pairs
+  for (int g = 0; g < nstages; ++g) {
+    // stage g's loads done: the younger ops are the 4 loads of each stage issued after it (up to
+    // D - 2) and the stores of the unit that ended last stage (32 per wave after a full
+    // off-diagonal super-tile; any other unit: waited for)
+    const int ahead = min(D - 2, nstages - 1 - g);   // stages issued after stage g
+    if (ahead >= 2) {
+      if (stored_full)
+        asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (ahead == 1) {
+      if (stored_full)
+        asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    issue(g + D - 1);
+    const int J0t = cJ0 + tj;
+    bool comp[2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) {
+      const int I = cI0 + ti;
+      comp[ti] = I < NT && J0t < NT && (I > J0t || (I == J0t && qr >= qc));
+    }
+    if ((comp[0] || comp[1]) && !(a.skip & (1 << 18))) {
+      const uint8_t* As = lds + (g % D) * 2 * TB2;
+      const uint8_t* Bs = As + TB2;
+      const int tail_ch = (int)(cnblk & 3);
+      const bool ztail = (cst == cnst - 1 && tail_ch != 0 && ch >= tail_ch);   // past the training animals
+      uint4 aq[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) aq[m] = *reinterpret_cast<const uint4*>(As + i8off_a(TILE * tj + 16 * (4 * qr + m) + prow, ch));
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+        if (!comp[ti]) continue;
+        uint4 bq[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          bq[n] = *reinterpret_cast<const uint4*>(Bs + i8off_b(TILE * ti + 16 * (4 * qc + n) + rho, ch));
+          if (ztail) bq[n] = uint4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          v4i av[4];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) av[m] = s2 == 0 ? fp4_operand(aq[m].x, aq[m].y) : fp4_operand(aq[m].z, aq[m].w);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            const v4i bv = s2 == 0 ? fp4_operand(bq[n].x, bq[n].y) : fp4_operand(bq[n].z, bq[n].w);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)   // cbsz = blgp = 4: A, B in fp4; E8M0 scales 128 = 2.0
+              cnt[ti][m][n] = mfma_fp4_16x16x128(av[m], bv, cnt[ti][m][n], 4, 4, 0, 128, 0, 128);
+          }
+        }
+      }
+    }
+    stored_full = false;
+    if (++cst == cnst) {
+      // the unit's epilogue: its tiles' counts (diagonal tiles J < 2 too: k_sys_diag_counts forms
+      // their K_JJ + lambda I afterwards -- the fp64 epilogue here would spill the accumulators)
+      stored_full = cI0 != cJ0 && cI0 + 1 < NT && !(a.skip & (1 << 16));
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+        const int I = cI0 + ti;
+        if (!comp[ti]) continue;
+        if (!(a.skip & (I != J0t ? 1 << 16 : 1 << 17))) {
+          store_counts16_any(I != J0t ? kc + ((int64_t)cb_ * (NT * (NT - 1) / 2) + I * (I - 1) / 2 + J0t) * KC_TILE
+                                      : a.kd + ((int64_t)cb_ * NT + J0t) * KD_TILE,
+                             cnt[ti], qr, qc, l, I == J0t);
+        }
+      }
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) cnt[ti][m][n] = v4f{0.f, 0.f, 0.f, 0.f};
+      if (++cu < u1) {
+        unit_tiles(cu, cb_, cI0, cJ0);
+        cnblk = cblk_tab[cb_ - b_first];
+        cnst = (int)((cnblk + 3) >> 2);
+      }
+      cst = 0;
+    }
+  }
+  tr.done(WGT_SYS, 0, 0, u0 / nsu);
+}
+
 // Fold-fused evaluation with shared counts (IntraGCV's folds, tblup_eval_folds*): when every fold's
 // training rows R_f and validation rows V_f make up the same multiset T_all, C_{R_f} = C_{T_all} -
 // C_{V_f}.  One workgroup per (individual b, tile) accumulates C_{T_all} over fold 0's rows
@@ -1715,7 +1951,7 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles_folds(CholArgs a, int
       st = (g - nsA) % nsV;
     }
   };
-  auto issue = [&](int64_t g) {
+  auto issue = [&](int64_t g) __attribute__((always_inline)) {
     int k;
     int64_t st;
     seg_of(g, k, st);
@@ -1820,10 +2056,42 @@ static CholArgs make_args(const CholLaunch& c, int J) {
   return a;
 }
 
+static int cu_count() {
+  static int n = 0;
+  if (n <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+int64_t sys_tiles_grid(const CholLaunch& c) {
+  const int64_t ntri = (int64_t)c.sd.NT * (c.sd.NT + 1) / 2;
+  const int64_t NS = (c.sd.NT + 1) / 2, units = c.B * (NS * (NS + 1) / 2);
+  const int64_t cus = cu_count();
+  const bool st = c.sys_st > 0 || (c.sys_st < 0 && units >= SYS_ST_MIN * cus);
+  const int64_t grid = std::min(units, cus);
+  const int64_t nsu = NS * (NS + 1) / 2, per = (units + grid - 1) / grid;
+  if (!st || c.sd.ns > SP_ROWTAB || per / nsu + 2 > SP_MAXIND) return -(c.B * ntri);
+  return grid;
+}
+
 hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
   CholArgs a = make_args(c, 0);
   const int ntri = c.sd.NT * (c.sd.NT + 1) / 2;
-  hipLaunchKernelGGL(k_sys_tiles, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
+  const int64_t grid = sys_tiles_grid(c);
+  if (grid > 0) {
+    const int NS = (c.sd.NT + 1) / 2;
+    hipLaunchKernelGGL(k_sys_tiles_st, dim3((unsigned)grid), dim3(64 * SPW), 0, s, a, c.kc, NS * (NS + 1) / 2,
+                       (int)(c.B * (NS * (NS + 1) / 2)));
+    if (hipError_t e = hipGetLastError()) return e;
+    a.wgt = nullptr;
+    hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_sys_tiles, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
+  }
   return hipGetLastError();
 }
 

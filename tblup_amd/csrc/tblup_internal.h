@@ -184,6 +184,7 @@ struct CholLaunch {
   int16_t* kd;           // SNP form with k_sys_tiles: the diagonal tiles' exact counts instead of Kd,
                          // [B][NT][36 packed lower blocks][64 lanes][4] (KD_TILE int16 per tile); the
                          // consumers form K_JJ + lambda I from them (kd_block, k_chol.hip)
+  int sys_st = -1;       // k_sys_tiles_st: -1 auto, 0 never, 1 whenever it applies (TBLUP_SYS_ST)
 };
 // k_sys_tiles output: per individual NT(NT-1)/2 off-diagonal tiles (I > J, t = I(I-1)/2 + J) of
 // 128 x 128 int16 counts, in the order the off-diagonal kernel's lanes read them:
@@ -242,6 +243,10 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
 // counts into c.kc, diagonal tiles' counts into c.kd (replaces launch_diag_grm and the int8 phase
 // of the off-diagonal tiles)
 hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s);
+// its grid: > 0 the persistent super-tile kernel's workgroups (k_sys_tiles_st), else minus the
+// per-tile kernel's
+int64_t sys_tiles_grid(const CholLaunch& c);
+constexpr int SP_ROWTAB = 4096;   // k_sys_tiles_st: rows of its LDS row table (ns <= SP_ROWTAB)
 // the same for a fold-fused chunk whose folds share their train + valid rows (FoldTab::share):
 // C_{R_f} = C_{T_all} - C_{V_f}, one workgroup per (individual, tile) for all F folds
 hipError_t launch_sys_tiles_folds(const CholLaunch& c, hipStream_t s);

@@ -177,3 +177,24 @@ def test_kernel_form_folds_fused(panel):
     for i in (0, 1):
         fo, _ = O.blup_grm_form(genomes[i], folds[2][0], folds[2][1], p["geno"], p["pheno"], 0.4)
         assert abs(fused[2][i] - fo) <= FIT_ATOL
+
+
+@pytest.mark.parametrize("ks,B", [((1000,), 256), ((100, 300), 3), ((1150, 700, 1000), 37), ((1000, 640), 300)])
+def test_sys_tiles_persistent_bit_identical(panel, ks, B):
+    """The persistent super-tile system-tile kernel (k_sys_tiles_st: 2 x 2 tiles per unit, one
+    workgroup per CU walking a run of units, LDS-DMA ring across unit boundaries) against the
+    per-tile kernel: every tile count is exact, so the results are bit-identical -- odd and even
+    tile counts (NT 1..9), runs that cross individuals (B = 37, 300), B = 256 by default (auto)."""
+    p = panel
+    rng = np.random.default_rng(71 + B)
+    genomes = [rng.choice(50_000, ks[i % len(ks)], replace=False) for i in range(B)]
+    st = _run(p, genomes, {"TBLUP_SYS_ST": "1"})
+    tile = _run(p, genomes, {"TBLUP_SYS_ST": "0"})
+    np.testing.assert_array_equal(st[0], tile[0])
+    np.testing.assert_array_equal(st[1], tile[1])
+    if B == 256:
+        auto = _run(p, genomes)
+        np.testing.assert_array_equal(auto[0], tile[0])
+    for i in (0, B - 1):
+        f, _ = O.blup_grm_form(genomes[i], p["T"], p["V"], p["geno"], p["pheno"], 0.4)
+        assert abs(st[0][i] - f) <= FIT_ATOL, i
