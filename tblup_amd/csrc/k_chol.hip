@@ -67,6 +67,17 @@ __device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
 #ifndef TBLUP_AB_ASM_GEMM1   // the GEMM1 ring's DMA as inline asm
 #define TBLUP_AB_ASM_GEMM1 1
 #endif
+#ifndef TBLUP_AB_ASM_I8   // the integer-count rings' DMA (int8 / packed tiles, per-tile system tiles) as inline asm
+#define TBLUP_AB_ASM_I8 1
+#endif
+// one ring DMA: inline asm (A) or the builtin
+template <bool A>
+__device__ __forceinline__ void ring_glds(const void* g, void* lds) {
+  if constexpr (A)
+    glds16_asm(g, lds);
+  else
+    __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)lds, 16, 0, 0);
+}
 
 // Stage image [16 k][128 x] of an Lt tile: 16-B chunk p of row k holds source chunk
 // p ^ 8(k&1), so the fragment pattern (16 x in one k row, the next k in lanes 16-31)
@@ -434,8 +445,8 @@ __device__ __forceinline__ void i8_tt8(const int8_t* sa, const int8_t* sb, int64
   constexpr int TB = TILE * KBLK;
   auto issue = [&](int64_t kb) {
     int8_t* slot = lds + (int)(kb % D) * 2 * TB;
-    __builtin_amdgcn_global_load_lds(sa + kb * kstep, (lds_ptr_t)(slot + w * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(sb + kb * kstep, (lds_ptr_t)(slot + TB + w * 1024), 16, 0, 0);
+    ring_glds<TBLUP_AB_ASM_I8>(sa + kb * kstep, slot + w * 1024);
+    ring_glds<TBLUP_AB_ASM_I8>(sb + kb * kstep, slot + TB + w * 1024);
   };
   for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
   const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
@@ -481,8 +492,8 @@ __device__ __forceinline__ void i8_tt8_pk64(const uint8_t* sa, const uint8_t* sb
   constexpr int TB = TILE * 64;
   auto issue = [&](int64_t st) {
     uint8_t* slot = lds + (int)(st % D) * 2 * TB;
-    __builtin_amdgcn_global_load_lds(sa + st * 64, (lds_ptr_t)(slot + w * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(sb + st * 64, (lds_ptr_t)(slot + TB + w * 1024), 16, 0, 0);
+    ring_glds<TBLUP_AB_ASM_I8>(sa + st * 64, slot + w * 1024);
+    ring_glds<TBLUP_AB_ASM_I8>(sb + st * 64, slot + TB + w * 1024);
   };
   for (int64_t st = 0; st < D - 1 && st < nst; ++st) issue(st);
   const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
@@ -548,8 +559,8 @@ __device__ __forceinline__ void i8_tt2d_pk64(const uint8_t* sa, const uint8_t* s
       for (int h = 0; h < 2; ++h) {
         const int64_t hs = 2 * st + h;
         if (hs < nh) {
-          __builtin_amdgcn_global_load_lds(sa + hs * 64, (lds_ptr_t)(slot + h * 2 * TB + w * 1024), 16, 0, 0);
-          __builtin_amdgcn_global_load_lds(sb + hs * 64, (lds_ptr_t)(slot + h * 2 * TB + TB + w * 1024), 16, 0, 0);
+          ring_glds<TBLUP_AB_ASM_I8>(sa + hs * 64, slot + h * 2 * TB + w * 1024);
+          ring_glds<TBLUP_AB_ASM_I8>(sb + hs * 64, slot + h * 2 * TB + TB + w * 1024);
         }
       }
     };
@@ -1637,8 +1648,8 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
     uint8_t* slot = lds + (int)(st % D) * 2 * TB;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      __builtin_amdgcn_global_load_lds(sa[h] + st * 64, (lds_ptr_t)(slot + (2 * w + h) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(sb[h] + st * 64, (lds_ptr_t)(slot + TB + (2 * w + h) * 1024), 16, 0, 0);
+      ring_glds<TBLUP_AB_ASM_I8>(sa[h] + st * 64, slot + (2 * w + h) * 1024);
+      ring_glds<TBLUP_AB_ASM_I8>(sb[h] + st * 64, slot + TB + (2 * w + h) * 1024);
     }
   };
   v4f cnt[4][4];
@@ -1959,8 +1970,8 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles_folds(CholArgs a, int
     uint8_t* slot = lds + (int)(g % D) * 2 * TB;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      __builtin_amdgcn_global_load_lds(base + oa[h], (lds_ptr_t)(slot + (2 * w + h) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(base + ob[h], (lds_ptr_t)(slot + TB + (2 * w + h) * 1024), 16, 0, 0);
+      ring_glds<TBLUP_AB_ASM_I8>(base + oa[h], slot + (2 * w + h) * 1024);
+      ring_glds<TBLUP_AB_ASM_I8>(base + ob[h], slot + TB + (2 * w + h) * 1024);
     }
   };
   v4f cnt[4][4];

@@ -1,0 +1,12 @@
+# integer-count rings (int8 / packed tiles, per-tile and fold system tiles) with inline-asm DMA:
+# parity suites, then interleaved A/B at pop 32 / 64, config 4 (kernel form) and IntraGCV folds
+set -e -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_schedule.py tests/test_gpu_shapes.py tests/test_gpu_parity.py tests/test_gpu_system.py > gpurun_out/r04_asmi8_test.log 2>&1 || { tail -30 gpurun_out/r04_asmi8_test.log; exit 1; }
+tail -2 gpurun_out/r04_asmi8_test.log
+POPS="64 32" bash tools/ab_env.sh 2 'base=' 'var=' 2>&1 | tee gpurun_out/r04_asmi8_ab.txt
+for r in 1 2; do for v in base var; do
+  TBLUP_GPU_LIB=ab/$v.so timeout -k 10 300 python bench.py --config config4 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/c4_$v.log 2> gpurun_out/c4_$v.err
+  python3 -c "import json;d=json.loads(open('gpurun_out/c4_$v.log').read().strip().splitlines()[-1]);print('config4', '$v', d['value'], d['kernel_ms_per_step'])" | tee -a gpurun_out/r04_asmi8_ab.txt
+done; done
