@@ -11,13 +11,14 @@ import json
 from collections import defaultdict
 
 CLASSES = {"k_indiv_stats": "stats", "k_gather": "gather", "k_grm": "grm", "k_diag_grm": "grm", "k_diag_grm8": "grm",
-           "k_sys_tiles": "grm",
+           "k_sys_tiles": "grm", "k_sys_tiles_st": "grm", "k_sys_diag_counts": "grm",
            "k_chol_diag": "chol_diag", "k_chol_offdiag": "chol_offdiag", "k_solve": "solve",
            "k_de_step": "de_step", "k_decode_topk": "decode", "k_snp_scan": "snp_scan"}
 
 
 def per_class(path, counter):
-    acc = defaultdict(list)
+    """{class: {kernel: [bytes per launch]}}"""
+    acc = defaultdict(lambda: defaultdict(list))
     with open(path) as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] != counter:
@@ -25,8 +26,14 @@ def per_class(path, counter):
             name = row["Kernel_Name"]
             for key, cls in CLASSES.items():
                 if "::" + key + "(" in name or "::" + key + "<" in name:
-                    acc[cls].append(float(row["Counter_Value"]) * 1024.0)
+                    acc[cls][key].append(float(row["Counter_Value"]) * 1024.0)
     return acc
+
+
+def class_mean(kernels):
+    """a class's bytes per launch: the sum over its kernels of each one's mean per launch (the
+    system tiles are two kernels per step: k_sys_tiles_st + k_sys_diag_counts)"""
+    return sum(sum(v) / len(v) for v in kernels.values())
 
 
 def main():
@@ -44,12 +51,12 @@ def main():
     for cls in CLASSES.values():
         if cls not in fetch or cls not in write:
             continue
-        f = 2.0 * sum(fetch[cls]) / len(fetch[cls])
-        w = sum(write[cls]) / len(write[cls])
+        f = 2.0 * class_mean(fetch[cls])
+        w = class_mean(write[cls])
         out["per_launch_bytes"][cls] = round(f + w)
         out["per_launch_fetch_bytes"][cls] = round(f)
         out["per_launch_write_bytes"][cls] = round(w)
-        out["launches"][cls] = len(fetch[cls])
+        out["launches"][cls] = max(len(v) for v in fetch[cls].values())
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out["per_launch_bytes"]))
 
