@@ -1827,7 +1827,8 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
   for (int g = 0; g < nstages; ++g) {
     // stage g's loads done: the younger ops are the 4 loads of each stage issued after it (up to
     // D - 2) and the stores of the unit that ended last stage (32 per wave after a full
-    // off-diagonal super-tile; any other unit: waited for)
+    // off-diagonal super-tile: 16 8-B stores per tile whose addresses lie 512 B apart within a
+    // lane, so none can be merged; any other unit: waited for)
     const int ahead = min(D - 2, nstages - 1 - g);   // stages issued after stage g
     if (ahead >= 2) {
       if (stored_full)
