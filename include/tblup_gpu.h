@@ -111,8 +111,9 @@ int tblup_get_traits(tblup_ctx* ctx, int64_t* n_traits);
  *   fitness  : out, batch doubles, |pearson(EBV_V, y_V)| (NaN when undefined)
  *   ebv      : optional out (may be NULL), batch x n_valid predicted breeding values
  *              (batch x n_traits x n_valid after tblup_set_traits)
- * Synchronous; host pointers.  TBLUP_ERR_STATE if a chained-solve hand-off wait expired
- * (tblup_solve_error); the outputs are then invalid.
+ * Synchronous; host pointers.  A chained solve (SNP form, small chunks) whose bounded hand-off
+ * wait expires does not fail the call: the chunk's factor is solved again by the one-workgroup
+ * back substitution, bit-identical to an unexpired run, and counted (tblup_chain_recoveries).
  */
 int tblup_eval_batch(tblup_ctx* ctx, int split_id, const int64_t* idx, const int64_t* offsets,
                      int64_t batch, double h2, int branch, double* fitness, double* ebv);
@@ -290,12 +291,18 @@ int tblup_index_error(tblup_ctx* ctx, void* stream, int* flag);
 
 /* Solve-error flag: the chained back substitution (SNP form, small batches) hands block rows
  * between workgroups and bounds every wait; a wait that gives up leaves the batch's fitnesses
- * invalid.  The synchronous entries (tblup_eval_batch, tblup_eval_folds) then fail with
- * TBLUP_ERR_STATE; after device entries read the flag here: synchronises `stream` (NULL = the
- * context's stream), *flag = 1 if a wait expired since the last read, clears it.  (The reference
- * has no such failure mode -- a dead worker hangs its parent, tblup/evaluator.py:397-398; here it
- * is an error, never a silent NaN.) */
+ * invalid.  The synchronous entries (tblup_eval_batch, tblup_eval_folds) recover by themselves
+ * (the chunk's solve re-run through k_solve; tblup_chain_recoveries counts it) and never raise
+ * this flag; after device entries read it here: synchronises `stream` (NULL = the context's
+ * stream), *flag = 1 if a wait expired since the last read, clears it -- the caller re-evaluates
+ * through a synchronous entry (the drop-in evaluator does).  (The reference has no such failure
+ * mode -- a dead worker hangs its parent, tblup/evaluator.py:397-398; here it is an error or a
+ * recovery, never a silent NaN.) */
 int tblup_solve_error(tblup_ctx* ctx, void* stream, int* flag);
+
+/* Number of chunks the synchronous entries re-solved after an expired chained-solve wait since
+ * the context was created (each one cost one extra back substitution). */
+int tblup_chain_recoveries(tblup_ctx* ctx, int64_t* count);
 
 /* Both status words without synchronising: enqueues on `stream` (NULL = the context's stream) a
  * copy of {index error, solve error} (2 x int32, nonzero = raised) into `host_status`

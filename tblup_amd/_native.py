@@ -52,6 +52,7 @@ SIGNATURES = {
     "tblup_index_error": (_c.c_int, [_P, _P, _c.POINTER(_c.c_int)]),
     "tblup_solve_error": (_c.c_int, [_P, _P, _c.POINTER(_c.c_int)]),
     "tblup_status_async": (_c.c_int, [_P, _P, _P]),
+    "tblup_chain_recoveries": (_c.c_int, [_P, _I64P]),
     "tblup_host_register": (_c.c_int, [_P, _c.c_int64]),
     "tblup_host_unregister": (_c.c_int, [_P]),
     "tblup_get_wg_trace": (_c.c_int, [_P, _c.POINTER(_c.c_uint64), _c.c_int64, _I64P]),

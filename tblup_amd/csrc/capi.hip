@@ -117,6 +117,17 @@ struct Carve {
   }
 };
 
+// TBLUP_DBG_SKIP (phase ablation, results wrong when set): honoured by diagnostic builds only
+// (tools/ab_build_defs.sh 'diag=-DTBLUP_DIAG_BUILD'); the production library ignores it
+inline int dbg_skip(const tblup_ctx* c) {
+#ifdef TBLUP_DIAG_BUILD
+  return c->dbg_skip;
+#else
+  (void)c;
+  return 0;
+#endif
+}
+
 // SNP (primal) form: the batched system-tile launch (k_sys_tiles) builds every exact tile up
 // front; int16 counts stay exact while n_T <= KC_MAX_NT (beyond it, and for one-tile systems, the
 // in-tile int8 products of the off-diagonal kernel).
@@ -340,11 +351,16 @@ FoldTab single_fold(const Split& sp, int64_t B) {
 
 // Enqueue the full pipeline for one chunk whose idx/off already sit in device memory.  ftp: the
 // systems' splits when they are not all sp (fold-fused evaluation; sp is then fold 0).
+// stop_stage: 0 the whole pipeline; 1 / 2 debug readbacks (K, L); 3 the solve only, through the
+// one-workgroup k_solve, on the factor an earlier run_chunk of the same chunk left in the same
+// carve (host entries, after that run's chained solve gave up a wait: bit-identical results).
 int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& sd, hipStream_t s,
               const int64_t* d_idx, const int64_t* d_off, const int64_t* h_off, int64_t B, double h2,
               int branch, Carve& cv, double* d_fit, double* d_ebv, int stop_stage, double** K_out,
               double** z_out, const FoldTab* ftp = nullptr) {
   const FoldTab ft = ftp ? *ftp : single_fold(sp, B);
+  const bool redo = stop_stage == 3;
+  c->last_chain_seq = 0;
   double grm_flops = 0.0, gather_bytes = 0.0, stats_bytes = 0.0;
   const double tri = (double)d.nT * (d.nT + 1) / 2.0 + (double)d.nV * d.nT;
   for (int64_t b = 0; b < B; ++b) {
@@ -376,13 +392,14 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   std::vector<OffPlan> plan(sd.NT);
   for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, AHEAD_SLOTS, c->diag_d);
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
-  int rc;
-  rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
-    return launch_indiv_stats(d_idx, d_off, B, ft, csA, d, sd, branch, h2, scal, u, rhs,
-                              (int32_t*)c->status.p + ST_INDEX, s);
-  });
+  int rc = 0;
+  if (!redo)
+    rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
+      return launch_indiv_stats(d_idx, d_off, B, ft, csA, d, sd, branch, h2, scal, u, rhs,
+                                (int32_t*)c->status.p + ST_INDEX, s);
+    });
   if (rc) return rc;
-  if (sd.form == FORM_DUAL) {
+  if (sd.form == FORM_DUAL && !redo) {
     // primal rows are read in place from the split matrix: no gather
     rc = timed(c, s, KC_GATHER, 0.0, gather_bytes, [&] {
       return launch_gather(ft, d_idx, d_off, pstride, B, csA, scal, d, panel, u, s);
@@ -402,7 +419,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   }
   if (K_out) *K_out = L;
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, panel, pstride, d_off, d_idx,
-                d.nRp, d.nRp / 4, ft, u, scal, c->dbg_skip | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
+                d.nRp, d.nRp / 4, ft, u, scal, dbg_skip(c) | (stop_stage == 2 ? FLAG_WRITE_LJJ : 0), nullptr, kcb,
                 Pp, Qb};
   cl.kd = kdb;
   cl.sys_st = c->sys_st;
@@ -410,7 +427,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const double T3 = (double)TILE * TILE * TILE;
   // profiling only: room for one record per Cholesky workgroup of this chunk
   uint64_t* wgt = nullptr;
-  if (c->wg_trace) {
+  if (c->wg_trace && !redo) {
     int64_t nwg = 0;
     for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
@@ -422,7 +439,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   }
   const double kbar = B > 0 ? (double)h_off[B] / (double)B : 0.0;
   const double cbar = (sd.form == FORM_PRIMAL) ? (double)d.nT : kbar;   // contraction length
-  if (use_st) {
+  if (redo) {
+  } else if (use_st) {
     // every system tile (I >= J) in one int8 launch: int ops 2 x 128^2 x n_T per tile
     const double ntri = (double)sd.NT * (sd.NT + 1) / 2.0;
     const double fg = (double)B * ntri * 2.0 * 128.0 * 128.0 * cbar;
@@ -449,7 +467,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   // chip is already full during the off-diagonal launches, and sharing CUs slows the
   // critical path more than it hides.)
   const double Bd = (double)B;
-  for (int J = 0; J < sd.NT; ++J) {
+  for (int J = 0; !redo && J < sd.NT; ++J) {
     const double jt = (double)J;
     const OffPlan& p = plan[J];
     // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
@@ -489,8 +507,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
                                  kbar * (double)(d.nT + d.nV));
   SolveChain ch{};
   const SolveChain* chp = nullptr;
-  if (use_chain(c, sd, B)) {
-    const size_t fbytes = ((size_t)B * chain_flags(sd.NT) + 1) * 4;
+  if (!redo && use_chain(c, sd, B)) {
+    const size_t fbytes = ((size_t)B * chain_flags(sd.NT) + CHAIN_ERR_RING + 1) * 4;
     if (c->chain.bytes < fbytes || c->chain_seq >= INT32_MAX - 1) {
       HIPCHK(hipStreamSynchronize(s));   // the flags may still be read by an earlier chained solve
       if (int rc2 = dev_alloc(c, c->chain, fbytes)) return rc2;
@@ -498,14 +516,17 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       c->chain_seq = 0;
     }
     ch.flags = (int32_t*)c->chain.p;
-    ch.err = ch.flags + (c->chain.bytes / 4 - 1);
+    int32_t* ring = ch.flags + (c->chain.bytes / 4 - CHAIN_ERR_RING - 1);
     ch.beta = cv.take<double>((size_t)B * d.nt * sd.ns);
     ch.cpart = cv.take<double>((size_t)B * sd.NT * sd.NT * d.nt * TILE);
     ch.epart = cv.take<double>((size_t)B * sd.NT * d.nt * d.nV);
     ch.mbpart = cv.take<double>((size_t)B * sd.NT * d.nt);
     if (int rc2 = ws_check(c, cv)) return rc2;
-    ch.expired = (int32_t*)c->status.p + ST_SOLVE;
     ch.seq = ++c->chain_seq;
+    ch.err = ring + ch.seq % CHAIN_ERR_RING;
+    // host entries recover from their ring slot (chain_expired); device entries raise the status word
+    ch.expired = c->host_entry ? ring + CHAIN_ERR_RING : (int32_t*)c->status.p + ST_SOLVE;
+    c->last_chain_seq = ch.seq;
     ch.mode = c->chain_sync;
     ch.spin_max = CHAIN_SPIN_MAX;
     ch.delay = 0;
@@ -514,7 +535,6 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       ch.spin_max = c->chain_dbg_spin;
       ch.delay = c->chain_dbg_delay;
     }
-    c->chain_used = true;
     chp = &ch;
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
@@ -525,21 +545,27 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   return rc;
 }
 
-const char* const kChainExpired =
-    "chained solve: a block-row hand-off wait expired (CHAIN_SPIN_MAX polls); the affected "
-    "individuals' fitnesses are invalid";
-
-// Synchronous entries, after their last synchronisation: fail the call if a chained solve it ran
-// gave up a wait (the status word is sticky on the device; reading clears it).
-int check_chain_status(tblup_ctx* c) {
-  if (!c->chain_used || !c->status.p) return 0;
-  c->chain_used = false;
-  int32_t h = 0;
-  HIPCHK(hipMemcpy(&h, (int32_t*)c->status.p + ST_SOLVE, 4, hipMemcpyDeviceToHost));
-  if (h == 0) return 0;
-  HIPCHK(hipMemset((int32_t*)c->status.p + ST_SOLVE, 0, 4));
-  return fail(TBLUP_ERR_STATE, kChainExpired);
+// Host entries, after the chunk's stream synchronisation: whether the chained solve `seq` (0: none)
+// gave up a wait.  Its ring slot holds seq exactly then (slots of other calls hold their own seqs).
+int chain_expired(tblup_ctx* c, int32_t seq, bool* out) {
+  *out = false;
+  if (seq <= 0 || !c->chain.p) return 0;
+  const int32_t* ring = (const int32_t*)c->chain.p + (c->chain.bytes / 4 - CHAIN_ERR_RING - 1);
+  int32_t v = 0;
+  HIPCHK(hipMemcpyAsync(&v, ring + seq % CHAIN_ERR_RING, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *out = v == seq;
+  return 0;
 }
+
+// Marks a synchronous entry for its duration: its chained solves write their expiry to the ring
+// only (the entry re-runs the affected chunk's solve through k_solve and counts it), not to the
+// context's sticky status word that the device entries' callers read.
+struct HostEntry {
+  tblup_ctx* c;
+  explicit HostEntry(tblup_ctx* cc) : c(cc) { c->host_entry = true; }
+  ~HostEntry() { c->host_entry = false; }
+};
 
 Split* find_split(tblup_ctx* c, int id) {
   auto it = c->splits.find(id);
@@ -585,8 +611,10 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   const char* env = getenv("TBLUP_WORKSPACE_MB");
   c->budget = (size_t)(env ? atoll(env) : 32768) << 20;
+#ifdef TBLUP_DIAG_BUILD
   const char* dbg = getenv("TBLUP_DBG_SKIP");
   c->dbg_skip = dbg ? atoi(dbg) : 0;
+#endif
   const char* wt = getenv("TBLUP_WG_TRACE");
   c->wg_trace = wt && atoi(wt) != 0;
   const char* fp = getenv("TBLUP_FORM");
@@ -818,6 +846,7 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
   if (!sp) return fail(TBLUP_ERR_ARG, "unknown split id");
   if (int rc = check_indices(c, idx, offsets[batch])) return rc;
   HIPCHK(hipSetDevice(c->device));
+  HostEntry he(c);
   const EvalDims d = dims_of(c, *sp);
   const bool want_ebv = ebv != nullptr;
   const SysDims sd = choose_sys(c, d, offsets, batch, branch, c->form_pref);
@@ -845,17 +874,26 @@ int tblup_eval_batch(tblup_ctx* c, int split_id, const int64_t* idx, const int64
     for (int64_t b = 0; b <= B; ++b) hoff[b] = offsets[b0 + b] - offsets[b0];
     HIPCHK(hipMemcpyAsync(d_idx, idx + offsets[b0], (size_t)sum_k * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(d_off, hoff.data(), (size_t)(B + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    if (int rc = run_chunk(c, *sp, d, sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv, d_fit, d_ebv, 0,
-                           nullptr, nullptr))
-      return rc;
-    HIPCHK(hipMemcpyAsync(fitness + b0, d_fit, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
-    if (want_ebv)
-      HIPCHK(hipMemcpyAsync(ebv + b0 * d.nt * d.nV, d_ebv, (size_t)B * d.nt * d.nV * 8, hipMemcpyDeviceToHost,
-                            c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    const Carve cv0 = cv;
+    for (int pass = 0;; ++pass) {
+      // pass 1: the chained solve of pass 0 gave up a wait -- the same factor, solved by k_solve
+      Carve cvp = cv0;
+      if (int rc = run_chunk(c, *sp, d, sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cvp, d_fit, d_ebv,
+                             pass ? 3 : 0, nullptr, nullptr))
+        return rc;
+      const int32_t seq = c->last_chain_seq;
+      HIPCHK(hipMemcpyAsync(fitness + b0, d_fit, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
+      if (want_ebv)
+        HIPCHK(hipMemcpyAsync(ebv + b0 * d.nt * d.nV, d_ebv, (size_t)B * d.nt * d.nV * 8, hipMemcpyDeviceToHost,
+                              c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      bool expired = false;
+      if (int rc = chain_expired(c, seq, &expired)) return rc;
+      if (!expired) break;
+      ++c->chain_recoveries;
+    }
     b0 = b1;
   }
-  if (int rc = check_chain_status(c)) return rc;
   if (c->profiling) return drain_events(c);
   return 0;
 }
@@ -913,7 +951,7 @@ static bool fold_fusable(const tblup_ctx* c, const std::vector<Split*>& sps, con
 // offsets built on the device, then run_chunk over F x B systems.
 static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd, hipStream_t s,
                            const int64_t* d_idx, const int64_t* d_off, const int64_t* h_off, int64_t B, double h2, int branch, Carve& cv,
-                           double* d_fit) {
+                           double* d_fit, int stop_stage = 0) {
   const int64_t F = (int64_t)sps.size(), FB = F * B, sum_k = h_off[B];
   const EvalDims d = dims_of(c, *sps[0]);
   int64_t* idx_f = cv.take<int64_t>((size_t)(F * sum_k));
@@ -940,8 +978,8 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
     ft.yT[f] = (const double*)sps[f]->yT.p;
     ft.ymu[f] = (const double*)sps[f]->ymu.p;
   }
-  return run_chunk(c, *sps[0], d, sd, s, idx_f, off_f, ho.data(), FB, h2, branch, cv, d_fit, nullptr, 0, nullptr,
-                   nullptr, &ft);
+  return run_chunk(c, *sps[0], d, sd, s, idx_f, off_f, ho.data(), FB, h2, branch, cv, d_fit, nullptr, stop_stage,
+                   nullptr, nullptr, &ft);
 }
 
 // workspace of a fused chunk: its replicated index lists and the diagonal tiles' counts included,
@@ -1018,6 +1056,7 @@ int tblup_eval_folds(tblup_ctx* c, const int* split_ids, int n_splits, const int
   if (!idx || !fitness) return fail(TBLUP_ERR_ARG, "null idx/fitness");
   if (int rc = check_indices(c, idx, offsets[batch])) return rc;
   HIPCHK(hipSetDevice(c->device));
+  HostEntry he(c);
   std::vector<EvalDims> ds(n_splits);
   for (int f = 0; f < n_splits; ++f) ds[f] = dims_of(c, *sps[f]);
   auto fold_bytes = [&](const int64_t* off, int64_t B, int64_t sum_k) {
@@ -1056,26 +1095,49 @@ int tblup_eval_folds(tblup_ctx* c, const int* split_ids, int n_splits, const int
     HIPCHK(hipMemcpyAsync(d_idx, idx + offsets[b0], (size_t)sum_k * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(d_off, hoff.data(), (size_t)(B + 1) * 8, hipMemcpyHostToDevice, c->stream));
     SysDims fsd{};
-    if (fold_fusable(c, sps, hoff.data(), B, branch, fsd)) {
-      Carve cv = head;
-      if (int rc = run_folds_fused(c, sps, fsd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv, d_fit))
-        return rc;
-    } else {
-      for (int f = 0; f < n_splits; ++f) {
-        Carve cv = head;   // every fold reuses the same workspace after the inputs, in stream order
-        const SysDims sd = choose_sys(c, ds[f], hoff.data(), B, branch, c->form_pref);
-        if (int rc = run_chunk(c, *sps[f], ds[f], sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv,
-                               d_fit + (int64_t)f * B, nullptr, 0, nullptr, nullptr))
+    const bool fused = fold_fusable(c, sps, hoff.data(), B, branch, fsd);
+    for (int pass = 0;; ++pass) {
+      // pass 1 after a chained solve gave up a wait: fused, the same factor solved by k_solve; split
+      // by split (the folds reuse one workspace, so the earlier folds' factors are gone), every fold
+      // again with the chained solve off -- bit-identical either way
+      std::vector<int32_t> seqs;
+      if (fused) {
+        Carve cv = head;
+        if (int rc = run_folds_fused(c, sps, fsd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv, d_fit,
+                                     pass ? 3 : 0))
           return rc;
+        seqs.push_back(c->last_chain_seq);
+      } else {
+        const int keep = c->solve_chain;
+        if (pass) c->solve_chain = 0;
+        for (int f = 0; f < n_splits; ++f) {
+          Carve cv = head;   // every fold reuses the same workspace after the inputs, in stream order
+          const SysDims sd = choose_sys(c, ds[f], hoff.data(), B, branch, c->form_pref);
+          const int rc = run_chunk(c, *sps[f], ds[f], sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv,
+                                   d_fit + (int64_t)f * B, nullptr, 0, nullptr, nullptr);
+          seqs.push_back(c->last_chain_seq);
+          if (rc) {
+            c->solve_chain = keep;
+            return rc;
+          }
+        }
+        c->solve_chain = keep;
       }
+      for (int f = 0; f < n_splits; ++f)
+        HIPCHK(hipMemcpyAsync(fitness + (int64_t)f * batch + b0, d_fit + (int64_t)f * B, (size_t)B * 8,
+                              hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      bool any = false;
+      for (int32_t q : seqs) {
+        bool e = false;
+        if (int rc = chain_expired(c, q, &e)) return rc;
+        any = any || e;
+      }
+      if (!any) break;
+      ++c->chain_recoveries;
     }
-    for (int f = 0; f < n_splits; ++f)
-      HIPCHK(hipMemcpyAsync(fitness + (int64_t)f * batch + b0, d_fit + (int64_t)f * B, (size_t)B * 8,
-                            hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
     b0 = b1;
   }
-  if (int rc = check_chain_status(c)) return rc;
   if (c->profiling) return drain_events(c);
   return 0;
 }
@@ -1216,7 +1278,6 @@ static int read_status_word(tblup_ctx* c, void* stream, int* flag, int word) {
   HIPCHK(hipMemcpyAsync(&h, w, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemsetAsync(w, 0, 4, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (word == ST_SOLVE) c->chain_used = false;
   *flag = h != 0;
   return 0;
 }
@@ -1234,7 +1295,13 @@ int tblup_status_async(tblup_ctx* c, void* stream, int32_t* host_status) {
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   HIPCHK(hipMemcpyAsync(host_status, c->status.p, ST_WORDS * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemsetAsync(c->status.p, 0, ST_WORDS * 4, s));
-  c->chain_used = false;
+  return 0;
+}
+
+int tblup_chain_recoveries(tblup_ctx* c, int64_t* count) {
+  if (int rc = check_ctx(c)) return rc;
+  if (!count) return fail(TBLUP_ERR_ARG, "null count");
+  *count = c->chain_recoveries;
   return 0;
 }
 

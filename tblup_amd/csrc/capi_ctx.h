@@ -86,7 +86,8 @@ struct tblup_ctx {
   bool wg_trace = false;
   DevBuf wgt;
   int64_t wgt_used = 0;
-  int dbg_skip = 0;   // TBLUP_DBG_SKIP: phase-ablation timing builds only (results are wrong when set)
+  int dbg_skip = 0;   // TBLUP_DBG_SKIP, read only by diagnostic builds (-DTBLUP_DIAG_BUILD): phase
+                      // ablation, results wrong when set; the production library never reads it
   int form_pref = 0;  // TBLUP_FORM: 0 auto, 1 kernel (dual) form only, 2 SNP (primal) form for snp batches
   // Cholesky schedule (results are bit-identical under every setting; see OffPlan):
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
@@ -104,9 +105,12 @@ struct tblup_ctx {
   // skip them (TBLUP_PAD_FIRST=0: trailing padding, equal up to rounding -- a test knob).
   int pad_first = 1;
   std::vector<int64_t> fold_hoff;   // host offsets of the last fold-fused chunk (host-side shapes only)
-  DevBuf chain;          // its flags [B][chain_flags(NT)] + the expiry flag (zeroed when allocated)
+  DevBuf chain;          // its flags [B][chain_flags(NT)], the expiry ring [CHAIN_ERR_RING] and one
+                         // scratch word (zeroed when allocated)
   int32_t chain_seq = 0; // flag value of the last chained solve
-  bool chain_used = false;   // a chained solve was enqueued since the status was last read
+  int32_t last_chain_seq = 0;   // seq of the chained solve the last run_chunk enqueued, 0 if none
+  bool host_entry = false;      // a synchronous entry is running: its chained solves recover on expiry
+  int64_t chain_recoveries = 0; // chunks whose expired chained solve was re-run through k_solve
   // debug knob (TBLUP_CHAIN_DEBUG="spin,delay,shots"): the next `shots` chained solves poll at
   // most `spin` times and delay one producer by `delay` sleep rounds -- forces an expiry (tests)
   int32_t chain_dbg_spin = 0, chain_dbg_delay = 0, chain_dbg_shots = 0;

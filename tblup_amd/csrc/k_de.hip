@@ -80,7 +80,7 @@ struct DeArgs {
   int64_t ldc;
   uint32_t* key_out;       // [624]
   int32_t* pos_out;
-  int dbg;                 // phase-ablation timing only (env TBLUP_DE_DBG; results wrong when set):
+  int dbg;                 // phase-ablation timing only (env TBLUP_DE_DBG, diagnostic builds; results wrong):
                            // 1 no jump correlation, 2 no mask recurrence, 4 no stream
 };
 
@@ -242,7 +242,11 @@ hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, 
                           const double* parent, int64_t ldp, const int32_t* donors, const int64_t* fixed, int strategy,
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
                           uint32_t* key_out, int32_t* pos_out, hipStream_t s) {
+#ifdef TBLUP_DIAG_BUILD   // phase ablation (results wrong when set): diagnostic builds only
   static const int dbg = getenv("TBLUP_DE_DBG") ? atoi(getenv("TBLUP_DE_DBG")) : 0;
+#else
+  constexpr int dbg = 0;
+#endif
   DeArgs a{key, pos0, polys, end_jump, end_s, end_pos, parent, ldp, donors, fixed, strategy, F, cr, clip, hi, L, pop,
            child, ldc, key_out, pos_out, dbg};
   hipLaunchKernelGGL(k_de_step, dim3(pop + 1), dim3(DE_THREADS), 0, s, a);

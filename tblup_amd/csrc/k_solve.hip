@@ -427,9 +427,10 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 // slots only delay dispatch; they end on their own.  The one assumption is the per-XCD in-order
 // dispatch of one kernel's blocks, an observed hardware behaviour, not a documented guarantee --
 // hence the bound on every wait: CHAIN_SPIN_MAX polls, after which the unit stores the call's seq
-// into ch.err (every later wait of the same call gives up at once), raises the context's sticky
-// status word ch.expired, and the host entries fail the call with TBLUP_ERR_STATE (device
-// entries: tblup_solve_error / tblup_status_async) -- an error, never a silent NaN fitness.  Every
+// into its expiry-ring slot ch.err (every later wait of the same call gives up at once); the host
+// entries read that slot and re-solve the chunk's factor through k_solve (bit-identical), device
+// entries see the context's sticky status word ch.expired (tblup_solve_error /
+// tblup_status_async) -- a recovery or an error, never a silent NaN fitness.  Every
 // sum has a fixed order, the same as k_solve's, so the results do not depend on B, the timing or
 // the grid, and equal k_solve's bit for bit.  With 8 | B an individual's units share one XCD
 // (block id = level * B + b), so its hand-offs stay in one L2.
@@ -590,6 +591,7 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
   for (int K = J + 1; K < NT; ++K)
     if (!chain_wait(flag_part(ch, b, NT, J, K), ch, sh)) {
       if (J == 0 && t == 0) fit[b] = __builtin_nan("");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the X_J LDS-DMA lands before the workgroup ends
       return;
     }
   tr_.waited();
@@ -661,6 +663,7 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
   for (int K = 1; K < NT; ++K)
     if (!chain_wait(flag_e(ch, b, NT, K), ch, sh)) {
       if (t == 0) fit[b] = __builtin_nan("");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       return;
     }
   const double muf = sc[SC_MUF];

@@ -260,9 +260,12 @@ struct SolveChain {
   double* cpart;    // [B][NT (row I)][NT (tile J)][nt][128]: L_JI^T beta_J
   double* epart;    // [B][NT][nt][nV]: block J's share of X_V beta
   double* mbpart;   // [B][NT][nt]: block J's share of sum_a s_a beta_a
-  int32_t* err;     // = seq of a call in which a wait gave up: the call's later waits give up at once
-  int32_t* expired; // the context's sticky solve-status word: set to 1 by a unit whose wait gave up
-                    // (the host entries read it and fail the call with TBLUP_ERR_STATE)
+  int32_t* err;     // this call's slot of the expiry ring (CHAIN_ERR_RING words, slot seq % CHAIN_ERR_RING):
+                    // = seq once a wait of the call gave up -- the call's later waits give up at once,
+                    // and the host entries read it to re-run that chunk's solve through k_solve
+  int32_t* expired; // device entries: the context's sticky solve-status word (set to 1 by a unit whose
+                    // wait gave up; tblup_solve_error / tblup_status_async); host entries: a scratch
+                    // word (they recover from their own ring slot instead)
   int32_t seq;      // this call's flag value
   int32_t mode;     // TBLUP_CHAIN_SYNC (k_solve.hip)
   int32_t spin_max; // polls before a wait gives up (CHAIN_SPIN_MAX; lowered only by the debug knob)
@@ -273,6 +276,8 @@ struct SolveChain {
 // Progress does not need the bound (see k_solve.hip); it turns a broken dispatch assumption into
 // an error the host reports instead of a hang.
 constexpr int32_t CHAIN_SPIN_MAX = 1 << 20;
+// expiry records, one slot per call sequence number modulo the ring size (after the flags)
+constexpr int CHAIN_ERR_RING = 64;
 // the context's device status words (tblup_index_error / tblup_solve_error / tblup_status_async)
 enum { ST_INDEX = 0, ST_SOLVE = 1, ST_WORDS = 2 };
 __host__ __device__ inline int64_t chain_flags(int NT) { return (int64_t)NT * (NT + 2); }

@@ -76,39 +76,52 @@ def shard_range(n_items, rank, world_size):
     return lo, hi
 
 
-def allgather_fitness(local, n_total, device=None):
+def allgather_fitness(local, n_total, device=None, status=None):
     """All-gather the per-rank fitness blocks into the full float64 vector (rank order).
 
     `local` is this rank's shard_range block of n_total individuals: a vector, or an
     (rows, block) matrix -- IntraGCV's per-fold fitnesses -- gathered in ONE collective into
     (rows, n_total).  With nccl the buffers live on `device` (the evaluating engine's GPU; default
-    the current device), so each rank hands RCCL its own GPU's memory."""
+    the current device), so each rank hands RCCL its own GPU's memory.
+
+    `status` (a short sequence of small non-negative ints, e.g. this rank's device status words
+    or an error code) travels in the same collective, appended to the block; the call then returns
+    (full, status_max), the elementwise maximum over the ranks -- so every rank sees a failure on
+    any rank and they all take the same decision (raise, or fall back) together."""
     import torch
     import torch.distributed as dist
 
     rank, ws = world()
     loc = np.asarray(local, dtype=np.float64)
+    st = None if status is None else np.asarray(status, dtype=np.float64).ravel()
     if ws == 1:
-        return loc
+        return loc if st is None else (loc, st.astype(np.int64))
     rows = loc.shape[0] if loc.ndim == 2 else None
     loc2 = loc.reshape(rows or 1, -1)
     R = loc2.shape[0]
     sizes = [shard_range(n_total, r, ws) for r in range(ws)]
     maxc = max(hi - lo for lo, hi in sizes)
+    S = 0 if st is None else len(st)
+    W = maxc + S
     if dist.get_backend() == "nccl":
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
     else:
         dev = torch.device("cpu")
-    buf = torch.full((R, maxc), float("nan"), dtype=torch.float64, device=dev)
+    buf = torch.full((R, W), float("nan"), dtype=torch.float64, device=dev)
     if loc2.shape[1]:
         buf[:, :loc2.shape[1]] = torch.as_tensor(loc2, device=dev)
-    out = torch.empty(ws * R * maxc, dtype=torch.float64, device=dev)
+    if S:
+        buf[0, maxc:] = torch.as_tensor(st, device=dev)
+    out = torch.empty(ws * R * W, dtype=torch.float64, device=dev)
     allgather_device(out, buf.reshape(-1))
-    out = out.cpu().numpy().reshape(ws, R, maxc)
+    out = out.cpu().numpy().reshape(ws, R, W)
     full = np.empty((R, n_total), dtype=np.float64)
     for r, (lo, hi) in enumerate(sizes):
         full[:, lo:hi] = out[r, :, :hi - lo]
-    return full if rows is not None else full[0]
+    full = full if rows is not None else full[0]
+    if st is None:
+        return full
+    return full, out[:, 0, maxc:].max(axis=0).astype(np.int64)
 
 
 def allgather_device(out, local):

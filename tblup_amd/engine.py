@@ -231,6 +231,14 @@ class GpuBlupEngine:
         _native.check("tblup_status_async", self._lib.tblup_status_async(
             self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.c_void_p(host_status.data_ptr())))
 
+    def chain_recoveries(self):
+        """Chunks the synchronous entries re-solved through k_solve after a chained-solve wait
+        expired (tblup_chain_recoveries); the speculative path's fallbacks are counted by the
+        evaluator (BlupParallelEvaluator.spec_fallbacks)."""
+        v = ctypes.c_int64(0)
+        _native.check("tblup_chain_recoveries", self._lib.tblup_chain_recoveries(self._ctx, ctypes.byref(v)))
+        return v.value
+
     @staticmethod
     def raise_status(status, fn="tblup_eval_batch_device", n_snps=None):
         """Raise for nonzero status words read through status_async."""

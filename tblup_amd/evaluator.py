@@ -23,6 +23,7 @@ from math import sqrt
 
 import numpy as np
 
+from . import _native
 from .distributed import allgather_fitness, destroy, init_from_env, shard_range, world
 
 
@@ -156,6 +157,7 @@ class BlupParallelEvaluator(ParallelEvaluator):
         self.snp_remover = snp_remover
         self.h2 = h2
         self._spec = None   # speculative evaluation of the last GPU DE generation (see _speculate)
+        self.spec_fallbacks = 0   # speculative evaluations dropped after a chained-solve expiry
         data = np.load(data_path, mmap_mode="r")
         self.n_samples, self.n_columns = data.shape[0], data.shape[1]
         if splitter:
@@ -175,8 +177,9 @@ class BlupParallelEvaluator(ParallelEvaluator):
         if ws == 1:
             return self.engine.evaluate(genomes, train_indices, validation_indices, self.h2)
         lo, hi = shard_range(total, rank, ws)
-        local = self.engine.evaluate(genomes[lo:hi], train_indices, validation_indices, self.h2)
-        return allgather_fitness(local, total, getattr(self.engine, "device", None))
+        return _gather_or_raise(lambda: self.engine.evaluate(genomes[lo:hi], train_indices, validation_indices,
+                                                             self.h2),
+                                (hi - lo,), total, getattr(self.engine, "device", None))
 
     @staticmethod
     def blup(indices, train_indices, validation_indices, data, labels, h2):
@@ -297,14 +300,25 @@ class BlupParallelEvaluator(ParallelEvaluator):
         hits = DeviceKeyStore.get(self.engine.device).rows(inds)
         if any(h is None or h[0] is not spec["keys"] or h[1] != i for i, h in enumerate(hits)):
             return None
+        status = np.zeros(2, dtype=np.int64)
         if spec["event"] is not None:
             spec["event"].synchronize()
-            self.engine.raise_status(spec["status"].numpy(), n_snps=self.engine.n_snps)
+            status = spec["status"].numpy().astype(np.int64)
             local = spec["host"].numpy().copy()
         else:
             local = np.zeros(0, dtype=np.float64)
-        if world()[1] > 1:   # every rank takes the same decision here (replicated state): one all-gather
-            return allgather_fitness(local, len(inds), getattr(self.engine, "device", None))
+        if world()[1] > 1:
+            # every rank takes the same decision here (replicated state): one all-gather, which carries
+            # every rank's status words, so a failure on any rank is seen by all of them
+            local, status = allgather_fitness(local, len(inds), getattr(self.engine, "device", None), status=status)
+        if status[0]:   # an index outside [-P, P): numpy's IndexError, on every rank
+            self.engine.raise_status((status[0], 0), n_snps=self.engine.n_snps)
+        if status[1]:
+            # a chained-solve wait expired in the speculative (device-entry) evaluation: drop it;
+            # evaluate() then evaluates these children through the synchronous entry, which
+            # re-solves an expired chunk by itself (tblup_chain_recoveries) -- same bits
+            self.spec_fallbacks += 1
+            return None
         return local
 
     def evaluate(self, previous_population, next_population, generation):
@@ -393,9 +407,9 @@ class IntraGCVBlupParallelEvaluator(InterGCVBlupParallelEvaluator):
         if ws == 1:
             return folds(genomes, splits, self.h2)
         lo, hi = shard_range(len(genomes), rank, ws)
-        local = np.asarray(folds(genomes[lo:hi], splits, self.h2)).reshape(self.n_folds, hi - lo)
         # every fold's block in one all-gather
-        return allgather_fitness(local, len(genomes), getattr(self.engine, "device", None))
+        return _gather_or_raise(lambda: np.asarray(folds(genomes[lo:hi], splits, self.h2)).reshape(self.n_folds, hi - lo),
+                                (self.n_folds, hi - lo), len(genomes), getattr(self.engine, "device", None))
 
     def _evaluate(self, population, to_evaluate, indices, generation):
         sums = {i: 0 for i in indices}
@@ -420,6 +434,29 @@ class MonteCarloCVBlupParallelEvaluator(BlupParallelEvaluator):
     def train_validation_indices(self, generation):
         from sklearn.model_selection import train_test_split
         return train_test_split(self.indices, test_size=0.2)
+
+
+def _gather_or_raise(evaluate, shape, n_total, device):
+    """This rank's shard evaluated, then the all-gather (torch.distributed).  A failure of the
+    shard's evaluation (an index outside [-P, P) in one rank's genomes) would otherwise raise on
+    that rank only and leave its peers waiting in the collective: the error code travels in the
+    same all-gather, and every rank raises together."""
+    err = None
+    try:
+        local = evaluate()
+    except _native.TblupError as e:
+        err = e
+        local = np.full(shape, np.nan)
+    code = 0 if err is None else (1 if isinstance(err, IndexError) else 2)
+    full, st = allgather_fitness(local, n_total, device, status=(code,))
+    if st[0]:
+        if err is not None:
+            raise err
+        cls = _native.TblupIndexError if st[0] == 1 else _native.TblupError
+        raise cls("tblup_eval_batch", _native.ERR_INDEX if st[0] == 1 else _native.ERR_STATE,
+                  "the evaluation failed on another rank" + (" (an index is out of bounds for axis 1)"
+                                                            if st[0] == 1 else ""))
+    return full
 
 
 # ---------------------------------------------------------------------------

@@ -85,3 +85,39 @@ def run_main_flow(rank, world, port, case, out_dir):
     D.compare(run, z, case)
     json.dump({"seen": seen, "group_inside": inside, "group_after": after},
               open(os.path.join(out_dir, f"main_rank{rank}.json"), "w"))
+
+
+def run_rank_error(rank, world, port, out_dir):
+    """One rank's shard fails (an out-of-bounds index, numpy's IndexError) while the other's
+    succeeds: both ranks must raise the same error type instead of rank 0 waiting in the fitness
+    all-gather; the status words travel in that all-gather."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import numpy as np
+    import torch.distributed as dist
+
+    from tblup_amd import _native
+    from tblup_amd.distributed import allgather_fitness
+    from tblup_amd.evaluator import _gather_or_raise
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    full, st = allgather_fitness(np.full(4 - rank, float(rank)), 7, status=(rank, 5 * (1 - rank)))
+    out["status_max"] = [int(x) for x in st]
+    out["full"] = [float(x) for x in full]
+
+    def shard():
+        if rank == 1:
+            raise _native.TblupIndexError("tblup_eval_batch", _native.ERR_INDEX, "index 9 is out of bounds")
+        return np.ones(4)
+    try:
+        _gather_or_raise(shard, (4,), 8, None)
+        out["raised"] = None
+    except _native.TblupIndexError as e:
+        out["raised"] = type(e).__name__
+    full = _gather_or_raise(lambda: np.full(4, rank + 0.5), (4,), 8, None)   # and a clean call after it
+    out["clean"] = [float(x) for x in full]
+    json.dump(out, open(os.path.join(out_dir, f"err_rank{rank}.json"), "w"))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -77,3 +77,24 @@ def test_two_rank_main_flow_without_preinitialised_group(golden_dir, tmp_path, c
         assert res[r]["group_inside"][0] is True and res[r]["group_after"] is False
         pop_batches = [n for n in res[r]["seen"][:2]]
         assert pop_batches == [16, 16]          # generation 0 and 1: 32 individuals over 2 ranks
+
+
+def test_rank_failure_raises_on_every_rank(tmp_path):
+    """An evaluation that fails on one rank only (an out-of-bounds index in its shard)
+    raises the same error on every rank instead of leaving the others in the all-gather; the
+    status words of every rank travel in the fitness all-gather (element-wise max)."""
+    from tests import dist_worker
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=dist_worker.run_rank_error, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = [json.load(open(tmp_path / f"err_rank{r}.json")) for r in range(2)]
+    for r in range(2):
+        assert res[r]["status_max"] == [1, 5]
+        assert res[r]["full"] == [0.0] * 4 + [1.0] * 3
+        assert res[r]["raised"] == "TblupIndexError"
+        assert res[r]["clean"] == [0.5] * 4 + [1.5] * 4

@@ -8,9 +8,11 @@ chained solve's failure mode.
   every automatic small-batch policy at once (ahead P-units with makespan slicing, D-units beside
   the diagonal, last-term mode at B <= 64, the chained solve) -- oracle samples and bit identity
   with every policy off (TBLUP_AHEAD=0 TBLUP_SOLVE_CHAIN=0 TBLUP_DIAG_D=0 TBLUP_LAST_TERM=0).
-* A chained-solve hand-off wait that expires fails the call (TBLUP_ERR_STATE / TblupError) or
-  raises the device status word -- never a silent NaN -- and the next call on the same context is
-  clean (TBLUP_CHAIN_DEBUG forces one expiry: a lowered poll bound and a late producer unit).
+* A chained-solve hand-off wait that expires is recovered by the host entries (the chunk's factor
+  re-solved through k_solve, same bits) or raises the device status word, which the drop-in
+  evaluator's speculative path answers by re-evaluating through the host entry -- never a silent
+  NaN -- and the next call on the same context is clean (TBLUP_CHAIN_DEBUG forces expiries: a
+  lowered poll bound and a late producer unit).
   Reference behaviour being replaced: a dead worker hangs its parent (tblup/evaluator.py:397-398).
 """
 import os
@@ -115,12 +117,12 @@ def test_chain_sync_modes_bit_identical(panel):
     np.testing.assert_array_equal(a[1], b[1])
 
 
-def test_chained_solve_expiry_is_an_error(panel):
+def test_chained_solve_expiry_recovers(panel):
     """TBLUP_CHAIN_DEBUG=spin,delay,shots: the next `shots` chained solves poll at most `spin`
-    times while one producer sleeps `delay` rounds, so a wait expires.  Host entry: TblupError
-    (TBLUP_ERR_STATE); device entry: the solve-error flag; then the same context is clean."""
+    times while one producer sleeps `delay` rounds, so a wait expires.  Host entry: the call
+    re-solves the chunk's factor through k_solve and returns the reference bits (counted by
+    tblup_chain_recoveries); device entry: the solve-error flag; then the same context is clean."""
     import torch
-    from tblup_amd import _native
     from tblup_amd.engine import GpuBlupEngine, concat_genomes
     p = panel
     genomes = p["genomes"][:8]                  # SNP form, B = 8 <= 160: the chained solve
@@ -128,10 +130,11 @@ def test_chained_solve_expiry_is_an_error(panel):
     with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,2"}):
         eng = GpuBlupEngine(p["geno"], p["pheno"], device=0)
     try:
-        with pytest.raises(_native.TblupError, match="chained solve") as ei:
-            eng.evaluate(genomes, p["T"], p["V"], 0.4)
-        assert ei.value.code == _native.ERR_STATE
-        # device entry: no synchronous failure, the status word is raised instead
+        fit, ebv = eng.evaluate(genomes, p["T"], p["V"], 0.4, return_ebv=True)   # shot 1: recovered
+        np.testing.assert_array_equal(fit, ref[0])
+        np.testing.assert_array_equal(ebv, ref[1])
+        assert eng.chain_recoveries() == 1
+        # device entry (shot 2): no synchronous failure, the status word is raised instead
         sid = eng.split_id(p["T"], p["V"])
         idx, off = concat_genomes(genomes)
         d_idx, d_off = torch.from_numpy(idx).cuda(), torch.from_numpy(off).cuda()
@@ -145,12 +148,76 @@ def test_chained_solve_expiry_is_an_error(panel):
         fit, ebv = eng.evaluate(genomes, p["T"], p["V"], 0.4, return_ebv=True)
         np.testing.assert_array_equal(fit, ref[0])
         np.testing.assert_array_equal(ebv, ref[1])
+        assert eng.chain_recoveries() == 1
         eng.evaluate_device(sid, d_idx.data_ptr(), d_off.data_ptr(), off, 0.4, d_fit.data_ptr(),
                             stream_ptr=s.cuda_stream)
         eng.check_device_status(s.cuda_stream)
         np.testing.assert_array_equal(d_fit.cpu().numpy(), ref[0])
+        # IntraGCV folds (host entry, fused): an expiry there recovers the same way
+        folds = [(p["T"][:1024], p["V"]), (p["T"][256:], p["V"])]
+        ref_f = eng.evaluate_folds(genomes, folds, 0.4)
     finally:
         eng.close()
+    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,1"}):
+        with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
+            np.testing.assert_array_equal(eng.evaluate_folds(genomes, folds, 0.4), ref_f)
+            assert eng.chain_recoveries() == 1
+    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,2", "TBLUP_FOLD_FUSE": "0"}):
+        with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:   # split by split: both folds again
+            np.testing.assert_array_equal(eng.evaluate_folds(genomes, folds, 0.4), ref_f)
+            assert eng.chain_recoveries() == 1
+
+
+def _generations(p, tmp_path, pop, gens, env):
+    """Generation 0 (evaluate) and `gens` GPU DE generations (evolve -> speculative evaluate)
+    through the drop-in classes on the config-2 panel; returns (fitness per generation,
+    chain recoveries, speculative fallbacks)."""
+    import random
+    from tests.ga_driver import RandomKeyIndividual
+    from tests.helpers import Pop
+    from tblup_amd.evaluator import BlupParallelEvaluator
+    from tblup_amd.evolver import DERandOneEvolver
+    gp, pp = str(tmp_path / "g.npy"), str(tmp_path / "y.npy")
+    if not os.path.exists(gp):
+        np.save(gp, p["geno"])
+        np.save(pp, p["pheno"])
+    random.seed(5)
+    np.random.seed(5)
+    rng = np.random.default_rng(6)
+    P = p["geno"].shape[1]
+    ev = BlupParallelEvaluator(gp, pp, 0.4)
+    ev.training_indices, ev.validation_indices = list(p["T"]), list(p["V"])
+    inds = [RandomKeyIndividual(1000, P, genome=rng.uniform(size=P)) for _ in range(pop)]
+    evo = DERandOneEvolver(P, 0.8, 0.5, False)
+    out = []
+    with _env(env):
+        with ev:
+            popn = Pop(inds, 0)
+            popn.evaluator = ev
+            ev.evaluate(popn, popn, 0)
+            out.append([i.fitness for i in popn.population])
+            for g in range(1, gens + 1):
+                popn.generation = g
+                kids = evo.evolve(popn)
+                ev.evaluate(popn, kids, g)
+                out.append([c.fitness for c in kids])
+                popn.population = [c if c.fitness > q.fitness else q for q, c in zip(popn.population, kids)]
+            rec = ev.engine.chain_recoveries()
+    return np.array(out), rec, ev.spec_fallbacks
+
+
+def test_evaluator_recovers_from_chain_expiry(panel, tmp_path):
+    """The drop-in evaluator under forced chained-solve expiries: generation 0
+    goes through the host entry (the chunk re-solved, chain_recoveries = 1), generation 1's
+    speculative device-entry evaluation expires too and is dropped (spec_fallbacks = 1): evaluate()
+    then evaluates the children through the host entry.  Every fitness equals an undisturbed run's
+    bit for bit, where the reference would have hung (tblup/evaluator.py:397-398)."""
+    p = panel
+    ref, rec0, fb0 = _generations(p, tmp_path, 16, 2, {})
+    assert (rec0, fb0) == (0, 0)
+    got, rec, fb = _generations(p, tmp_path, 16, 2, {"TBLUP_CHAIN_DEBUG": "1000,20000,2"})
+    np.testing.assert_array_equal(got, ref)
+    assert (rec, fb) == (1, 1)
 
 
 def test_kernel_form_folds_fused(panel):
