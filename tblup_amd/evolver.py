@@ -30,7 +30,7 @@ import numpy as np
 
 from . import _native
 from .distributed import shard_range, world
-from .keystore import DeviceKeyStore, track, work_stream
+from .keystore import DeviceKeyStore, freeze_heap, track, work_stream
 from .shmrows import RING as _SHM
 
 
@@ -94,6 +94,7 @@ class GpuDEStep:
 
     def __init__(self, device=0):
         self._lib = _native.load()
+        freeze_heap()
         ctx = ctypes.c_void_p()
         _native.check("tblup_ctx_create", self._lib.tblup_ctx_create(None, 0, 0, 0, None, int(device),
                                                                      ctypes.byref(ctx)))
@@ -253,13 +254,17 @@ class _RowBlocks:
     over older blocks: when more than `keep` older blocks are still referenced by the
     population, the least-referenced ones are compacted -- those individuals' genomes are
     replaced by equal own copies (set_internal_genome, individual.py:100-101) -- so at most
-    keep + 1 generations (about 2 GiB) stay page-locked.  Freed blocks go back to torch's caching host
+    keep + 2 generations (about 2 GiB) stay page-locked.  The copies run on worker threads
+    while the next generation's GPU work and transfers are in flight, and the genomes are
+    swapped to them at the next compaction (an own array each: they are never DMA'd again,
+    their device rows stay in the key store).  Freed blocks go back to torch's caching host
     allocator and are reused without new page-locking."""
 
     def __init__(self, keep=12):
         self.keep = keep
         self._reg = {}   # id(block) -> weakref(block)
         self._reserved = set()
+        self._pending = []   # (individual, its genome when the copy started, future of the copy)
 
     def keep_for(self, nbytes):
         """Older blocks kept page-locked for blocks of nbytes (about 2 GiB in all)."""
@@ -298,11 +303,28 @@ class _RowBlocks:
             b = b.base
         return None
 
+    def finish(self, store=None):
+        """Swap the members whose copies the last compaction started to those copies: skipped
+        for a genome replaced or written (TrackedGenome marks it stale) since the copy began --
+        it stays where it is and a later compaction takes it."""
+        pending, self._pending = self._pending, []
+        for indv, old, fut in pending:
+            new = fut.result()
+            if getattr(indv, "_genome", None) is not old or old._stale:
+                continue
+            t = track(new)
+            indv.set_internal_genome(t)
+            if store is not None:
+                store.rebind(indv, old, t)
+
     def compact(self, individuals, store=None):
         """Blocks that only a few members of the population still use (<= n / 64 rows), and
-        the least-used ones beyond `keep`, give those members own copies (page-locked
-        buffers from torch's caching allocator: no page faults); the key store keeps their
-        device rows."""
+        the least-used ones beyond `keep`: those members' genomes are copied into own arrays on
+        worker threads (np.copyto releases the GIL; the copies overlap the next generation's
+        transfers) and swapped by the next call (finish); the key store keeps their device rows.
+        (Round 4 copied them here, on the caller's thread, into page-locked buffers: 2-12 ms per
+        generation at pop 1024.)"""
+        self.finish(store)
         self._reg = {k: r for k, r in self._reg.items() if r() is not None}
         if not self._reg:
             return
@@ -316,27 +338,42 @@ class _RowBlocks:
         few = max(1, len(individuals) // 64)
         # at most `keep` older blocks, fewer when they are large (about 2 GiB page-locked)
         big = max(r().nbytes for r in self._reg.values())
-        keep = self.keep_for(big)
+        keep = self.keep_for(big) - 1   # the blocks dropped here are released at the next call (finish)
         drop = [k for i, k in enumerate(order) if len(users[k]) <= few or i < len(order) - keep]
         if not drop:
             return
-        import torch
         moved = [indv for k in drop for indv in users[k]
                  if indv.get_internal_genome() is indv._genome]   # RandomKey / Index semantics only
-        bufs = [torch.empty(indv._genome.shape[0], dtype=torch.float64, pin_memory=True).numpy() for indv in moved]
+        pool = _pool()
+        # runs of rows per job: few pool round trips, each copy large enough to release the GIL
+        per = max(1, (len(moved) + 7) // 8)
+        for j0 in range(0, len(moved), per):
+            grp = moved[j0:j0 + per]
+            fut = pool.submit(_copy_genomes, [indv._genome for indv in grp])
+            for j, indv in enumerate(grp):
+                self._pending.append((indv, indv._genome, _Part(fut, j)))
 
-        def copy(j):
-            np.copyto(bufs[j], moved[j]._genome)
-        if len(moved) > 4:
-            list(_pool().map(copy, range(len(moved))))
-        else:
-            for j in range(len(moved)):
-                copy(j)
-        for indv, buf in zip(moved, bufs):
-            old, new = indv._genome, track(buf)
-            indv.set_internal_genome(new)
-            if store is not None:
-                store.rebind(indv, old, new)
+
+def _copy_genomes(genomes):
+    return [np.array(g.view(np.ndarray)) for g in genomes]
+
+
+class _Part:
+    """Item j of a future's list result."""
+
+    def __init__(self, fut, j):
+        self.fut, self.j = fut, j
+
+    def result(self):
+        return self.fut.result()[self.j]
+
+
+def _assigns_genome(indv):
+    """Whether set_internal_genome only stores the array (IndexIndividual's, individual.py:100-101,
+    inherited by RandomKey / Nullable): then a child may be bound to its row before the row's
+    transfer has landed.  CoevolutionIndividual's reads the last element (individual.py:194-208)."""
+    f = getattr(type(indv), "set_internal_genome", None)
+    return getattr(f, "__qualname__", "") == "IndexIndividual.set_internal_genome"
 
 
 _BLOCKS = _RowBlocks()
@@ -454,6 +491,22 @@ class _GpuDEEvolver(Evolver):
         # the candidates (new uids, the parent's other attributes) while the transfer runs
         next_pop = [_copy_individual(population[i]) for i in range(n)]
         t = _mark(t, "ev_candidates")
+        if (shared is not None or block_rows) and all(_assigns_genome(c) for c in next_pop):
+            # whole-block rows: every child is bound to its row (a view: nothing reads the values),
+            # recorded, and the older blocks compacted while the rows are still in flight; the
+            # children are returned once their rows have landed (every rank's, for a shared block)
+            arrays = _BLOCKS.rows(shared if shared is not None else host.numpy())
+            t = _mark(t, "ev_arrays")
+            self._bind(next_pop, arrays, inds, genomes, children, parents, store, speculated, evaluator)
+            t = _mark(t, "ev_bind_record")
+            _BLOCKS.compact(inds, store)
+            t = _mark(t, "ev_compact")
+            events[-1].synchronize()
+            if shared is not None:
+                import torch.distributed as dist
+                dist.barrier()   # every rank's shard of the rows has landed
+            _mark(t, "ev_rows_landed")
+            return next_pop
         if shared is not None:
             events[-1].synchronize()
             import torch.distributed as dist
@@ -470,7 +523,16 @@ class _GpuDEEvolver(Evolver):
                 dest = [torch.empty(L, dtype=torch.float64, pin_memory=True).numpy() for _ in range(n)]
             arrays = _copy_rows(host.numpy(), dtypes, ready=[ev.synchronize for ev in events], dest=dest)
         t = _mark(t, "ev_arrays")
-        for i in range(n):
+        self._bind(next_pop, arrays, inds, genomes, children, parents, store, speculated, evaluator, dtypes)
+        t = _mark(t, "ev_bind_record")
+        # older blocks the parents leave sparsely used, while the GPU still evaluates the children
+        _BLOCKS.compact(inds, store)
+        _mark(t, "ev_compact")
+        return next_pop
+
+    @staticmethod
+    def _bind(next_pop, arrays, inds, genomes, children, parents, store, speculated, evaluator, dtypes=None):
+        for i in range(len(next_pop)):
             next_pop[i].set_internal_genome(arrays[i])
         if speculated:
             evaluator._spec_bind(next_pop)
@@ -478,11 +540,6 @@ class _GpuDEEvolver(Evolver):
             store.record(children, next_pop, arrays)
             store.record(parents, inds, genomes, adopt=True)
         store.prune([x.uid for x in inds] + [x.uid for x in next_pop])
-        t = _mark(t, "ev_bind_record")
-        # older blocks the parents leave sparsely used, while the GPU still evaluates the children
-        _BLOCKS.compact(inds, store)
-        _mark(t, "ev_compact")
-        return next_pop
 
 
 class DERandOneEvolver(_GpuDEEvolver):

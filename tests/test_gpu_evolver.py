@@ -1,6 +1,7 @@
 """GPU DE step (k_de.hip through tblup_de_step): children and RNG states bit-exact to the
 reference's evolvers (goldens) and to the numpy oracle at config-2 size."""
 import hashlib
+from copy import deepcopy
 import random
 
 import numpy as np
@@ -242,11 +243,16 @@ def test_gpu_de_small_shapes_vs_oracle(gpu, L, pop, pre):
 
 
 
-def test_gpu_block_rows_many_generations(gpu, tmp_path):
+@pytest.mark.parametrize("kind", ["helpers", "reference"])
+def test_gpu_block_rows_many_generations(gpu, tmp_path, kind):
     """14 generations of evolve -> evaluate -> select with the children's genomes as rows of
     page-locked per-generation blocks: equal to the host-oracle loop generation by generation,
-    the blocks still in use stay bounded (compaction), compacted genomes keep their device
-    rows, and rows are independent arrays (an in-place write touches one child only)."""
+    the blocks still in use stay bounded (compaction, its copies on worker threads), compacted
+    genomes keep their device rows, and rows are independent arrays (an in-place write touches
+    one child only).  kind "reference": individuals with the reference's set_internal_genome
+    (tests/ga_driver.py, individual.py:100-101), whose children are bound to their rows while
+    the rows are still in flight."""
+    from tests import ga_driver as GD
     from oracle import blup_oracle as O
     from tblup_amd import evolver as EVM
     from tblup_amd.evaluator import BlupParallelEvaluator
@@ -263,7 +269,10 @@ def test_gpu_block_rows_many_generations(gpu, tmp_path):
         random.seed(9)
         np.random.seed(9)
         ev = BlupParallelEvaluator(str(tmp_path / "g.npy"), str(tmp_path / "y.npy"), 0.4)
-        inds = [RandomKeyIndividual(keys0[i].copy(), k) for i in range(pop)]
+        if kind == "reference":
+            inds = [GD.RandomKeyIndividual(k, p, genome=keys0[i].copy()) for i in range(pop)]
+        else:
+            inds = [RandomKeyIndividual(keys0[i].copy(), k) for i in range(pop)]
         fits, alive = [], []
         with ev:
             popn = Pop(inds, 0)
@@ -279,7 +288,12 @@ def test_gpu_block_rows_many_generations(gpu, tmp_path):
                     DeviceKeyStore.get(0).clear()
                     want = D.de_generation([x.get_internal_genome() for x in popn.population],
                                            [x.fitness for x in popn.population], g, "de_rand_1", p, 0.8, 0.5, False)
-                    kids = [RandomKeyIndividual(w, k) for w in want]
+                    if kind == "reference":   # as the reference's evolver makes them (no RNG draw)
+                        kids = [deepcopy(q) for q in popn.population]
+                        for c, w in zip(kids, want):
+                            c.set_internal_genome(w)
+                    else:
+                        kids = [RandomKeyIndividual(w, k) for w in want]
                 ev.evaluate(popn, kids, g)
                 popn.population = [c if c.fitness > q.fitness else q for q, c in zip(popn.population, kids)]
                 fits.append([x.fitness for x in kids])

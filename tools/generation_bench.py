@@ -46,6 +46,18 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
     evo = DERandOneEvolver(p, 0.8, 0.5, False)
     out = {"n": n, "p": p, "k": k, "pop": pop, "world": world}
     phase = {}
+    # time spent in python's cyclic garbage collector, per generation (gc.callbacks)
+    import gc
+    gc_t = {"start": 0.0, "ms": 0.0, "n2": 0}
+
+    def gc_cb(ph, info):
+        if ph == "start":
+            gc_t["start"] = time.perf_counter()
+        else:
+            gc_t["ms"] += 1e3 * (time.perf_counter() - gc_t["start"])
+            gc_t["n2"] += info.get("generation", 0) == 2
+    gc.callbacks.append(gc_cb)
+    seg_all, gc_all = [], []
 
     def timed(obj, name):
         fn = getattr(obj, name)
@@ -87,6 +99,9 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
             t2 = time.perf_counter()
             popn.population = [c if c.fitness > q.fitness else q for q, c in zip(popn.population, kids)]
             ts.append((t1 - t0, t2 - t1, time.perf_counter() - t0))
+            seg_all.append({k: round(1e3 * v, 2) for k, v in EVM.PROFILE.items()})
+            gc_all.append((round(gc_t["ms"], 2), gc_t["n2"]))
+            gc_t["ms"], gc_t["n2"] = 0.0, 0
             if g == gens:
                 out["phases_last_gen_ms"] = {k: round(1e3 * v, 2) for k, v in phase.items()}
                 out["evolve_segments_last_gen_ms"] = {k: round(1e3 * v, 2) for k, v in EVM.PROFILE.items()}
@@ -98,7 +113,9 @@ def main(n=2000, p=50000, k=1000, pop=256, gens=4):
                     "gpu_generation_ms_median": float(np.median(allg)),
                     "gpu_generation_ms_mean_all": float(np.mean(allg)),
                     "gpu_generation_ms_mean_after_first": float(np.mean(allg[1:])) if len(allg) > 1 else None,
-                    "gpu_generation_ms_all": [round(x, 2) for x in allg]})
+                    "gpu_generation_ms_all": [round(x, 2) for x in allg],
+                    "gc_ms_and_full_collections_all": gc_all,
+                    "evolve_segments_all_ms": seg_all})
         if world > 1:
             from tblup_amd.shmrows import RING
             out["shared_rows"] = any(r is not None for r in RING._rings.values())
