@@ -16,7 +16,7 @@ uniforms, mutant, crossover and clip are computed in parallel.  The children's
 genomes and the numpy / python RNG states afterwards are bit-identical to the
 reference's sequential loop (tests/test_evolver.py, tests/test_gpu_evolver.py).
 
-SaDE and MDE_pBX (evolver.py:423-720) draw per-individual F/CR from normal and
+SaDE and MDE_pBX (evolver.py:407-547, 550-687) draw per-individual F/CR from normal and
 Cauchy distributions and are not accelerated: `get_evolver` raises for them.
 There is no CPU fallback: without the HIP library, `evolve` raises ImportError.
 """
