@@ -50,25 +50,7 @@ constexpr int NSLOT = TBLUP_NSLOT;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-// LDS-DMA of 16 B per lane (lane i -> lds + 16 i) as inline asm, for the stage rings.  The compiler
-// sees __builtin_amdgcn_global_load_lds as an LDS write in flight and waits vmcnt(0) before the
-// next LDS read of ANY address (ROCm 7.2, checked in the emitted code): in a ring that issues
-// stage s + 1 and then reads stage s, that wait drained the prefetch, so every stage's load
-// latency was exposed.  Hidden from the compiler, the DMA is ordered by the ring's own counted
-// s_waitcnt + barrier, which every reader of a stage sits behind.  m0 is saved and restored around
-// the DMA (its LDS address is sampled at issue), so the asm leaves m0 as the compiler last set it:
-// the builtin LDS-DMAs beside these rings (k_chol_diag, the off-diagonal kernel) keep whatever m0
-// setup the compiler hoisted or merged for them, by construction.  (m0 is a reserved register, so
-// it cannot be declared clobbered: clang warns that the clobber is not honoured.)
-__device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
-  const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(g), "s"(la)
-      : "memory");
-}
+// (glds16_asm, the stage rings' LDS-DMA as inline asm: tblup_internal.h)
 #ifndef TBLUP_AB_ASM_SYRK   // A/B builds only (tools/ab_build_defs.sh): the SYRK ring's DMA as inline asm
 #define TBLUP_AB_ASM_SYRK 1
 #endif

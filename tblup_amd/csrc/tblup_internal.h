@@ -101,6 +101,27 @@ struct EvalDims {
   int nt;           // traits
 };
 
+// LDS-DMA of 16 B per lane (lane i -> lds + 16 i) as inline asm, for the stage rings.  The compiler
+// sees __builtin_amdgcn_global_load_lds as an LDS write in flight and waits vmcnt(0) before the
+// next LDS read of ANY address (ROCm 7.2, checked in the emitted code): in a ring that issues
+// stage s + 1 and then reads stage s, that wait drained the prefetch, so every stage's load
+// latency was exposed.  Hidden from the compiler, the DMA is ordered by the ring's own counted
+// s_waitcnt + barrier, which every reader of a stage sits behind (the compiler's own counted waits
+// on its loads stay correct: an extra outstanding DMA only makes them wait for more).  m0 is saved
+// and restored around the DMA (its LDS address is sampled at issue), so the asm leaves m0 as the
+// compiler last set it: builtin LDS-DMAs beside these rings keep whatever m0 setup the compiler
+// hoisted or merged for them, by construction.  (m0 is a reserved register, so it cannot be
+// declared clobbered: clang warns that the clobber is not honoured.)
+__device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(la)
+      : "memory");
+}
+
 // ---- packed lower-triangular 16x16 block storage of a 128x128 tile (LDS and Dinv) ----
 constexpr int NB = 16;                       // base block edge
 constexpr int NBLK = TILE / NB;              // 8 block rows
