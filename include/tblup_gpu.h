@@ -261,6 +261,16 @@ int tblup_de_step_device_async(tblup_ctx* ctx, int strategy, const double* d_par
                                int64_t ldc, void* stream);
 int tblup_de_state_wait(tblup_ctx* ctx, uint32_t* mt_key, int32_t* mt_pos);
 
+/* tblup_de_step_device_async with a strategy, mutation factor and crossover rate per individual
+ * (host arrays of pop): the adaptive evolvers' generation -- SaDE (tblup/evolver.py:407-547) draws
+ * each individual's strategy (DE/rand/1 or DE/current-to-best/1, python's random.random() < p)
+ * and its crossover rate, with one F per generation.  Same numpy stream layout (one
+ * np.random.rand(L) per individual, in order); completed by tblup_de_state_wait. */
+int tblup_de_step_device_async_mix(tblup_ctx* ctx, const int32_t* strategies, const double* F, const double* cr,
+                                   const double* d_parents, int64_t pop, int64_t L, int64_t ld, const int32_t* donors,
+                                   const int64_t* fixed, int clip, double clip_hi, const uint32_t* mt_key,
+                                   int32_t mt_pos, double* d_children, int64_t ldc, void* stream);
+
 /* Enqueue dst row i (L doubles, row stride ldd) = the device row d_src_rows[i] (a host array of
  * n device pointers, each to L doubles on this context's device) on `stream` (NULL = the
  * context's stream): one launch per 128 rows.  The DE step's parents gathered from the rows

@@ -69,3 +69,19 @@ def de_generation(genomes, fitness, generation, strategy, dimensionality, cr, F,
             out.append(np.clip(child, 0, dimensionality - 1))
         return out
     raise NotImplementedError(strategy)
+
+
+def de_children(genomes, strategies, donors, fixed, F, crs, clip, hi):
+    """Children of one SaDE generation (evolver.py:523-545) from the host's draws: per individual
+    DE/rand/1 (strategy 0, donors a, b, c: evolver.py:118-132) or DE/current-to-best/1 (strategy 1,
+    donors best, a, b: evolver.py:199-214) with its own crossover rate and the caller's forced
+    position, one np.random.rand(L) per individual in order (evolver.py:74-82), optional clip."""
+    out = []
+    for i, x in enumerate(genomes):
+        a, b, c = (genomes[j] for j in donors[i])
+        mutant = a + F * (b - c) if strategies[i] == 0 else x + F * (a - x) + F * (b - c)
+        take = np.random.rand(len(x)) < crs[i]
+        take[fixed[i]] = True
+        child = np.where(take, mutant, x)
+        out.append(np.clip(child, 0, hi) if clip else child)
+    return out

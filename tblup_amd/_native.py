@@ -67,6 +67,9 @@ SIGNATURES = {
                                               _c.c_double, _c.c_double, _c.c_int, _c.c_double, _U32P, _c.c_int32,
                                               _P, _c.c_int64, _P]),
     "tblup_de_state_wait": (_c.c_int, [_P, _U32P, _I32P]),
+    "tblup_de_step_device_async_mix": (_c.c_int, [_P, _I32P, _DP, _DP, _P, _c.c_int64, _c.c_int64, _c.c_int64, _I32P,
+                                                  _I64P, _c.c_int, _c.c_double, _U32P, _c.c_int32, _P, _c.c_int64,
+                                                  _P]),
     "tblup_grm": (_c.c_int, [_P, _I64P, _c.c_int64, _DP]),
     "tblup_snp_scan": (_c.c_int, [_P, _I64P, _c.c_int64, _DP, _I64P, _I64P, _DP]),
     "tblup_mt19937_jump": (_c.c_int, [_U32P, _c.c_int32, _c.c_uint64, _U32P, _I32P]),

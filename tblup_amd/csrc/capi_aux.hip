@@ -139,15 +139,22 @@ static int validate_de(int strategy, int64_t pop, int64_t L, const int32_t* dono
   return 0;
 }
 
-int tblup_de_step_device_async(tblup_ctx* c, int strategy, const double* d_parents, int64_t pop, int64_t L,
-                               int64_t ld, const int32_t* donors, const int64_t* fixed, double F, double cr, int clip,
-                               double clip_hi, const uint32_t* mt_key, int32_t mt_pos, double* d_children,
-                               int64_t ldc, void* stream) {
+// The asynchronous step, with optional per-individual strategies / F / crossover rates (host
+// arrays of pop; null: the scalars).
+static int de_step_async(tblup_ctx* c, int strategy, const int32_t* strat_i, const double* F_i, const double* cr_i,
+                         const double* d_parents, int64_t pop, int64_t L, int64_t ld, const int32_t* donors,
+                         const int64_t* fixed, double F, double cr, int clip, double clip_hi, const uint32_t* mt_key,
+                         int32_t mt_pos, double* d_children, int64_t ldc, void* stream) {
   clear_error();
   if (int rc = check_ctx(c)) return rc;
   if (c->de_pending) return fail(TBLUP_ERR_STATE, "the previous DE step's state was not fetched (tblup_de_state_wait)");
   int32_t* const mt_pos_in = &mt_pos;
   if (int rc = validate_de(strategy, pop, L, donors, fixed, cr, mt_key, mt_pos_in)) return rc;
+  for (int64_t i = 0; strat_i && i < pop; ++i)
+    if (strat_i[i] != TBLUP_DE_RAND_1 && strat_i[i] != TBLUP_DE_CURRENT_TO_BEST_1)
+      return fail(TBLUP_ERR_ARG, "unknown DE strategy");
+  for (int64_t i = 0; cr_i && i < pop; ++i)
+    if (!(cr_i[i] == cr_i[i])) return fail(TBLUP_ERR_ARG, "crossover rate is NaN");
   if (ld < L || ldc < L) return fail(TBLUP_ERR_ARG, "ld/ldc < L");
   if (!d_parents || !d_children) return fail(TBLUP_ERR_ARG, "null device pointers");
   HIPCHK(hipSetDevice(c->device));
@@ -164,7 +171,8 @@ int tblup_de_step_device_async(tblup_ctx* c, int strategy, const double* d_paren
   }
   // per-call arguments: key in, key out, pos out, donors, fixed
   const size_t o_keyo = 624 * 4, o_pos = 2 * 624 * 4, o_don = o_pos + 16, o_fix = o_don + (size_t)round_up(12 * pop, 16);
-  const size_t small = o_fix + 8 * (size_t)pop;
+  const size_t o_str = o_fix + 8 * (size_t)pop, o_F = o_str + (size_t)round_up(4 * pop, 16), o_cr = o_F + 8 * (size_t)pop;
+  const size_t small = o_cr + 8 * (size_t)pop;
   if (small > c->de_small.bytes) {
     HIPCHK(hipStreamSynchronize(s));
     if (int rc = dev_alloc(c, c->de_small, small)) return rc;
@@ -184,18 +192,42 @@ int tblup_de_step_device_async(tblup_ctx* c, int strategy, const double* d_paren
   std::memcpy(stage, mt_key, 624 * 4);
   std::memcpy(stage + o_don, donors, 12 * pop);
   std::memcpy(stage + o_fix, fixed, 8 * pop);
+  if (strat_i) std::memcpy(stage + o_str, strat_i, 4 * pop);
+  if (F_i) std::memcpy(stage + o_F, F_i, 8 * pop);
+  if (cr_i) std::memcpy(stage + o_cr, cr_i, 8 * pop);
   HIPCHK(hipMemcpyAsync(base, stage, small, hipMemcpyHostToDevice, s));
   const tblup_mt::EndState e = tblup_mt::end_state(mt_pos, 2 * (uint64_t)L * (uint64_t)pop);
   HIPCHK(launch_de_step((const uint32_t*)base, mt_pos, (const uint32_t*)c->de_polys.p, c->de_end_jump ? 1 : 0, e.s,
                         e.pos, d_parents, ld, (const int32_t*)(base + o_don), (const int64_t*)(base + o_fix), strategy,
                         F, cr, clip ? 1 : 0, clip_hi, L, (int)pop, d_children, ldc, (uint32_t*)(base + o_keyo),
-                        (int32_t*)(base + o_pos), s));
+                        (int32_t*)(base + o_pos), s, strat_i ? (const int32_t*)(base + o_str) : nullptr,
+                        F_i ? (const double*)(base + o_F) : nullptr, cr_i ? (const double*)(base + o_cr) : nullptr));
   if (!c->de_host) HIPCHK(hipHostMalloc((void**)&c->de_host, 625 * 4, hipHostMallocDefault));
   if (!c->de_ev) HIPCHK(hipEventCreateWithFlags(&c->de_ev, hipEventDisableTiming));
   HIPCHK(hipMemcpyAsync(c->de_host, base + o_keyo, 624 * 4 + 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->de_ev, s));
   c->de_pending = true;
   return 0;
+}
+
+int tblup_de_step_device_async(tblup_ctx* c, int strategy, const double* d_parents, int64_t pop, int64_t L,
+                               int64_t ld, const int32_t* donors, const int64_t* fixed, double F, double cr, int clip,
+                               double clip_hi, const uint32_t* mt_key, int32_t mt_pos, double* d_children,
+                               int64_t ldc, void* stream) {
+  return de_step_async(c, strategy, nullptr, nullptr, nullptr, d_parents, pop, L, ld, donors, fixed, F, cr, clip,
+                       clip_hi, mt_key, mt_pos, d_children, ldc, stream);
+}
+
+int tblup_de_step_device_async_mix(tblup_ctx* c, const int32_t* strategies, const double* F, const double* cr,
+                                   const double* d_parents, int64_t pop, int64_t L, int64_t ld, const int32_t* donors,
+                                   const int64_t* fixed, int clip, double clip_hi, const uint32_t* mt_key,
+                                   int32_t mt_pos, double* d_children, int64_t ldc, void* stream) {
+  if (!strategies || !F || !cr) {
+    clear_error();
+    return fail(TBLUP_ERR_ARG, "null strategies/F/cr");
+  }
+  return de_step_async(c, strategies[0], strategies, F, cr, d_parents, pop, L, ld, donors, fixed, F[0], cr[0], clip,
+                       clip_hi, mt_key, mt_pos, d_children, ldc, stream);
 }
 
 int tblup_de_state_wait(tblup_ctx* c, uint32_t* mt_key, int32_t* mt_pos) {

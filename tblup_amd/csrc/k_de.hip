@@ -82,6 +82,11 @@ struct DeArgs {
   int32_t* pos_out;
   int dbg;                 // phase-ablation timing only (env TBLUP_DE_DBG, diagnostic builds; results wrong):
                            // 1 no jump correlation, 2 no mask recurrence, 4 no stream
+  // per-individual strategy / F / crossover rate ([pop] each; null: the scalars above) -- SaDE
+  // (evolver.py:407-547): each individual's strategy by python's random.random() < p, its own cr
+  const int32_t* strat_i;
+  const double* F_i;
+  const double* cr_i;
 };
 
 __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
@@ -166,6 +171,8 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
   // streamed with every thread (coalesced loads, many in flight) instead of 312 lanes per block.
   const int f = i == 0 ? 0 : 2;
   const int64_t L = a.L;
+  const int strategy = a.strat_i ? a.strat_i[i] : a.strategy;
+  const double F = a.F_i ? a.F_i[i] : a.F, cr = a.cr_i ? a.cr_i[i] : a.cr;
   const double* P = a.parent + (int64_t)i * a.ldp;
   double* C = a.child + (int64_t)i * a.ldc;
   const int d0 = a.donors[3 * i], d1 = a.donors[3 * i + 1], d2 = a.donors[3 * i + 2];
@@ -193,7 +200,7 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
         if (j >= lo && j < hi) {
           const uint32_t w0 = mt_temper(blk[2 * q]) >> 5, w1 = mt_temper(blk[2 * q + 1]) >> 6;
           const double u = ((double)w0 * 67108864.0 + (double)w1) / 9007199254740992.0;
-          if (u < a.cr || j == fixed) atomicOr(&mask[(j - lo) >> 5], 1u << ((j - lo) & 31));
+          if (u < cr || j == fixed) atomicOr(&mask[(j - lo) >> 5], 1u << ((j - lo) & 31));
         }
       }
       if ((MTN / 2) * (b + 1) - f / 2 > hi) break;   // this block also feeds the next segment
@@ -223,8 +230,8 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
         if (j >= hi) continue;
         double v = x[r];
         if (m[r]) {
-          if (a.strategy == 0) v = y0[r] + a.F * (y1[r] - y2[r]);
-          else v = (v + a.F * (y0[r] - v)) + a.F * (y1[r] - y2[r]);
+          if (strategy == 0) v = y0[r] + F * (y1[r] - y2[r]);
+          else v = (v + F * (y0[r] - v)) + F * (y1[r] - y2[r]);
         }
         if (a.clip) {   // numpy's _NPY_CLIP: MIN(MAX(v, 0), hi) with a > b ? a : b, NaN passes through
           v = (v != v || v > 0.0) ? v : 0.0;
@@ -241,14 +248,15 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
 hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, int end_jump, int end_s, int end_pos,
                           const double* parent, int64_t ldp, const int32_t* donors, const int64_t* fixed, int strategy,
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
-                          uint32_t* key_out, int32_t* pos_out, hipStream_t s) {
+                          uint32_t* key_out, int32_t* pos_out, hipStream_t s, const int32_t* strat_i,
+                          const double* F_i, const double* cr_i) {
 #ifdef TBLUP_DIAG_BUILD   // phase ablation (results wrong when set): diagnostic builds only
   static const int dbg = getenv("TBLUP_DE_DBG") ? atoi(getenv("TBLUP_DE_DBG")) : 0;
 #else
   constexpr int dbg = 0;
 #endif
   DeArgs a{key, pos0, polys, end_jump, end_s, end_pos, parent, ldp, donors, fixed, strategy, F, cr, clip, hi, L, pop,
-           child, ldc, key_out, pos_out, dbg};
+           child, ldc, key_out, pos_out, dbg, strat_i, F_i, cr_i};
   hipLaunchKernelGGL(k_de_step, dim3(pop + 1), dim3(DE_THREADS), 0, s, a);
   return hipGetLastError();
 }

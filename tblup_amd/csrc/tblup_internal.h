@@ -312,7 +312,8 @@ hipError_t launch_decode_topk(const double* keys, int64_t B, int64_t d, int64_t 
 hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, int end_jump, int end_s, int end_pos,
                           const double* parent, int64_t ldp, const int32_t* donors, const int64_t* fixed, int strategy,
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
-                          uint32_t* key_out, int32_t* pos_out, hipStream_t s);
+                          uint32_t* key_out, int32_t* pos_out, hipStream_t s, const int32_t* strat_i = nullptr,
+                          const double* F_i = nullptr, const double* cr_i = nullptr);
 
 // ---- launcher (k_de.hip): rows from scattered device rows into one matrix (up to ROWPTRS rows
 //      per launch, source pointers in the kernel arguments) ----

@@ -16,15 +16,23 @@ uniforms, mutant, crossover and clip are computed in parallel.  The children's
 genomes and the numpy / python RNG states afterwards are bit-identical to the
 reference's sequential loop (tests/test_evolver.py, tests/test_gpu_evolver.py).
 
-SaDE and MDE_pBX (evolver.py:407-547, 550-687) draw per-individual F/CR from normal and
-Cauchy distributions and are not accelerated: `get_evolver` raises for them.
-There is no CPU fallback: without the HIP library, `evolve` raises ImportError.
+The adaptive evolvers keep the reference's bookkeeping (AdaptiveEvolver, evolver.py:297-404) on
+the host.  SaDE (evolver.py:407-547) runs its generation on the GPU too: every individual's
+strategy (python's random.random() < p) and crossover rate are drawn on the host in the
+reference's order and the step takes them per individual (tblup_de_step_device_async_mix; numpy's
+stream still holds one np.random.rand(L) per individual).  MDE_pBX (evolver.py:550-687) draws
+np.random.choice (rejection-sampled randint) between the individuals' np.random.rand(L) calls, so
+each individual's numpy stream offset depends on the draws before it; it runs its DE step on the
+host, as the reference does, with the reference's RNG consumption.
+There is no CPU fallback for the GPU steps: without the HIP library, `evolve` raises ImportError.
 """
 import abc
+import csv
 import ctypes
 import os
 import random
 from copy import deepcopy
+from math import ceil
 
 import numpy as np
 
@@ -40,10 +48,10 @@ def get_evolver(args):
         return DERandOneEvolver(args.dimensionality, args.crossover_rate, args.mutation_intensity, args.clip)
     if args.de_strategy == "de_currenttobest_1":
         return DECurrentToBestOneEvolver(args.dimensionality, args.crossover_rate, args.mutation_intensity, args.clip)
-    if args.de_strategy in ("sade", "mde_pbx"):
-        raise NotImplementedError(
-            "Evolver {} has no GPU step in tblup_amd (adaptive F/CR draws); use tblup.evolver.get_evolver for it"
-            .format(args.de_strategy))
+    if args.de_strategy == "sade":
+        return SaDE(args.dimensionality, args.clip)
+    if args.de_strategy == "mde_pbx":
+        return MDE_pBX(args.dimensionality, args.generations, args.clip)
     raise NotImplementedError("Evolver with config option {} is not implemented.".format(args.de_strategy))
 
 
@@ -130,7 +138,7 @@ class GpuDEStep:
         children as a device tensor.  Runs on torch's current stream.  defer: return
         (children, finish) without waiting for the step; finish() waits for the new MT state
         only (tblup_de_state_wait) and hands it to numpy -- call it before numpy's global RNG is
-        used again."""
+        used again.  strategy / F / cr: scalars, or one per individual (SaDE)."""
         import torch
         pop, L = parents.shape
         donors = np.ascontiguousarray(donors, dtype=np.int32)
@@ -142,12 +150,25 @@ class GpuDEStep:
             children = torch.empty_like(parents)
         st, key, pos = self._rng_state()
         stream = ws.cuda_stream
-        _native.check("tblup_de_step_device_async", self._lib.tblup_de_step_device_async(
-            self._ctx, int(strategy), ctypes.c_void_p(parents.data_ptr()), pop, L, parents.stride(0),
-            donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-            float(F), float(cr), 1 if clip else 0, float(clip_hi),
-            key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), pos.value,
-            ctypes.c_void_p(children.data_ptr()), children.stride(0), ctypes.c_void_p(stream)))
+        if np.ndim(strategy) or np.ndim(F) or np.ndim(cr):
+            strat_i = np.ascontiguousarray(np.broadcast_to(strategy, (pop,)), dtype=np.int32)
+            F_i = np.ascontiguousarray(np.broadcast_to(F, (pop,)), dtype=np.float64)
+            cr_i = np.ascontiguousarray(np.broadcast_to(cr, (pop,)), dtype=np.float64)
+            _native.check("tblup_de_step_device_async_mix", self._lib.tblup_de_step_device_async_mix(
+                self._ctx, strat_i.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                F_i.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), cr_i.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                ctypes.c_void_p(parents.data_ptr()), pop, L, parents.stride(0),
+                donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), 1 if clip else 0, float(clip_hi),
+                key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), pos.value,
+                ctypes.c_void_p(children.data_ptr()), children.stride(0), ctypes.c_void_p(stream)))
+        else:
+            _native.check("tblup_de_step_device_async", self._lib.tblup_de_step_device_async(
+                self._ctx, int(strategy), ctypes.c_void_p(parents.data_ptr()), pop, L, parents.stride(0),
+                donors.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), float(F), float(cr), 1 if clip else 0,
+                float(clip_hi), key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), pos.value,
+                ctypes.c_void_p(children.data_ptr()), children.stride(0), ctypes.c_void_p(stream)))
         cur.wait_stream(ws)   # later caller work on the children is ordered behind the step
 
         def finish():
@@ -186,7 +207,9 @@ def _child_dtypes(genomes, donors, strategy, mi, clip):
     e = np.zeros(0, dtype=bool)
     for i, (x, y, z) in enumerate(donors):
         t, a, b, c = (np.zeros(0, dtype=dts[j]) for j in (i, x, y, z))
-        mutant = a + mi * (b - c) if strategy == 0 else t + mi * (a - t) + mi * (b - c)
+        st = strategy[i] if np.ndim(strategy) else strategy
+        m = mi[i] if np.ndim(mi) else mi
+        mutant = a + m * (b - c) if st == 0 else t + m * (a - t) + m * (b - c)
         r = np.where(e, mutant, t)
         out.append((np.clip(r, 0, 1) if clip else r).dtype)
     return out
@@ -400,6 +423,14 @@ def _copy_individual(indv):
         indv._genome = g
 
 
+def _common_length(population):
+    n = len(population)
+    L = len(population[0].get_internal_genome()) if n else 0
+    if any(len(population[i].get_internal_genome()) != L for i in range(n)):
+        raise ValueError("DE needs internal genomes of one length (numpy broadcasting in evolver.py:132)")
+    return L
+
+
 class Evolver(abc.ABC):
     """evolver.py:35-44."""
 
@@ -428,15 +459,18 @@ class _GpuDEEvolver(Evolver):
         import time
         t = time.perf_counter()
         mi = 5 if population.generation % 5 == 0 else self.mutation_intensity
+        L = _common_length(population)
+        donors, fixed = self._donors(population, L)
+        return self._gpu_generation(population, t, donors, fixed, self.strategy, mi, self.crossover_rate,
+                                    self._clip())
+
+    def _gpu_generation(self, population, t, donors, fixed, strategy, mi, cr, clip):
+        """The children of one generation (donors / fixed: the python-`random` draws already made;
+        strategy, mi, cr: scalars or one per individual) through the GPU DE step."""
         n = len(population)
         import torch
         genomes = [population[i].get_internal_genome() for i in range(n)]
-        L = len(genomes[0])
-        if any(len(g) != L for g in genomes):
-            raise ValueError("DE needs internal genomes of one length (numpy broadcasting in evolver.py:132)")
-        donors, fixed = self._donors(population, L)
-        clip = self._clip()
-        dtypes = _child_dtypes(genomes, donors, self.strategy, mi, clip)
+        dtypes = _child_dtypes(genomes, donors, strategy, mi, clip)
         t = _mark(t, "ev_donors")
         step = GpuDEStep.get(self.device)
         import torch
@@ -446,8 +480,8 @@ class _GpuDEEvolver(Evolver):
             parents = store.gather(inds, L, host_rows=lambda i: genomes[i],
                                    copy_rows=step.gather_rows)   # device-resident parents
             t = _mark(t, "ev_gather")
-            children, rng_done = step.step_device(self.strategy, parents, donors, fixed, mi, self.crossover_rate,
-                                                  clip, self.dimensionality - 1, defer=True)
+            children, rng_done = step.step_device(strategy, parents, donors, fixed, mi, cr, clip,
+                                                  self.dimensionality - 1, defer=True)
             t = _mark(t, "ev_prepare_step")
             try:
                 # the population's evaluator (tblup_amd) may start evaluating the children on the GPU
@@ -588,3 +622,304 @@ class DECurrentToBestOneEvolver(_GpuDEEvolver):
             donors[i] = (best_index, a, b)
             fixed[i] = random.randrange(0, L)
         return donors, fixed
+
+
+# ---------------------------------------------------------------------------------------------
+# Adaptive evolvers (evolver.py:297-687)
+# ---------------------------------------------------------------------------------------------
+class AdaptiveEvolver(Evolver):
+    """Bookkeeping of the F / CR values whose candidates entered the population (evolver.py:297-404),
+    with the reference's parameter report (a `_params` CSV beside the monitor's results file)."""
+
+    def __init__(self):
+        self.successful_fs = []
+        self.successful_crs = []
+        self.previous_pop_uids = None
+        self.crs = []
+        self.fs = []
+
+    def should_report(self):
+        return True
+
+    def report(self, population):
+        stem, ext = os.path.splitext(os.path.basename(population.monitor.results_file))
+        path = os.path.join(os.path.dirname(population.monitor.results_file), stem + "_params" + ext)
+        if population.generation == 1:
+            with open(path, "w") as f:
+                csv.writer(f).writerow(self.get_header())
+        with open(path, "a") as f:
+            csv.writer(f).writerow(self.get_params_row())
+
+    @abc.abstractmethod
+    def get_header(self):
+        raise NotImplementedError()
+
+    @abc.abstractmethod
+    def get_params_row(self):
+        raise NotImplementedError()
+
+    def evolve(self, population):
+        """The per-generation adaptation step subclasses run first (evolver.py:336-356)."""
+        if self.should_report():
+            self.report(population)
+        if self.previous_pop_uids is None:
+            self.previous_pop_uids = [x.uid for x in population]
+        self.count_outcomes(population)
+        if self.should_regenerate_crs(population):
+            self.regenerate_crs(population)
+        if self.should_regenerate_fs(population):
+            self.regenerate_fs(population)
+        self.previous_pop_uids = [x.uid for x in population]
+
+    def count_outcomes(self, population):
+        """A changed uid at position i: the candidate made with crs[i] / fs[i] entered the population."""
+        for i, (old, cur) in enumerate(zip(self.previous_pop_uids, population)):
+            if old != cur.uid:
+                if i < len(self.crs):
+                    self.successful_crs.append(self.crs[i])
+                if i < len(self.fs):
+                    self.successful_fs.append(self.fs[i])
+
+    @abc.abstractmethod
+    def should_regenerate_crs(self, population):
+        raise NotImplementedError()
+
+    @abc.abstractmethod
+    def generate_cr(self):
+        raise NotImplementedError()
+
+    def regenerate_crs(self, population):
+        self.crs = [self.generate_cr() for _ in range(len(population))]
+
+    @abc.abstractmethod
+    def should_regenerate_fs(self, population):
+        raise NotImplementedError()
+
+    @abc.abstractmethod
+    def generate_f(self):
+        raise NotImplementedError()
+
+    def regenerate_fs(self, population):
+        self.fs = [self.generate_f() for _ in range(len(population))]
+
+
+class SaDE(AdaptiveEvolver, _GpuDEEvolver):
+    """Self-adaptive DE (Qin & Suganthan 2005; evolver.py:407-547), its generation on the GPU.
+
+    Per generation: cr_m re-estimated every 25 generations, the crossover rates redrawn every 5
+    (N(cr_m, 0.1) clipped to [0, 1]), one F ~ N(0.5, 0.3) clipped to [0, 2], and per individual
+    DE/rand/1 with probability p, else DE/current-to-best/1, p learnt from the strategies' success
+    counts after a 50-generation learning period.  The host draws what the reference draws, in its
+    order (numpy's normal() calls, then per individual random.random(), the donors and the forced
+    crossover position); the GPU step computes every child with its own strategy and rate."""
+
+    f_m = 0.5
+    f_std = 0.3
+    cr_std = 0.1
+    recalculate_mean_interval = 25
+    regenerate_crs_interval = 5
+    initial_learning_period = 50
+
+    def __init__(self, dimensionality, clip=True):
+        AdaptiveEvolver.__init__(self)
+        self.dimensionality = dimensionality
+        self.clip = clip
+        self.cr_m = 0.5
+        self.p = 0.5
+        self.strategy_one_indices = set()
+        self.ns_1, self.ns_2, self.nf_1, self.nf_2 = 0, 0, 0, 0
+
+    def get_header(self):
+        return ["cr_m", "p"]
+
+    def get_params_row(self):
+        return [self.cr_m, self.p]
+
+    def should_regenerate_crs(self, population):
+        return len(self.crs) == 0 or population.generation % self.regenerate_crs_interval == 0
+
+    def should_recalculate_cr_m(self, generation):
+        return generation != 0 and generation % self.recalculate_mean_interval == 0
+
+    def recalculate_cr_m(self):
+        if self.successful_crs:
+            self.cr_m = np.mean(self.successful_crs)
+
+    def generate_f(self):
+        return np.clip(np.random.normal(self.f_m, self.f_std), 0, 2)
+
+    def generate_cr(self):
+        return np.clip(np.random.normal(self.cr_m, self.cr_std), 0, 1)
+
+    def should_regenerate_fs(self, population):
+        return False
+
+    def recalculate_p(self, population):
+        if population.generation >= self.initial_learning_period and (self.ns_1 or self.ns_2):
+            num = self.ns_1 * (self.ns_2 + self.nf_2)
+            self.p = num / (self.ns_2 * (self.ns_1 + self.nf_1) + num)
+
+    def count_outcomes(self, population):
+        AdaptiveEvolver.count_outcomes(self, population)
+        if population.generation == self.initial_learning_period:
+            # learning period over: counters restart from one success each (evolver.py:479-484)
+            self.ns_1, self.ns_2, self.nf_1, self.nf_2 = 1, 1, 0, 0
+        for i, (old, cur) in enumerate(zip(self.previous_pop_uids, population)):
+            one = i in self.strategy_one_indices
+            if old == cur.uid:
+                if one:
+                    self.nf_1 += 1
+                else:
+                    self.nf_2 += 1
+            elif one:
+                self.ns_1 += 1
+            else:
+                self.ns_2 += 1
+
+    def evolve(self, population):
+        import time
+        t = time.perf_counter()
+        if self.should_recalculate_cr_m(population.generation):
+            self.recalculate_cr_m()
+        AdaptiveEvolver.evolve(self, population)
+        self.recalculate_p(population)
+        f = self.generate_f()
+        n = len(population)
+        L = _common_length(population)
+        best = max(population, key=lambda indv: indv.fitness)
+        best_index = population.population.index(best)
+        strategies = np.empty(n, dtype=np.int32)
+        donors = np.empty((n, 3), dtype=np.int32)
+        fixed = np.empty(n, dtype=np.int64)
+        self.strategy_one_indices = set()
+        for i in range(n):
+            if random.random() < self.p:   # DE/rand/1 (evolver.py:118-121)
+                self.strategy_one_indices.add(i)
+                strategies[i] = 0
+                a = exclusive_randrange(0, n, [i])
+                b = exclusive_randrange(0, n, [i, a])
+                donors[i] = (a, b, exclusive_randrange(0, n, [i, a, b]))
+            else:                          # DE/current-to-best/1 (evolver.py:199-203)
+                strategies[i] = 1
+                a = exclusive_randrange(0, n, [i, best_index])
+                donors[i] = (best_index, a, exclusive_randrange(0, n, [i, best_index, a]))
+            fixed[i] = random.randrange(0, L)   # the crossover's forced position (evolver.py:76)
+        crs = np.array([float(c) for c in self.crs[:n]], dtype=np.float64)
+        return self._gpu_generation(population, t, donors, fixed, strategies, f, crs, self.clip)
+
+
+class MDE_pBX(AdaptiveEvolver):
+    """MDE_pBX (Islam et al. 2012; evolver.py:550-687), the DE step on the host.
+
+    Each individual draws its group best and its parent with np.random.choice -- rejection-sampled
+    integers, a data-dependent number of MT19937 words -- between the individuals' np.random.rand(L)
+    calls, so an individual's numpy stream offset depends on every draw before it and cannot be
+    jumped to in parallel as the GPU step does.  The generation therefore runs as the reference's
+    loop: the same draws in the same order, DE/current-to-best/1 with the chosen best and parent,
+    binary crossover, optional clip."""
+
+    f_scale = 0.1
+    cr_std = 0.1
+    group_q = 0.15
+
+    def __init__(self, dimensionality, generations, clip=True):
+        AdaptiveEvolver.__init__(self)
+        self.dimensionality = dimensionality
+        self.clip = clip
+        self.g_max = generations
+        self.cr_m = 0.6
+        self.f_m = 0.5
+        self.p = None
+
+    def get_header(self):
+        return ["cr_m", "f_m"]
+
+    def get_params_row(self):
+        return [self.cr_m, self.f_m]
+
+    def should_regenerate_fs(self, population):
+        return True
+
+    def should_regenerate_crs(self, population):
+        return True
+
+    def generate_cr(self):
+        """N(cr_m, 0.1), redrawn until in [0, 1]."""
+        while True:
+            cr = np.random.normal(self.cr_m, self.cr_std)
+            if 0 <= cr <= 1:
+                return cr
+
+    def generate_f(self):
+        """Cauchy(f_m, 0.1) (scipy.stats.cauchy on numpy's global RandomState), redrawn until in [0, 1]."""
+        from scipy.stats import cauchy
+        while True:
+            f = cauchy.rvs(loc=self.f_m, scale=self.f_scale)
+            if 0 <= f <= 1:
+                return f
+
+    @staticmethod
+    def mean_pow(vals, n=1.5):
+        """The power mean of formula (10), simplified for positive values as the reference does."""
+        assert n > 0, "n must be a positive number."
+        return sum(vals) / pow(1 / len(vals), -n)
+
+    @staticmethod
+    def get_weight_factor(p, q):
+        return p + q * random.random()
+
+    def recalculate_cr_m(self):
+        if self.successful_crs:
+            w = self.get_weight_factor(0.9, 0.1)
+            self.cr_m = w * self.cr_m + (1 - w) * self.mean_pow(self.successful_crs)
+            self.successful_crs = []
+
+    def recalculate_f_m(self):
+        if self.successful_fs:
+            w = self.get_weight_factor(0.8, 0.2)
+            self.f_m = w * self.f_m + (1 - w) * self.mean_pow(self.successful_fs)
+            self.successful_fs = []
+
+    def recalculate_p(self, population):
+        self.p = ceil((len(population) / 2) * (1 - (population.generation / self.g_max)))
+
+    def evolve(self, population):
+        self.recalculate_cr_m()
+        self.recalculate_f_m()
+        self.recalculate_p(population)
+        AdaptiveEvolver.evolve(self, population)
+        order = np.argsort([x.fitness for x in population])
+        q_best = order[-int(len(population) * self.group_q):]
+        p_best = order[-self.p:]
+        n = len(population)
+        out = []
+        for i in range(n):
+            best = population[np.random.choice(q_best, 1).item()]
+            parent_idx = np.random.choice(p_best, 1).item()
+            out.append(_host_current_to_best(population, self.fs[i], self.crs[i], self.dimensionality, parent_idx,
+                                             best, self.clip))
+        return out
+
+
+def _host_current_to_best(population, mi, cr, dimensionality, parent_idx, best, clip):
+    """DECurrentToBestOneEvolver.de_currenttobest_one with binary crossover (evolver.py:63-82,
+    179-221) on the host: the reference's draws (exclusive_randrange x 2, random.randrange, one
+    np.random.rand(L)) and its float arithmetic order."""
+    n = len(population)
+    best_index = population.population.index(best)
+    excl = [parent_idx, best_index]
+    a = exclusive_randrange(0, n, excl)
+    excl.append(a)
+    b = exclusive_randrange(0, n, excl)
+    ga, gb = population[a].get_internal_genome(), population[b].get_internal_genome()
+    child = deepcopy(population[parent_idx])
+    x = child.get_internal_genome()
+    mutant = x + mi * (best.get_internal_genome() - x) + mi * (ga - gb)
+    L = len(x)
+    fixed = random.randrange(0, L)
+    take = np.random.rand(L) < cr
+    take[fixed] = True
+    child.set_internal_genome(np.where(take, mutant, x))
+    if clip:
+        child.set_internal_genome(np.clip(child.get_internal_genome(), 0, dimensionality - 1))
+    return child

@@ -416,6 +416,135 @@ def gen_de():
     np.savez_compressed(os.path.join(HERE, "de.npz"), **out)
 
 
+SADE_CASES = [
+    # name, individual kind, d, length, pop, generations, clip
+    ("sade_rk", "rk", 150, 15, 8, 56, False),
+    ("sade_rk_clip", "rk", 120, 10, 6, 12, True),
+    ("sade_index", "index", 200, 20, 6, 12, True),
+]
+
+
+def gen_sade():
+    """The reference's SaDE (evolver.py:297-547) over whole runs of generations: each generation's
+    children (the first ones whole, then by checksum), the adaptive state after it (cr_m, p, the
+    strategy success / failure counts), the parameter CSV it reports (AdaptiveEvolver.report) and the
+    RNG states at the end.  The children's fitness comes from a generator of its own (never python's
+    `random` or numpy's global one), and selection is DE's greedy replacement (selector.py:27-32), so
+    the success counting of count_outcomes sees real uid changes; 56 generations cover the cr
+    regenerations (every 5), the cr_m recalculations (25, 50) and the learning period's reset (50)."""
+    from tblup.evolver import SaDE
+    from tblup.individual import RandomKeyIndividual, IndexIndividual
+    out = {}
+    for ci, (name, kind, d, length, pop, gens, clip) in enumerate(SADE_CASES):
+        rng = np.random.default_rng(300 + ci)
+        if kind == "index":
+            parents = [rng.integers(0, d, size=length) for _ in range(pop)]
+            inds = [IndexIndividual(length, d, genome=g.copy()) for g in parents]
+        else:
+            parents = [rng.uniform(size=d) for _ in range(pop)]
+            inds = [RandomKeyIndividual(length, d, genome=g.copy()) for g in parents]
+        fit = rng.uniform(size=pop)
+        for ind, f in zip(inds, fit):
+            ind.fitness = float(f)
+        frng = np.random.default_rng(400 + ci)
+        tmp = tempfile.mkdtemp()
+
+        class Mon:
+            results_file = os.path.join(tmp, "results.csv")
+
+        random.seed(500 + ci)
+        np.random.seed(600 + ci)
+        np.random.rand(3 * ci + 1)
+        ev = SaDE(d, clip=clip)
+        popn = _Pop(inds, 1)
+        popn.monitor = Mon
+        p = "%s_" % name
+        sha_rows, state = [], []
+        for g in range(1, gens + 1):
+            popn.generation = g
+            kids = ev.evolve(popn)
+            kg = np.stack([np.asarray(k.get_internal_genome()) for k in kids])
+            if g <= 3:
+                out[p + "children_g%d" % g] = kg
+            sha_rows.append(sha(kg))
+            state.append([ev.cr_m, ev.p, ev.ns_1, ev.ns_2, ev.nf_1, ev.nf_2, len(ev.successful_crs)])
+            for k, f in zip(kids, frng.uniform(size=pop)):
+                k.fitness = float(f)
+            popn.population = [k if k.fitness > q.fitness else q for q, k in zip(popn.population, kids)]
+        st = np.random.get_state()
+        out[p + "parents"] = np.stack([np.asarray(g) for g in parents])
+        out[p + "fitness"] = fit
+        out[p + "children_sha256"] = np.array(sha_rows)
+        out[p + "state"] = np.array(state, dtype=np.float64)
+        out[p + "children_dtype"] = np.array(str(kg.dtype))
+        out[p + "params_csv"] = np.array(open(os.path.join(tmp, "results_params.csv")).read())
+        out[p + "mt_key"] = np.asarray(st[1], dtype=np.uint32)
+        out[p + "mt_pos"] = np.int64(st[2])
+        out[p + "gauss"] = np.array([st[3], st[4]], dtype=np.float64)
+        out[p + "py_next"] = np.float64(random.random())
+    np.savez_compressed(os.path.join(HERE, "sade.npz"), **out)
+
+
+MDE_CASES = [
+    # name, individual kind, d, length, pop, generations (g_max), clip
+    ("mde_rk", "rk", 150, 15, 12, 8, False),
+    ("mde_index", "index", 200, 20, 8, 6, True),
+]
+
+
+def gen_mde():
+    """The reference's MDE_pBX (evolver.py:550-687) over whole runs, recorded as gen_sade records
+    SaDE (the adaptive state: cr_m, f_m, p)."""
+    from tblup.evolver import MDE_pBX
+    from tblup.individual import RandomKeyIndividual, IndexIndividual
+    out = {}
+    for ci, (name, kind, d, length, pop, gens, clip) in enumerate(MDE_CASES):
+        rng = np.random.default_rng(700 + ci)
+        if kind == "index":
+            parents = [rng.integers(0, d, size=length) for _ in range(pop)]
+            inds = [IndexIndividual(length, d, genome=g.copy()) for g in parents]
+        else:
+            parents = [rng.uniform(size=d) for _ in range(pop)]
+            inds = [RandomKeyIndividual(length, d, genome=g.copy()) for g in parents]
+        fit = rng.uniform(size=pop)
+        for ind, f in zip(inds, fit):
+            ind.fitness = float(f)
+        frng = np.random.default_rng(800 + ci)
+        tmp = tempfile.mkdtemp()
+
+        class Mon:
+            results_file = os.path.join(tmp, "results.csv")
+
+        random.seed(900 + ci)
+        np.random.seed(1000 + ci)
+        ev = MDE_pBX(d, gens, clip=clip)
+        popn = _Pop(inds, 1)
+        popn.monitor = Mon
+        p = "%s_" % name
+        sha_rows, state = [], []
+        for g in range(1, gens + 1):
+            popn.generation = g
+            kids = ev.evolve(popn)
+            kg = np.stack([np.asarray(k.get_internal_genome()) for k in kids])
+            if g <= 2:
+                out[p + "children_g%d" % g] = kg
+            sha_rows.append(sha(kg))
+            state.append([ev.cr_m, ev.f_m, ev.p, len(ev.successful_crs), len(ev.successful_fs)])
+            for k, f in zip(kids, frng.uniform(size=pop)):
+                k.fitness = float(f)
+            popn.population = [k if k.fitness > q.fitness else q for q, k in zip(popn.population, kids)]
+        st = np.random.get_state()
+        out[p + "parents"] = np.stack([np.asarray(g) for g in parents])
+        out[p + "fitness"] = fit
+        out[p + "children_sha256"] = np.array(sha_rows)
+        out[p + "state"] = np.array(state, dtype=np.float64)
+        out[p + "params_csv"] = np.array(open(os.path.join(tmp, "results_params.csv")).read())
+        out[p + "mt_key"] = np.asarray(st[1], dtype=np.uint32)
+        out[p + "mt_pos"] = np.int64(st[2])
+        out[p + "py_next"] = np.float64(random.random())
+    np.savez_compressed(os.path.join(HERE, "mde.npz"), **out)
+
+
 def gen_pca():
     """pca_splitter (evaluator.py:641-663) on synthetic panels: n = 200 (sklearn's full SVD)
     and n = 600 (randomized SVD drawing from numpy's global RNG, seeded), both directions."""
@@ -631,7 +760,7 @@ def gen_main_runs():
 GENERATORS = {
     "grm": gen_grm, "blup": gen_blup_small, "edge": gen_blup_edge, "decode": gen_decode,
     "flow": gen_evaluator_flow, "config2": gen_blup_config2, "de": gen_de, "pca": gen_pca, "seed": gen_seed,
-    "extra": gen_blup_extra, "main": gen_main_runs,
+    "extra": gen_blup_extra, "main": gen_main_runs, "sade": gen_sade, "mde": gen_mde,
 }
 
 if __name__ == "__main__":

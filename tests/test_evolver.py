@@ -109,7 +109,7 @@ def test_get_evolver_factory():
     assert isinstance(ev, E.DERandOneEvolver) and ev.clip is False
     args.de_strategy = "de_currenttobest_1"
     assert isinstance(E.get_evolver(args), E.DECurrentToBestOneEvolver)
-    for bad in ("sade", "mde_pbx", "nope"):
+    for bad in ("nope",):
         args.de_strategy = bad
         with pytest.raises(NotImplementedError):
             E.get_evolver(args)
@@ -181,3 +181,98 @@ def test_native_donors_small_population_stays_in_python():
                              d.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                              f.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
     assert rc != 0 and b"pop" in lib.tblup_last_error()
+
+
+# ---- adaptive evolvers (evolver.py:297-687) against whole reference runs (tests/golden/make_golden.py
+# gen_sade / gen_mde): every generation's children, the adaptive state, the parameter CSV, the RNGs ----
+ADAPT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# name -> (kind, d, length, pop, generations, clip, case index): make_golden.py SADE_CASES / MDE_CASES
+SADE_META = {"sade_rk": ("rk", 150, 15, 8, 56, False, 0), "sade_rk_clip": ("rk", 120, 10, 6, 12, True, 1),
+             "sade_index": ("index", 200, 20, 6, 12, True, 2)}
+MDE_META = {"mde_rk": ("rk", 150, 15, 12, 8, False, 0), "mde_index": ("index", 200, 20, 8, 6, True, 1)}
+
+
+def _adaptive_run(z, name, meta, make_evolver, seeds, tmp_path, state_of):
+    """Drive `make_evolver()` through the recorded run: individuals with the reference's semantics
+    (tests/ga_driver.py), fitness from the run's own generator, greedy selection."""
+    import hashlib
+    from tests import ga_driver as GD
+    from tests.helpers import Pop
+    kind, d, length, pop, gens, clip, ci = meta
+    parents = z[name + "_parents"]
+    cls = GD.IndexIndividual if kind == "index" else GD.RandomKeyIndividual
+    inds = [cls(length, d, genome=parents[i].copy()) for i in range(pop)]
+    for ind, f in zip(inds, z[name + "_fitness"]):
+        ind.fitness = float(f)
+    frng = np.random.default_rng(seeds[2] + ci)
+    random.seed(seeds[0] + ci)
+    np.random.seed(seeds[1] + ci)
+    if name.startswith("sade"):
+        np.random.rand(3 * ci + 1)
+    ev = make_evolver(d, gens, clip)
+    popn = Pop(inds, 1)
+    popn.monitor = SimpleNamespace(results_file=str(tmp_path / "results.csv"))
+    for g in range(1, gens + 1):
+        popn.generation = g
+        kids = ev.evolve(popn)
+        kg = np.stack([np.asarray(k.get_internal_genome()) for k in kids])
+        if name + "_children_g%d" % g in z.files:
+            np.testing.assert_array_equal(kg, z[name + "_children_g%d" % g])
+        assert hashlib.sha256(np.ascontiguousarray(kg).tobytes()).hexdigest() == str(z[name + "_children_sha256"][g - 1]), g
+        np.testing.assert_array_equal(np.array(state_of(ev), dtype=np.float64), z[name + "_state"][g - 1])
+        for k, f in zip(kids, frng.uniform(size=pop)):
+            k.fitness = float(f)
+        popn.population = [k if k.fitness > q.fitness else q for q, k in zip(popn.population, kids)]
+    assert open(tmp_path / "results_params.csv").read() == str(z[name + "_params_csv"])
+    st = np.random.get_state()
+    np.testing.assert_array_equal(np.asarray(st[1], dtype=np.uint32), z[name + "_mt_key"])
+    assert st[2] == int(z[name + "_mt_pos"])
+    if name + "_gauss" in z.files:
+        assert [st[3], st[4]] == list(z[name + "_gauss"])
+    assert random.random() == float(z[name + "_py_next"])
+
+
+def _sade_state(ev):
+    return [ev.cr_m, ev.p, ev.ns_1, ev.ns_2, ev.nf_1, ev.nf_2, len(ev.successful_crs)]
+
+
+@pytest.mark.parametrize("name", sorted(SADE_META))
+def test_sade_host_side_matches_reference(name, tmp_path, monkeypatch):
+    """tblup_amd.evolver.SaDE (its adaptation, draws and report) over a whole reference run, with the
+    GPU DE step swapped for the oracle's children from the same draws (the GPU step itself:
+    tests/test_gpu_evolver.py)."""
+    from copy import deepcopy
+    from tblup_amd import evolver as EV
+
+    def host_generation(self, population, t, donors, fixed, strategy, mi, cr, clip):
+        genomes = [population[i].get_internal_genome() for i in range(len(population))]
+        kids = D.de_children(genomes, strategy, donors, fixed, mi, cr, clip, self.dimensionality - 1)
+        out = []
+        for i, c in enumerate(kids):
+            k = deepcopy(population[i])
+            k.set_internal_genome(c)
+            out.append(k)
+        return out
+    monkeypatch.setattr(EV.SaDE, "_gpu_generation", host_generation)
+    z = np.load(os.path.join(ADAPT, "sade.npz"))
+    _adaptive_run(z, name, SADE_META[name], lambda d, g, clip: EV.SaDE(d, clip), (500, 600, 400), tmp_path,
+                  _sade_state)
+
+
+@pytest.mark.parametrize("name", sorted(MDE_META))
+def test_mde_pbx_matches_reference(name, tmp_path):
+    """tblup_amd.evolver.MDE_pBX (host DE step) reproduces whole reference runs: children, the adapted
+    cr_m / f_m / p, the parameter CSV and both RNG states."""
+    from tblup_amd import evolver as EV
+    z = np.load(os.path.join(ADAPT, "mde.npz"))
+    _adaptive_run(z, name, MDE_META[name], lambda d, g, clip: EV.MDE_pBX(d, g, clip), (900, 1000, 800), tmp_path,
+                  lambda ev: [ev.cr_m, ev.f_m, ev.p, len(ev.successful_crs), len(ev.successful_fs)])
+
+
+def test_get_evolver_adaptive():
+    from tblup_amd import evolver as EV
+    a = SimpleNamespace(de_strategy="sade", dimensionality=10, clip=True, generations=5)
+    assert isinstance(EV.get_evolver(a), EV.SaDE)
+    a.de_strategy = "mde_pbx"
+    e = EV.get_evolver(a)
+    assert isinstance(e, EV.MDE_pBX) and e.g_max == 5
