@@ -210,6 +210,13 @@ class DeviceKeyStore:
         g = getattr(indv, "_genome", None)
         return g if isinstance(g, np.ndarray) else None
 
+    def record_rows(self, tensor, individuals, arrays):
+        """record() for a generation's children that the evolver has just bound to fresh TrackedGenome
+        rows (every individual's genome IS arrays[i]): one dict update."""
+        self._entries.update({indv.uid: (tensor, i, weakref.ref(g), getattr(indv, "length", None))
+                              for i, (indv, g) in enumerate(zip(individuals, arrays))
+                              if getattr(indv, "_genome", None) is g})
+
     def record(self, tensor, individuals, arrays, adopt=False):
         """Row i of `tensor` (pop x L, on the device) holds arrays[i]; recorded for individuals
         whose internal genome IS that array (RandomKey / Index semantics: get_internal_genome()
