@@ -473,6 +473,7 @@ class _GpuDEEvolver(Evolver):
         n = len(population)
         import torch
         genomes = [population[i].get_internal_genome() for i in range(n)]
+        L = len(genomes[0])
         dtypes = _child_dtypes(genomes, donors, strategy, mi, clip)
         t = _mark(t, "ev_donors")
         step = GpuDEStep.get(self.device)
