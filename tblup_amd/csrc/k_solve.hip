@@ -135,8 +135,21 @@ __device__ __forceinline__ double sum8(double v) {
 // bit-identical, so the launcher may pick either per batch) ----
 constexpr int PCTH = 512;   // Pearson / centring-term reductions as over 512 threads
 
-// p = (L_JI^T beta_J)[row] for the 16 r of lane group seg of the row's 8 threads (x: the row's
-// 16 doubles at r = 16 seg ..), xor-reduced over the 8 threads: every thread of the row holds p
+// The tile stream's mapping: the 8 threads of a row take its 16-B chunks interleaved -- thread seg
+// chunks seg, seg + 8, .., seg + 56 -- so each load instruction of a wave covers 8 whole 128-B lines
+// (8 rows) instead of 64 lines 16 B apart (thread seg once held 16 consecutive doubles: every load then
+// touched a line per lane -- PMC at config 2: the texture address unit stalled by the L1 for 87M
+// cycles per k_solve launch, profiles/r05_pmc_units.json), and the beta_J reads of one instruction hit 8
+// consecutive 16-B LDS chunks (bank-conflict free).
+// v of the X_J products (vsh) keeps 2 doubles of padding after every 16: the 16-element segment s
+// that the row's thread s reads starts at 18 s, so a wave's 8 segments fall on 8 distinct bank groups
+// (unpadded, 128 B apart, they fell on 2: 4-way conflicts; 52.9M SQ_LDS_BANK_CONFLICT cycles per
+// k_solve launch with the old tile mapping).
+constexpr int TPAD = TILE + TILE / 8;
+__device__ __forceinline__ int vpi(int i) { return i + 2 * (i >> 4); }
+
+// p = (L_JI^T beta_J)[row] over the row's chunks of thread seg (x[e]: doubles 2 (seg + 8 e), +1 of the
+// row), xor-reduced over the row's 8 threads: every thread of the row holds p
 template <int NTR>
 __device__ __forceinline__ void tile_row_partial(const v2d (&x)[8], const double* beta, int64_t stride, int seg,
                                                  double (&p)[NTR]) {
@@ -146,8 +159,8 @@ __device__ __forceinline__ void tile_row_partial(const v2d (&x)[8], const double
   for (int e = 0; e < 8; ++e)   // explicit fmas: no contraction choice left to the compiler
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr)
-      p[tr] = __builtin_fma(x[e][1], beta[tr * stride + 16 * seg + 2 * e + 1],
-                            __builtin_fma(x[e][0], beta[tr * stride + 16 * seg + 2 * e], p[tr]));
+      p[tr] = __builtin_fma(x[e][1], beta[tr * stride + 2 * seg + 16 * e + 1],
+                            __builtin_fma(x[e][0], beta[tr * stride + 2 * seg + 16 * e], p[tr]));
 #pragma unroll
   for (int tr = 0; tr < NTR; ++tr) {
     p[tr] = sum8(p[tr]);
@@ -165,7 +178,7 @@ __device__ __forceinline__ bool xrow_load(const double* Dj, int row, int seg, v2
   return ok;
 }
 template <int NTR>
-__device__ __forceinline__ void xrow_apply(const v2d (&xr)[8], bool ok, int row, int seg, const double (*vsh)[TILE],
+__device__ __forceinline__ void xrow_apply(const v2d (&xr)[8], bool ok, int row, int seg, const double (*vsh)[TPAD],
                                            double (&s2)[NTR]) {
 #pragma unroll
   for (int tr = 0; tr < NTR; ++tr) s2[tr] = 0.0;
@@ -174,7 +187,7 @@ __device__ __forceinline__ void xrow_apply(const v2d (&xr)[8], bool ok, int row,
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const v2d xv = xr[m];
-      const int i0 = 16 * seg + 2 * (m ^ sw);
+      const int i0 = 18 * seg + 2 * (m ^ sw);   // vpi(16 seg + 2 (m ^ sw))
 #pragma unroll
       for (int tr = 0; tr < NTR; ++tr) s2[tr] = __builtin_fma(xv[1], vsh[tr][i0 + 1], __builtin_fma(xv[0], vsh[tr][i0], s2[tr]));
     }
@@ -218,7 +231,7 @@ template <int NTR>
 __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict__ fit, double* __restrict__ ebv) {
   extern __shared__ double dyn[];  // alpha[nt][ns], e[nt][nV], then (primal) int32 rowp[ns]
   __shared__ double part[NTH / 64][2 * TILE];   // reused as [64][64]
-  __shared__ double vsh[MAXT][TILE];
+  __shared__ double vsh[MAXT][TPAD];
   __shared__ double wblk[KBLK];
   __shared__ double red[4 * 16];
   const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, ns = c.sd.ns, prow = c.sd.prow;
@@ -251,13 +264,13 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     // two tiles per step: 256 B per thread (256 KiB per workgroup) in flight
     for (int J = I + 1; J < ((c.skip & 1024) ? 0 : NT); J += 2) {
       const bool two = J + 1 < NT;
-      const double* row0 = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 16 * seg;
+      const double* row0 = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 2 * seg;
       const double* row1 = two ? row0 + (int64_t)NT * TILE * TILE : row0;
       v2d x0[8], x1[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x0[e] = *reinterpret_cast<const v2d*>(row0 + 2 * e);
+      for (int e = 0; e < 8; ++e) x0[e] = *reinterpret_cast<const v2d*>(row0 + 16 * e);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x1[e] = *reinterpret_cast<const v2d*>(row1 + 2 * e);
+      for (int e = 0; e < 8; ++e) x1[e] = *reinterpret_cast<const v2d*>(row1 + 16 * e);
       double p[NTR];
       tile_row_partial<NTR>(x0, alpha + J * TILE, ns, seg, p);
 #pragma unroll
@@ -273,7 +286,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     const bool xrow = xrow_load(Db + (int64_t)I * NPACK * BLKD, rc, seg, xr);
 #pragma unroll
     for (int tr = 0; tr < NTR; ++tr)
-      if (seg == 0) vsh[tr][rc] = alpha[tr * ns + (int64_t)I * TILE + rc] - s[tr];
+      if (seg == 0) vsh[tr][vpi(rc)] = alpha[tr * ns + (int64_t)I * TILE + rc] - s[tr];
     __syncthreads();
     double s2[NTR];
     xrow_apply<NTR>(xr, xrow, rc, seg, vsh, s2);
@@ -528,15 +541,15 @@ __device__ __forceinline__ void chain_publish(int32_t* f, int32_t seq, int mode)
 }
 
 // rows rc and rc + 64 of tile (J, I) (transposed storage: row r = column 128 I + r of L, block J),
-// 16 contiguous doubles at 16 seg each
+// the row's 16-B chunks seg + 8 e (tile_row_partial's mapping)
 __device__ __forceinline__ void chain_tile_load(const CholLaunch& c, int64_t b, int J, int I, int rc, int seg,
                                                 v2d (&x)[2][8]) {
   const int NT = c.sd.NT;
-  const double* tile = c.L + ((b * NT + J) * (int64_t)NT + I) * TILE * TILE + 16 * seg;
+  const double* tile = c.L + ((b * NT + J) * (int64_t)NT + I) * TILE * TILE + 2 * seg;
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[h][e] = *reinterpret_cast<const v2d*>(tile + (rc + 64 * h) * TILE + 2 * e);
+    for (int e = 0; e < 8; ++e) x[h][e] = *reinterpret_cast<const v2d*>(tile + (rc + 64 * h) * TILE + 16 * e);
 }
 
 // c_{J->I} = L_JI^T beta_J (beta_J in bsh) -> cpart, then its flag
@@ -559,7 +572,7 @@ __device__ __forceinline__ void chain_tile_publish(const SolveChain& ch, int64_t
 template <int NTR>
 __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, double* fit, double* ebv,
                            double* xl, int* sh, ChainTrace& tr_) {
-  __shared__ double vsh[NTR][TILE];   // z_J, then v
+  __shared__ double vsh[NTR][TPAD];   // z_J, then v (padded: vpi)
   __shared__ double bsh[NTR][TILE];   // beta_J
   __shared__ int32_t rowp[TILE];
   __shared__ double red[4 * 16];
@@ -583,7 +596,7 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
   }
   v2d x[2][8];
   if (J > 0) chain_tile_load(c, b, J, J - 1, rc, seg, x);
-  for (int i = t; i < NTR * TILE; i += CTH) vsh[i / TILE][i % TILE] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
+  for (int i = t; i < NTR * TILE; i += CTH) vsh[i / TILE][vpi(i % TILE)] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
   for (int r = t; r < nr; r += CTH) {
     const int64_t g = (int64_t)J * TILE + r;
     rowp[r] = (g < pad) ? (int32_t)c.d.P : (int32_t)snp_col(c.idx[o0 + g - pad], c.d.P);
@@ -601,7 +614,7 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
     const int tr = i / TILE, cc = i % TILE;
     double acc = 0.0;
     for (int K = J + 1; K < NT; ++K) acc += cload(ch.cpart + (((b * NT + J) * NT + K) * NTR + tr) * TILE + cc);
-    vsh[tr][cc] = vsh[tr][cc] - acc;
+    vsh[tr][vpi(cc)] = vsh[tr][vpi(cc)] - acc;
   }
   __syncthreads();
 #pragma unroll
