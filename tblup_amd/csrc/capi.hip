@@ -241,10 +241,20 @@ bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B) {
 // A/B): the diagonal launches lose ~8 us each at every B (0.349 -> 0.282 ms per step at B = 32,
 // 0.394 -> 0.331 at 256) but the off-diagonal launches gain 42 (B = 32) to 97 us (256): +3.3% at
 // 32, +2.0% at 64, -1.3% at 128, -1% at 192 and 256.
+// Per diagonal launch (bit J: diagonal J takes its last term from launch J-1), round 5: at
+// 64 < B <= 160 only diagonal launches 1 and 3 -- the workgroup traces of round 4 (pop 128,
+// profiles/r04_wg_trace_pop128_auto.txt / _lastterm.txt) give, per launch, the off-diagonal launch's
+// extra time against the next diagonal launch's saving: J = 0: -1.1 / -9.1 us, J = 2: +0.5 / -5.6;
+// every other launch loses.
 constexpr int64_t LT_MAX_B = 64;
-bool use_last_term(const tblup_ctx* c, const SysDims& sd, int64_t B) {
-  return sd.NT >= 2 && (c->last_term == 1 || (c->last_term < 0 && B <= LT_MAX_B));
+constexpr int64_t LT_PART_MAX_B = 160;
+uint32_t last_term_mask(const tblup_ctx* c, const SysDims& sd, int64_t B) {
+  if (sd.NT < 2 || c->last_term == 0) return 0;
+  if (c->lt_mask >= 0) return (uint32_t)c->lt_mask;
+  if (c->last_term == 1 || B <= LT_MAX_B) return ~1u;   // every diagonal launch J >= 1
+  return B <= LT_PART_MAX_B ? (1u << 1) | (1u << 3) : 0u;
 }
+bool use_last_term(const tblup_ctx* c, const SysDims& sd, int64_t B) { return last_term_mask(c, sd, B) != 0; }
 
 size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k,
                    bool with_ebv) {
@@ -467,12 +477,14 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   // chip is already full during the off-diagonal launches, and sharing CUs slows the
   // critical path more than it hides.)
   const double Bd = (double)B;
+  const uint32_t ltm = last_term_mask(c, sd, B);
   for (int J = 0; !redo && J < sd.NT; ++J) {
     const double jt = (double)J;
     const OffPlan& p = plan[J];
     // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
     // forward-substitution GEMV (the exact system tiles are counted under KC_GRM)
-    const double lt_d = Qb ? 0.0 : std::min(jt, 1.0);   // the last SYRK term's share of this launch
+    const bool qd = Qb && ((ltm >> J) & 1u), qo = Qb && ((ltm >> (J + 1)) & 1u);
+    const double lt_d = qd ? 0.0 : std::min(jt, 1.0);   // the last SYRK term's share of this launch
     // (+ the D-units when they run in this launch: 128^3 per L < J, as in the off-diagonal launch)
     const double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt) + (p.ndd ? Bd * T3 * jt : 0.0);
     const double bd = Bd * (TILE * TILE * lt_d * 8.0 + 2.0 * TILE * TILE * 8.0) +
@@ -481,7 +493,9 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       cl.wgt = wgt + c->wgt_used * WGT_REC;
       c->wgt_used += B * (1 + p.ndd) + DTR_RECS;
     }
+    cl.q = qd ? Qb : nullptr;   // diagonal J: its last term from launch J-1
     rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, p, s); });
+    cl.q = qo ? Qb : nullptr;   // off-diagonal J: the last term of diagonal J+1
     if (rc) return rc;
     if (p.nI > 0) {
       // T-units: GEMM1 over the L not summed ahead (2*128^3 each) + the triangular solve 128^3;
@@ -489,7 +503,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       // tiles' int-ops are excluded
       const double lt = p.ahead_cur ? 1.0 : jt;
       const double fo = Bd * p.nI * (2.0 * T3 * lt + T3) + Bd * p.nP * 2.0 * T3 * jt + (p.nds ? Bd * T3 * jt : 0.0) +
-                        (Qb ? Bd * T3 : 0.0);
+                        (qo ? Bd * T3 : 0.0);
       const double bo = Bd * p.nI * (TILE * TILE * lt * 8.0 + TILE * TILE * 8.0) +
                         Bd * p.nP * (2.0 * TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) +
                         (p.nds ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
@@ -623,6 +637,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_SOLVE_CHAIN")) c->solve_chain = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_CHAIN_SYNC")) c->chain_sync = atoi(e);
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_LT_MASK")) c->lt_mask = (int)strtol(e, nullptr, 0);
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_SYS_ST")) c->sys_st = std::max(-1, std::min(1, atoi(e)));

@@ -94,7 +94,8 @@ struct tblup_ctx {
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
   int diag_d = -1;    // TBLUP_DIAG_D: D-units in the diagonal launch (-1 auto, 0 never, 1 always)
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
-  int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (B <= LT_MAX_B), 0 never, 1 always (see use_last_term)
+  int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (last_term_mask), 0 never, 1 always (see use_last_term)
+  int lt_mask = -1;      // TBLUP_LT_MASK: the diagonal launches in last-term mode by bit (A/B timing; -1 auto)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
