@@ -158,7 +158,7 @@ static double list_makespan(std::initializer_list<std::pair<double, int64_t>> cl
 }
 
 OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_pol, int64_t slots, int diag_d,
-                        int dd_maxj) {
+                        int dd_maxj, int diag_e, int64_t ncu) {
   OffPlan p{};
   p.nI = NT - J - 1;
   if (p.nI <= 0) {
@@ -183,6 +183,19 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   if (dt && (diag_d == 1 || (diag_d < 0 && B > DD_MIN_B && B <= DD_MAX_B && J <= dd_maxj))) {
     p.ndd = 1;
     dt = 0;
+  }
+  // E-units: column J's GEMM1 term L = Ls0 of its first tiles, on the CUs the diagonal launch J
+  // leaves idle (its B diagonal workgroups and D-units take one CU each: 144 KiB of LDS).  One term
+  // (29 us alone on a CU, measured) ends inside the ~45 us diagonal launch.  Auto: every idle CU
+  // when the column's tiles all get one or the idle CUs are >= 2B; else none -- an off-diagonal
+  // launch of one round is as long as its longest units, so shortening a third of the tiles gains
+  // nothing while the E-units' loads slow the diagonal launch (A/B, profiles/r05_epol_ab.txt: pop 32
+  // +8.5%, 64 +2.6% with partial columns vs +0.8% without, 96 / 160 partial columns -0.5 / -1%).
+  // 2: only columns whose every tile gets one.
+  if (J >= 1 && (diag_e == 1 || ((diag_e < 0 || diag_e == 2) && ncu > 0))) {
+    const int64_t idle = std::max<int64_t>(0, ncu - B * (1 + p.ndd));
+    p.ne = diag_e == 1 ? B * p.nI : std::min<int64_t>(B * p.nI, idle);
+    if (p.ne < B * p.nI && (diag_e == 2 || idle < 2 * B)) p.ne = 0;
   }
   p.nrs = 1;
   p.nds = dt;
@@ -220,9 +233,16 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
 
 namespace {
 
-bool any_ahead(const tblup_ctx* c, int64_t B, int NT, bool st) {
-  for (int J = 0; J < NT; ++J)
-    if (off_plan(B, NT, J, st, c->ahead, c->nrs, AHEAD_SLOTS, c->diag_d).nP > 0) return true;
+OffPlan plan_of(const tblup_ctx* c, int64_t B, int NT, int J, bool st) {
+  return off_plan(B, NT, J, st, c->ahead, c->nrs, AHEAD_SLOTS, c->diag_d, DD_MAX_J, c->diag_e, cu_count());
+}
+
+// the chunk's launches hand partial sums of off-diagonal tiles on (P-units or E-units)
+bool uses_part(const tblup_ctx* c, int64_t B, int NT, bool st) {
+  for (int J = 0; J < NT; ++J) {
+    const OffPlan p = plan_of(c, B, NT, J, st);
+    if (p.nP > 0 || p.ne > 0) return true;
+  }
   return false;
 }
 
@@ -272,7 +292,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add((size_t)B * sd.NT * NPACK * BLKD * 8);                    // diagonal GRM tiles
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * KD_TILE * 2 : 0);  // their int16 counts (k_sys_tiles)
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
-  add(any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
+  add(uses_part(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
   if (use_chain(c, sd, B)) {                                    // chained solve: beta, c_{J->I}, EBV shares
     add((size_t)B * d.nt * sd.ns * 8);
     add((size_t)B * sd.NT * sd.NT * d.nt * TILE * 8);
@@ -395,15 +415,23 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* Kdg = cv.take<double>((size_t)B * sd.NT * NPACK * BLKD);
   int16_t* kdb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * KD_TILE) : nullptr;
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
-  double* Pp = any_ahead(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
+  double* Pp = uses_part(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
   double* Qb = use_last_term(c, sd, B) ? cv.take<double>((size_t)B * NPACK * BLKD) : nullptr;
   const bool fold_share = use_st && ft.nf > 1 && ft.share;   // k_sys_tiles_folds
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
-  for (int J = 0; J < sd.NT; ++J) plan[J] = off_plan(B, sd.NT, J, use_st, Pp ? c->ahead : 0, c->nrs, AHEAD_SLOTS, c->diag_d);
+  for (int J = 0; J < sd.NT; ++J) plan[J] = plan_of(c, B, sd.NT, J, use_st);
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
+  // the scalars formed after k_sys_tiles_st / k_sys_tiles_folds, in their K_JJ epilogue launch (one
+  // launch less; neither reads a scalar), else by k_indiv_stats first
+  CholLaunch probe{};
+  probe.B = B;
+  probe.sd = sd;
+  probe.sys_st = c->sys_st;
+  const bool fuse_stats = !redo && use_st && sd.form == FORM_PRIMAL && (fold_share || sys_tiles_grid(probe) > 0);
+  const StatsFuse sf{csA, d.n, d.nT, branch, h2, (int32_t*)c->status.p + ST_INDEX, scal, u, rhs};
   int rc = 0;
-  if (!redo)
+  if (!redo && !fuse_stats)
     rc = timed(c, s, KC_STATS, 2.0 * (double)h_off[B], stats_bytes, [&] {
       return launch_indiv_stats(d_idx, d_off, B, ft, csA, d, sd, branch, h2, scal, u, rhs,
                                 (int32_t*)c->status.p + ST_INDEX, s);
@@ -439,7 +467,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   uint64_t* wgt = nullptr;
   if (c->wg_trace && !redo) {
     int64_t nwg = 0;
-    for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + DTR_RECS + offdiag_grid(plan[J], B);
+    for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + plan[J].ne + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
     if (use_chain(c, sd, B)) nwg += B * sd.NT;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
@@ -461,9 +489,11 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       const int64_t sg = fold_share ? -(B * sd.NT * (sd.NT + 1) / 2) : sys_tiles_grid(cl);
       c->wgt_used += sg > 0 ? sg : -sg;
     }
-    rc = timed(c, s, KC_GRM, fg, bg, [&] {
+    cl.stats = fuse_stats ? &sf : nullptr;
+    rc = timed(c, s, KC_GRM, fg, bg + (fuse_stats ? stats_bytes : 0.0), [&] {
       return fold_share ? launch_sys_tiles_folds(cl, s) : launch_sys_tiles(cl, s);
     });
+    cl.stats = nullptr;
     if (rc) return rc;
   } else {
     // int ops of the diagonal GRM tiles J < 2 (J >= 2 run inside the column-0 off-diagonal launch)
@@ -486,12 +516,14 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     const bool qd = Qb && ((ltm >> J) & 1u), qo = Qb && ((ltm >> (J + 1)) & 1u);
     const double lt_d = qd ? 0.0 : std::min(jt, 1.0);   // the last SYRK term's share of this launch
     // (+ the D-units when they run in this launch: 128^3 per L < J, as in the off-diagonal launch)
-    const double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt) + (p.ndd ? Bd * T3 * jt : 0.0);
+    // (+ the E-units: one 2*128^3 GEMM1 term each, moved out of launch J's T-units)
+    const double fd = Bd * (T3 * lt_d + 2.0 * T3 / 3.0 + 2.0 * TILE * TILE * jt) + (p.ndd ? Bd * T3 * jt : 0.0) +
+                      (double)p.ne * 2.0 * T3;
     const double bd = Bd * (TILE * TILE * lt_d * 8.0 + 2.0 * TILE * TILE * 8.0) +
-                      (p.ndd ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
+                      (p.ndd ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0) + (double)p.ne * 3.0 * TILE * TILE * 8.0;
     if (wgt) {
       cl.wgt = wgt + c->wgt_used * WGT_REC;
-      c->wgt_used += B * (1 + p.ndd) + DTR_RECS;
+      c->wgt_used += B * (1 + p.ndd) + p.ne + DTR_RECS;
     }
     cl.q = qd ? Qb : nullptr;   // diagonal J: its last term from launch J-1
     rc = timed(c, s, KC_DIAG, fd, bd, [&] { return launch_chol_diag(cl, J, p, s); });
@@ -503,7 +535,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
       // tiles' int-ops are excluded
       const double lt = p.ahead_cur ? 1.0 : jt;
       const double fo = Bd * p.nI * (2.0 * T3 * lt + T3) + Bd * p.nP * 2.0 * T3 * jt + (p.nds ? Bd * T3 * jt : 0.0) +
-                        (qo ? Bd * T3 : 0.0);
+                        (qo ? Bd * T3 : 0.0) - (double)p.ne * 2.0 * T3;
       const double bo = Bd * p.nI * (TILE * TILE * lt * 8.0 + TILE * TILE * 8.0) +
                         Bd * p.nP * (2.0 * TILE * TILE * jt * 8.0 + TILE * TILE * 8.0) +
                         (p.nds ? 2.0 * Bd * TILE * TILE * jt * 8.0 : 0.0);
@@ -642,6 +674,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_SYS_ST")) c->sys_st = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_DIAG_E")) c->diag_e = std::max(-1, std::min(2, atoi(e)));
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_NRS")) c->nrs = (atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 0;
   if (const char* e = getenv("TBLUP_CHAIN_DEBUG")) {

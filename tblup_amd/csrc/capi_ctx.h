@@ -93,6 +93,7 @@ struct tblup_ctx {
   int ahead = -1;     // TBLUP_AHEAD: -1 auto (per launch: B * (NT - 2 - j) < AHEAD_SLOTS), 0 never, 1 always
   int nrs = 0;        // TBLUP_NRS: partial-sum row slices, 0 auto, else 1 / 2 / 4
   int diag_d = -1;    // TBLUP_DIAG_D: D-units in the diagonal launch (-1 auto, 0 never, 1 always)
+  int diag_e = -1;    // TBLUP_DIAG_E: E-units in the diagonal launch (-1 auto, 0 never, 1 every tile)
   int chain_sync = 0;    // TBLUP_CHAIN_SYNC (k_solve.hip)
   int last_term = -1;    // TBLUP_LAST_TERM: -1 auto (last_term_mask), 0 never, 1 always (see use_last_term)
   int lt_mask = -1;      // TBLUP_LT_MASK: the diagonal launches in last-term mode by bit (A/B timing; -1 auto)

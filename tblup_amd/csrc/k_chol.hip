@@ -27,6 +27,7 @@
 // makes its accumulator land in the f64 C layout, so the exact integer GRM counts
 // become the fp64 accumulators of the Cholesky GEMM without any data movement.
 #include "i8_tile.h"
+#include "k_stats.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -1146,26 +1147,6 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
   dstamp(a, 29);
 }
 
-// Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
-// K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.
-__global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
-  __shared__ double rsh[MAXT][TILE];
-  WgTrace tr(a.wgt);
-  if ((int64_t)blockIdx.x >= a.B) {
-    // OffPlan::ndd: the D-unit of diagonal target J+1 (S = K - sum_{L<J}), on a CU the diagonal
-    // workgroups (dispatched first) leave idle; blocks B + x and x share an XCD when 8 | B
-    const int64_t b = xcd_remap(blockIdx.x - a.B, gridDim.x - a.B);
-    syrk_partial8(a, b, a.J + 1, a.J, lds, 0);
-    tr.done(WGT_DPREP, a.J, a.J + 1, b);
-    return;
-  }
-  // individual b on the XCD that runs its off-diagonal tiles (same L2 for L, S, X, w)
-  const int64_t b = xcd_remap(blockIdx.x, a.B);
-  diag_tile(a, b, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
-  tr.done(WGT_DIAG, a.J, a.J, b);
-}
-
 // ---------------------------------------------------------------------------
 // Off-diagonal launch of column J: one 8-wave workgroup per unit, two per CU (LDS <= 72 KiB).
 //   T-unit, tile (I, J), I > J:
@@ -1279,7 +1260,7 @@ __device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, i
 }
 
 // T-unit: tile (I, J).
-__device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, int ahead_cur, double* lds,
+__device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, int ahead_cur, int edone, double* lds,
                                           double* uj_sh, double* ui_sh, double (*zj_sh)[TILE]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int J = a.J, NT = a.NT;
@@ -1288,7 +1269,8 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
   const double* Lb = a.L + b * (int64_t)NT * NT * TT;
   v4d acc[8];
   int2 kcv[8];
-  if (ahead_cur) {
+  const bool from_part = ahead_cur || edone;
+  if (from_part) {
     const double* pd = part_ptr(a, b, I, J);
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb) {
@@ -1307,10 +1289,10 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
       zj_sh[tr][t] = (tr < a.nt) ? a.z[(b * a.nt + tr) * ns + j0 + t] : 0.0;
   }
   __syncthreads();
-  if (!ahead_cur) k_acc<8>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
+  if (!from_part) k_acc<8>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
 
-  // 1. T^T = K_JI - sum_L L_JL L_IL^T over the L not summed by launch J-1
-  const int Ls = ahead_cur ? J - 1 : 0;
+  // 1. T^T = K_JI - sum_L L_JL L_IL^T over the L not summed by launch J-1 or this tile's E-unit
+  const int Ls = (ahead_cur ? J - 1 : 0) + edone;
   if (J > Ls && !(a.skip & 64))
     gemm1_a32<8>(Lb + (int64_t)J * NT * TT + (int64_t)Ls * TT, Lb + (int64_t)I * NT * TT + (int64_t)Ls * TT, J - Ls, 0,
                  lds, acc, Ls == 0 ? skip_rows(a, b) : 0);
@@ -1377,6 +1359,77 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
     syrk_lower8_32(Lout, 8, lds, qa, 0, J == 0 ? skip_rows(a, b) : 0);
     store_syrk_blocks(a.q + b * (int64_t)NPACK * BLKD, nullptr, qa, 0);
   }
+}
+
+// E-unit (diagonal launch J, on a CU its other workgroups leave idle): the GEMM1 term L = ls0 of tile
+// (I, J) -- from K_JI (ls0 = 0) or from launch J-1's partial over L < J-1 (ls0 = J-1) -- into the
+// partial-sum slot J&1, where launch J's T-unit picks it up (OffPlan::ne).  The same k_acc start and
+// gemm1_a32 MFMA chains as the T-unit, split after the term: bit-identical.
+__device__ __forceinline__ void e_unit(const CholArgs& a, int64_t b, int I, int ls0, double* lds) {
+  const int t = threadIdx.x, l = t & 63;
+  const int J = a.J, NT = a.NT;
+  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
+  double* uj_sh = lds + NPACK * BLKD;   // past the GEMM1 ring (2 x 32 KiB) and k_acc's int8 ring
+  double* ui_sh = uj_sh + TILE;
+  double* pd = part_ptr(a, b, I, J);
+  v4d acc[8];
+  if (ls0 > 0) {
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const v2d* s2 = reinterpret_cast<const v2d*>(pd + (cb * 64 + l) * 4);
+      const v2d lo = s2[0], hi = s2[1];
+      acc[cb] = v4d{lo[0], lo[1], hi[0], hi[1]};
+    }
+  } else {
+    int2 kcv[8];
+    if (a.kc) kc_issue<8>(a, b, I, J, 0, kcv);
+    if (t < TILE) {
+      uj_sh[t] = a.u[b * a.prow + j0 + t];
+      ui_sh[t] = a.u[b * a.prow + i0 + t];
+    }
+    __syncthreads();
+    k_acc<8>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
+  }
+  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+  if (!(a.skip & 64))
+    gemm1_a32<8>(Lb + (int64_t)J * NT * TT + (int64_t)ls0 * TT, Lb + (int64_t)I * NT * TT + (int64_t)ls0 * TT, 1, 0, lds,
+                 acc, ls0 == 0 ? skip_rows(a, b) : 0);
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) {
+    v2d* d = reinterpret_cast<v2d*>(pd + (cb * 64 + l) * 4);
+    d[0] = v2d{acc[cb][0], acc[cb][1]};
+    d[1] = v2d{acc[cb][2], acc[cb][3]};
+  }
+}
+
+// Diagonal tile J of every individual: for J >= 2 the previous off-diagonal launch left
+// K_JJ - sum_{L < J-1} in S[J&1], and the L = J-1 term is subtracted here.  Grid: the B diagonal
+// workgroups, then nd D-units, then ne E-units (OffPlan).
+__global__ __launch_bounds__(DTHR) void k_chol_diag(CholArgs a, int64_t ne, int ls0) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * NPACK * BLKD];   // 144 KiB: T/L and X
+  __shared__ double rsh[MAXT][TILE];
+  WgTrace tr(a.wgt);
+  if ((int64_t)blockIdx.x >= a.B) {
+    const int64_t x = blockIdx.x - a.B, nd = gridDim.x - a.B - ne;
+    if (x < nd) {
+      // OffPlan::ndd: the D-unit of diagonal target J+1 (S = K - sum_{L<J}), on a CU the diagonal
+      // workgroups (dispatched first) leave idle; blocks B + x and x share an XCD when 8 | B
+      const int64_t b = xcd_remap(x, nd);
+      syrk_partial8(a, b, a.J + 1, a.J, lds, 0);
+      tr.done(WGT_DPREP, a.J, a.J + 1, b);
+    } else {
+      const int64_t lg = xcd_remap(x - nd, ne);
+      const int64_t b = lg % a.B;
+      const int I = a.J + 1 + (int)(lg / a.B);
+      e_unit(a, b, I, ls0, lds);
+      tr.done(WGT_EPART, a.J, I, b);
+    }
+    return;
+  }
+  // individual b on the XCD that runs its off-diagonal tiles (same L2 for L, S, X, w)
+  const int64_t b = xcd_remap(blockIdx.x, a.B);
+  diag_tile(a, b, a.J, a.J >= 2 ? a.J - 1 : 0, lds, rsh);
+  tr.done(WGT_DIAG, a.J, a.J, b);
 }
 
 // K_JJ for every (individual, J) with the off-diagonal kernel's 8-wave int8 tile (A = B =
@@ -1507,7 +1560,9 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
       b = lg / p.nI;
       I = a.J + 1 + (int)(lg % p.nI);
     }
-    tile_unit(a, b, I, p.ahead_cur, lds, uj_sh, ui_sh, zj_sh);
+    // an E-unit of the diagonal launch summed the term L = Ls0 of the first ne tiles (I-major)
+    const int ed = (int64_t)(I - a.J - 1) * a.B + b < p.ne ? 1 : 0;
+    tile_unit(a, b, I, p.ahead_cur, ed, lds, uj_sh, ui_sh, zj_sh);
     tr.done(WGT_TILE, a.J, I, b);
     return;
   }
@@ -1539,13 +1594,12 @@ constexpr int STW = 4;   // waves per system-tile workgroup
 
 // K_JJ + lambda I (identity on padding rows) from a diagonal tile's accumulators (exact counts in
 // fp32) as packed fp64 blocks into Kd: the tiles J < 2, which the diagonal kernel reads directly
-__device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr,
-                                                      int qc, int l) {
-  const double* sc = a.scal + b * SCAL;
+// (sc / ub: the system's scalars and tile J's centring sums -- scal / u, or their LDS copies)
+__device__ __forceinline__ void sys_diag_epilogue_src(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr,
+                                                      int qc, int l, const double* sc, const double* ub) {
   const int64_t j0 = (int64_t)J * TILE;
   const double sa_ = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], lam = sc[SC_LAM], sm = sc[SC_SM];
   const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
-  const double* ub = a.u + b * a.prow + j0;
   double* Kd = a.Kd + (b * a.NT + J) * (int64_t)NPACK * BLKD;
   // every centring sum this lane needs, loaded before the first store (Kd and u are both double
   // pointers: loads interleaved with the stores were issued one after another, ~47 us a launch)
@@ -1574,6 +1628,10 @@ __device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v
         Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
       }
     }
+}
+__device__ __forceinline__ void sys_diag_epilogue_inl(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr,
+                                                      int qc, int l) {
+  sys_diag_epilogue_src(a, cnt, b, J, qr, qc, l, a.scal + b * SCAL, a.u + b * a.prow + (int64_t)J * TILE);
 }
 __device__ void sys_diag_epilogue(const CholArgs& a, const v4f (&cnt)[4][4], int64_t b, int J, int qr, int qc, int l);
 
@@ -1721,8 +1779,9 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
   constexpr int TB2 = 2 * TILE * 64;   // one 256-row operand image of a stage: 16 KiB
   __shared__ __attribute__((aligned(16))) uint8_t lds[D * 2 * TB2];   // 96 KiB at D = 3
   __shared__ int32_t rowtab[SP_ROWTAB];
-  __shared__ int32_t cblk_tab[SP_MAXIND];   // contraction blocks of the run's individuals (no global
-                                            // load inside the ring: its use would wait vmcnt(0))
+  __shared__ int32_t cblk_tab[SP_MAXIND];   // contraction blocks of the run's individuals (SNP form:
+                                            // n_Tp / 64 each, SC_CBLK -- not read from scal, so this
+                                            // launch may precede the scalars' k_stats_diag_counts)
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int tj = w >> 2, qr = (w >> 1) & 1, qc = w & 1;
   const int NT = a.NT;
@@ -1788,7 +1847,7 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
   };
   if (u0 >= u1) return;
   const int nind = (u1 - 1) / nsu - b_first + 1;
-  if (t < nind) cblk_tab[t] = (int32_t)a.scal[(int64_t)(b_first + t) * SCAL + SC_CBLK];
+  if (t < nind) cblk_tab[t] = (int32_t)(a.ytp / KBLK);
   __syncthreads();
   setup_issue();
   // total stages of the run (the units of one individual share its stage count)
@@ -2050,6 +2109,49 @@ __global__ __launch_bounds__(64 * STW) void k_sys_diag_counts(CholArgs a) {
   sys_diag_epilogue_inl(a, cnt, s, J, qr, qc, l);
 }
 
+// k_sys_tiles_st chunks: k_sys_diag_counts with the per-individual scalars formed here (the same
+// stats_wg code as k_indiv_stats) instead of in a launch before the system tiles -- one launch less
+// on the chain.  Workgroup (b, J < 2): stats_wg (workgroup J = 0 also stores scal), tile
+// J's centring sums into LDS, then the epilogue from the LDS copies; the u / rhs rows are split
+// between the two workgroups.
+__global__ __launch_bounds__(64 * STW) void k_stats_diag_counts(CholArgs a, StatsFuse x) {
+  static_assert(64 * STW == STATS_THREADS, "stats_wg runs on the workgroup's 256 threads");
+  __shared__ StatsShared sh;
+  __shared__ double u_sh[TILE];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, qr = w >> 1, qc = w & 1;
+  const int64_t b = blockIdx.x >> 1;
+  const int J = (int)(blockIdx.x & 1);
+  const bool tile = qr >= qc && J < a.NT;   // the upper quadrant is never read
+  // the counts first: their loads overlap the scalars' reduction
+  v4f cnt[4][4];
+  const int16_t* kt = a.kd + (b * a.NT + J) * KD_TILE;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cb = 4 * qr + m, ib = 4 * qc + n;
+      int2 p = {0, 0};
+      if (tile && cb >= ib) p = *reinterpret_cast<const int2*>(kt + ((cb * (cb + 1) / 2 + ib) * 64 + l) * 4);
+      cnt[m][n] = v4f{(float)(int16_t)(p.x & 0xffff), (float)(int16_t)(p.x >> 16), (float)(int16_t)(p.y & 0xffff),
+                      (float)(int16_t)(p.y >> 16)};
+    }
+  // the u / rhs rows split between the individual's two workgroups
+  const int64_t half = (a.ns / 2 + 63) & ~(int64_t)63;
+  stats_wg(a.idx, a.off, a.ft, x.csA, x.n, x.nT, a.ytp, a.P, a.form, a.ns, a.padfirst, a.nt, x.branch, x.h2, b,
+           J == 0 ? x.scal : nullptr, x.u, x.rhs, x.err, sh, J == 0 ? 0 : half, J == 0 ? half : a.ns);
+  // u_a = s_a of tile J's rows (stats_wg's u, from the same loads)
+  if (t < TILE) {
+    const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
+    const int64_t pad = a.padfirst ? a.ns - k : 0;
+    const int64_t r = (int64_t)J * TILE + t;
+    const int32_t* csT = a.ft.csT[fold_of(a.ft, b)];
+    u_sh[t] = (r < a.ns && sys_real(r, pad, k)) ? (double)csT[snp_col(a.idx[o0 + r - pad], a.P)] : 0.0;
+  }
+  __syncthreads();
+  if (!tile) return;
+  sys_diag_epilogue_src(a, cnt, b, J, qr, qc, l, sh.sc, u_sh);
+}
+
 static CholArgs make_args(const CholLaunch& c, int J) {
   CholArgs a{c.L, c.Dinv, c.z, c.w, c.S, c.Kd, c.yT, c.rhs, c.panel, c.pstride, c.u, c.scal, c.sd.ns,
              c.sd.prow, c.sd.form, c.idx, c.off, c.gpk_row, c.d.P, c.d.nTp, c.d.nt, c.sd.NT, J, c.skip,
@@ -2058,7 +2160,7 @@ static CholArgs make_args(const CholLaunch& c, int J) {
   return a;
 }
 
-static int cu_count() {
+int cu_count() {
   static int n = 0;
   if (n <= 0) {
     int dev = 0;
@@ -2090,8 +2192,12 @@ hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
                        (int)(c.B * (NS * (NS + 1) / 2)));
     if (hipError_t e = hipGetLastError()) return e;
     a.wgt = nullptr;
-    hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a);
+    if (c.stats)
+      hipLaunchKernelGGL(k_stats_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a, *c.stats);
+    else
+      hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a);
   } else {
+    if (c.stats) return hipErrorInvalidValue;   // the per-tile kernel reads the scalars
     hipLaunchKernelGGL(k_sys_tiles, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
   }
   return hipGetLastError();
@@ -2103,7 +2209,10 @@ hipError_t launch_sys_tiles_folds(const CholLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL(k_sys_tiles_folds, dim3((unsigned)(c.ft.bpf * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
   if (hipError_t e = hipGetLastError()) return e;
   a.wgt = nullptr;
-  hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a);
+  if (c.stats)   // k_sys_tiles_folds reads no scalar either
+    hipLaunchKernelGGL(k_stats_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a, *c.stats);
+  else
+    hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a);
   return hipGetLastError();
 }
 
@@ -2124,10 +2233,12 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
 
 hipError_t launch_chol_diag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s) {
   CholArgs a = make_args(c, J);
-  const int64_t nwg = c.B * (1 + p.ndd);
+  const int64_t nwg = c.B * (1 + p.ndd) + p.ne;
+  // E-units need the partial-sum slots and a tile below the diagonal
+  if (p.ne > 0 && (c.part == nullptr || J < 1 || p.ne > c.B * p.nI)) return hipErrorInvalidValue;
   // profiling: the phase stamps of this launch follow its workgroup records
   if (c.wgt) a.dtr = c.wgt + nwg * WGT_REC;
-  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)nwg), dim3(DTHR), 0, s, a);
+  hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)nwg), dim3(DTHR), 0, s, a, p.ne, p.ahead_cur ? J - 1 : 0);
   return hipGetLastError();
 }
 

@@ -195,13 +195,21 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
       if (b > 0) mt_block(ring, (int)(b & 1), tid);
       const uint32_t* blk = ring + (b & 1) * MTN;
       const int q = tid;
-      if (q < MTN / 2 && !(b == 0 && q < f / 2)) {
-        const int64_t j = (MTN / 2) * b + q - f / 2;
-        if (j >= lo && j < hi) {
-          const uint32_t w0 = mt_temper(blk[2 * q]) >> 5, w1 = mt_temper(blk[2 * q + 1]) >> 6;
-          const double u = ((double)w0 * 67108864.0 + (double)w1) / 9007199254740992.0;
-          if (u < cr || j == fixed) atomicOr(&mask[(j - lo) >> 5], 1u << ((j - lo) & 31));
-        }
+      const int64_t j = (MTN / 2) * b + q - f / 2;
+      const bool valid = q < MTN / 2 && !(b == 0 && q < f / 2) && j >= lo && j < hi;
+      bool set = false;
+      if (valid) {
+        const uint32_t w0 = mt_temper(blk[2 * q]) >> 5, w1 = mt_temper(blk[2 * q + 1]) >> 6;
+        const double u = ((double)w0 * 67108864.0 + (double)w1) / 9007199254740992.0;
+        set = u < cr || j == fixed;
+      }
+      // a wave's elements are consecutive: one OR per mask word it touches (<= 3), from the word's
+      // first lane in the wave, instead of 32 lanes' atomics on one LDS word (bank conflicts)
+      const uint64_t bal = __builtin_amdgcn_ballot_w64(set);
+      const int lane = tid & 63, bit = (int)((j - lo) & 31);
+      if (valid && (bit == 0 || lane == 0)) {
+        const uint32_t wb = (uint32_t)(lane >= bit ? bal >> (lane - bit) : bal << (bit - lane));
+        if (wb) atomicOr(&mask[(j - lo) >> 5], wb);
       }
       if ((MTN / 2) * (b + 1) - f / 2 > hi) break;   // this block also feeds the next segment
     }

@@ -14,6 +14,7 @@
 //   sum_s (a_is - 2p_s)(a_js - 2p_s) = (A A^T)_ij - (u_i + u_j)/N + q/N^2
 // with u_i = sum_s m_s a_is and q = sum_s m_s^2.
 #include "tblup_internal.h"
+#include "k_stats.h"
 
 namespace tblup {
 
@@ -157,82 +158,21 @@ hipError_t launch_fold_offsets(const int64_t* off, int64_t B, int64_t F, int64_t
 // ---------------------------------------------------------------------------
 // per-individual scalars: branch, 1/N, q/N^2, 1/d, mu, lambda
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_indiv_stats(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
-                                                     FoldTab ft, const int32_t* __restrict__ csA, int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
-                                                     int64_t ns, int pad_first, int nt, int branch, double h2,
-                                                     double* __restrict__ scal, double* __restrict__ u,
-                                                     double* __restrict__ rhs, int32_t* __restrict__ err) {
-  const int64_t b = blockIdx.x;
-  const int64_t o0 = off[b], k = off[b + 1] - o0;
-  const int32_t* __restrict__ csT = ft.csT[fold_of(ft, b)];   // the system's split
-  const double* __restrict__ xty = ft.xty[fold_of(ft, b)];
-  int mode = branch;
-  if (mode == 0) mode = (k > n) ? 1 : 2;  // evaluator.py:257
-  const int32_t* cs = (mode == 1) ? csA : csT;
-  const bool primal = form == FORM_PRIMAL;   // snp branch only (host guarantees)
-  int64_t m1 = 0, q = 0;
-  int bad = 0;
-  for (int64_t s = threadIdx.x; s < k; s += 256) {
-    const int64_t p = idx[o0 + s];
-    bad |= (p < -P || p >= P);
-    const int64_t m = cs[snp_col(p, P)];
-    m1 += m;
-    q += m * m;
-  }
-  __shared__ int64_t r1[256], r2[256];
-  __shared__ double invd_sh;
-  r1[threadIdx.x] = m1;
-  r2[threadIdx.x] = q;
-  const int any_bad = __syncthreads_or(bad);
-  if (any_bad && threadIdx.x == 0) *err = 1;   // vector store; every writer stores 1
-  for (int st = 128; st > 0; st >>= 1) {
-    if ((int)threadIdx.x < st) {
-      r1[threadIdx.x] += r1[threadIdx.x + st];
-      r2[threadIdx.x] += r2[threadIdx.x + st];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const double N = (mode == 1) ? (double)n : (double)nT;
-    const double M1 = (double)r1[0], Q = (double)r2[0];
-    const double d = M1 / N - Q / (2.0 * N * N);  // 2 sum p(1-p)
-    double* sc = scal + b * SCAL;
-    // primal (SNP-space) form: C_ab = (X^T X)_ab - s_a s_b / n_T over train rows
-    sc[SC_SA] = primal ? 0.0 : 1.0 / N;
-    sc[SC_CN] = primal ? 0.0 : Q / (N * N);
-    sc[SC_INVD] = 1.0 / d;
-    sc[SC_MUF] = (mode == 2) ? 1.0 : 0.0;
-    sc[SC_LAM] = (1.0 - h2) / h2;
-    sc[SC_D] = d;
-    sc[SC_MODE] = (double)mode;
-    sc[SC_K] = (double)k;
-    sc[SC_SM] = primal ? 1.0 / (double)nT : 0.0;
-    sc[SC_NROW] = primal ? (double)k : (double)nT;
-    sc[SC_CBLK] = primal ? (double)(nTp / KBLK) : (double)((k + KBLK - 1) / KBLK);
-    sc[SC_BAD] = any_bad ? 1.0 : 0.0;
-    sc[SC_PAD] = (primal && pad_first) ? (double)(ns - k) : 0.0;
-    invd_sh = 1.0 / d;
-  }
-  if (!primal) return;
-  __syncthreads();
-  // u_a = s_a (train allele count), rhs_ta = X_c^T (y_T,t - mu_t) / d = xty[t][p_a] / d
-  // (the sklearn primal right-hand side in 1/d units); zero on padding rows (system row a holds
-  // selected SNP a - pad)
-  const double invd = invd_sh;
-  const int64_t pad = pad_first ? ns - k : 0;
-  for (int64_t a = threadIdx.x; a < ns; a += 256) {
-    const bool real = sys_real(a, pad, k);
-    const int64_t p = real ? snp_col(idx[o0 + a - pad], P) : 0;
-    u[b * ns + a] = real ? (double)csT[p] : 0.0;
-    for (int t = 0; t < nt; ++t) rhs[(b * nt + t) * ns + a] = real ? xty[t * P + p] * invd : 0.0;
-  }
+__global__ __launch_bounds__(STATS_THREADS) void k_indiv_stats(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
+                                                               FoldTab ft, const int32_t* __restrict__ csA, int64_t n, int64_t nT, int64_t nTp, int64_t P, int form,
+                                                               int64_t ns, int pad_first, int nt, int branch, double h2,
+                                                               double* __restrict__ scal, double* __restrict__ u,
+                                                               double* __restrict__ rhs, int32_t* __restrict__ err) {
+  __shared__ StatsShared sh;
+  stats_wg(idx, off, ft, csA, n, nT, nTp, P, form, ns, pad_first, nt, branch, h2, blockIdx.x, scal, u, rhs, err, sh, 0,
+           ns);
 }
 
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const FoldTab& ft,
                               const int32_t* colsum_all, const EvalDims& d, const SysDims& sd,
                               int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
                               hipStream_t s) {
-  hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(256), 0, s, idx, off, ft, colsum_all, d.n,
+  hipLaunchKernelGGL(k_indiv_stats, dim3((unsigned)B), dim3(STATS_THREADS), 0, s, idx, off, ft, colsum_all, d.n,
                      d.nT, d.nTp, d.P, sd.form, sd.ns, sd.pad_first, d.nt, branch, h2, scal, u, rhs, err);
   return hipGetLastError();
 }

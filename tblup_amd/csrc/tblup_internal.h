@@ -175,6 +175,19 @@ hipError_t launch_grm(const int8_t* panel, int64_t panel_stride, const int64_t* 
                       const double* scal, const EvalDims& d, int64_t B, double* K, hipStream_t s);
 
 // ---- launchers (k_chol.hip, k_solve.hip) ----
+// SNP form with k_sys_tiles_st (which reads no scalar): k_indiv_stats' inputs and outputs, when the
+// scalars are formed in the launch after the system tiles (k_stats_diag_counts, fused with the
+// K_JJ + lambda I epilogue of the tiles J < 2) instead of in a launch of their own before them
+struct StatsFuse {
+  const int32_t* csA;    // allele counts over all n animals (gblup p)
+  int64_t n, nT;
+  int branch;
+  double h2;
+  int32_t* err;          // the context's index-error status word
+  double* scal;          // [B][SCAL]
+  double* u;             // [B][ns]
+  double* rhs;           // [B][nt][ns]
+};
 struct CholLaunch {
   EvalDims d;
   SysDims sd;
@@ -206,6 +219,7 @@ struct CholLaunch {
                          // [B][NT][36 packed lower blocks][64 lanes][4] (KD_TILE int16 per tile); the
                          // consumers form K_JJ + lambda I from them (kd_block, k_chol.hip)
   int sys_st = -1;       // k_sys_tiles_st: -1 auto, 0 never, 1 whenever it applies (TBLUP_SYS_ST)
+  const StatsFuse* stats = nullptr;   // launch_sys_tiles: form the scalars after k_sys_tiles_st
 };
 // k_sys_tiles output: per individual NT(NT-1)/2 off-diagonal tiles (I > J, t = I(I-1)/2 + J) of
 // 128 x 128 int16 counts, in the order the off-diagonal kernel's lanes read them:
@@ -219,7 +233,7 @@ constexpr int WGT_REC = 4;
 // a diagonal launch's records are followed by DTR_RECS records holding the phase stamps of
 // its workgroup 0 (8 waves x 64 uint64), written as kind-0 records
 constexpr int DTR_RECS = 8 * 64 / WGT_REC;
-enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_PART = 6, WGT_DPREP = 9 };   // 7 / 8: the chained solve (k_solve.hip)
+enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_PART = 6, WGT_DPREP = 9, WGT_EPART = 10 };   // 7 / 8: the chained solve (k_solve.hip)
 // Work units of the off-diagonal launch of column J, per individual (k_chol.hip):
 //   nI  T-units: tiles (I, J), I > J
 //   nP  x nrs P-units (ahead schedule): partial sums K - sum_{L<J} of tiles (I, J+1), I >= J+2, in
@@ -228,10 +242,16 @@ enum { WGT_DIAG = 1, WGT_TILE = 2, WGT_PREP = 3, WGT_KJJ = 4, WGT_SYS = 5, WGT_P
 //   n_kd K_JJ workgroups (column 0 of the kernel form only)
 //   ndd: the D-units run in the DIAGONAL launch J instead (whole, one per individual; nds = 0), on
 //   the CUs its B workgroups leave idle -- they need only the columns L < J, complete before it
+//   ne  E-units, also in the DIAGONAL launch J (after its D-units), one per CU still idle: the GEMM1
+//       term L = Ls0 (Ls0 = J-1 after an ahead launch, else 0) of column J's tiles e < ne in
+//       I-major order (tile (J+1 + e / B, J) of individual e % B), into the partial-sum slot J&1;
+//       such a tile's T-unit starts from that partial and sums from Ls0 + 1 (its MFMA chains
+//       unchanged: bit-identical)
 struct OffPlan {
   int nI, nP, nrs, nds, ahead_cur;
   int ndd;
   int64_t n_kd;
+  int64_t ne;
   __host__ __device__ int64_t units() const { return (int64_t)nP * nrs + nds + nI; }
 };
 // Schedule policy (host, per chunk: a function of B and the system shape only, so the results
@@ -251,8 +271,13 @@ constexpr int64_t DD_MAX_B = 128;
 #define TBLUP_AB_DD_MAX_J 3
 #endif
 constexpr int DD_MAX_J = TBLUP_AB_DD_MAX_J;
+// diag_e: E-units in the diagonal launch, -1 auto (one per CU the launch's other workgroups leave
+// idle, ncu - B (1 + ndd), when that covers every tile of the column or is >= 2B; so none at
+// B >= ncu), 0 never, 1 every tile of the column (tests), 2 only columns covered whole
 OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs, int64_t slots = AHEAD_SLOTS,
-                 int diag_d = 0, int dd_maxj = DD_MAX_J);
+                 int diag_d = 0, int dd_maxj = DD_MAX_J, int diag_e = 0, int64_t ncu = 0);
+// multiprocessor count of the current device (256 when the query fails)
+int cu_count();
 inline int64_t offdiag_grid(const OffPlan& p, int64_t B) { return p.nI > 0 ? B * p.units() + p.n_kd : 0; }
 // Fused GRM + tile Cholesky, column by column (k_chol.hip): diagonal tile J (k_chol_diag),
 // then the off-diagonal tiles (I > J, J) plus the preparation of diagonal tile J+1.

@@ -4,11 +4,12 @@ target's in 1 / 2 block slices) redistribute the same MFMA chains over workgroup
 the two solve kernels (k_solve: one workgroup per individual; k_solve_chain: an individual's
 block rows and tiles over the chip, chosen for small batches) share one arithmetic, and the
 diagonal tile's last SYRK term runs the same MFMA chains whether the diagonal launch or the
-previous launch's tile (J, J-1) workgroup computes it, and the diagonal
-target's partial sum runs in the off-diagonal launch or beside the diagonal one, so fitness
+previous launch's tile (J, J-1) workgroup computes it, the diagonal target's partial sum runs in
+the off-diagonal launch or beside the diagonal one, and a tile's GEMM1 term L = Ls0 runs in its
+T-unit or in an E-unit beside the diagonal launch, so fitness
 and EBVs must be bit-identical under every setting, for both system forms and for system sizes
 from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS / TBLUP_SOLVE_CHAIN /
-TBLUP_LAST_TERM / TBLUP_PAD_FIRST / TBLUP_DIAG_D are read when a context is created.)"""
+TBLUP_LAST_TERM / TBLUP_PAD_FIRST / TBLUP_DIAG_D / TBLUP_DIAG_E are read when a context is created.)"""
 import os
 
 import numpy as np
@@ -31,6 +32,9 @@ SETTINGS = [
     {"TBLUP_LAST_TERM": "0"},                       # ... in the diagonal launch
     {"TBLUP_DIAG_D": "1"},                          # diagonal-target partials in the diagonal launches
     {"TBLUP_DIAG_D": "0"},                          # ... in the off-diagonal launches
+    {"TBLUP_DIAG_E": "1"},                          # a GEMM1 term of every tile in the diagonal launch
+    {"TBLUP_DIAG_E": "0"},                          # ... of none
+    {"TBLUP_AHEAD": "0", "TBLUP_DIAG_E": "1"},      # ... from K (term L = 0) at every column
 ]
 
 

@@ -7,7 +7,8 @@ chained solve's failure mode.
 * Config 3's per-GPU shard at N = 8 (B = 128 at the config-2 shape) and N = 32 shards (B = 32):
   every automatic small-batch policy at once (ahead P-units with makespan slicing, D-units beside
   the diagonal, last-term mode at B <= 64, the chained solve) -- oracle samples and bit identity
-  with every policy off (TBLUP_AHEAD=0 TBLUP_SOLVE_CHAIN=0 TBLUP_DIAG_D=0 TBLUP_LAST_TERM=0).
+  with every policy off (TBLUP_AHEAD=0 TBLUP_SOLVE_CHAIN=0 TBLUP_DIAG_D=0 TBLUP_LAST_TERM=0
+  TBLUP_DIAG_E=0).
 * A chained-solve hand-off wait that expires is recovered by the host entries (the chunk's factor
   re-solved through k_solve, same bits) or raises the device status word, which the drop-in
   evaluator's speculative path answers by re-evaluating through the host entry -- never a silent
@@ -26,7 +27,8 @@ pytestmark = pytest.mark.gpu
 
 EBV_RTOL = 1e-9
 FIT_ATOL = 1e-9
-KNOBS_OFF = {"TBLUP_AHEAD": "0", "TBLUP_SOLVE_CHAIN": "0", "TBLUP_DIAG_D": "0", "TBLUP_LAST_TERM": "0"}
+KNOBS_OFF = {"TBLUP_AHEAD": "0", "TBLUP_SOLVE_CHAIN": "0", "TBLUP_DIAG_D": "0", "TBLUP_LAST_TERM": "0",
+             "TBLUP_DIAG_E": "0"}
 
 
 def _relmax(a, b):

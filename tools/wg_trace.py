@@ -17,7 +17,7 @@ os.environ["TBLUP_WG_TRACE"] = "1"
 
 import bench  # noqa: E402
 
-KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part", 9: "dprep"}   # (7 / 8: chained solve, tools/solve_trace.py)
+KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part", 9: "dprep", 10: "epart"}   # (7 / 8: chained solve, tools/solve_trace.py)
 
 
 def main():
@@ -38,7 +38,7 @@ def main():
     torch.cuda.synchronize()
     rec = eng.wg_trace()
     raw = eng.wg_trace(raw=True)
-    rec = rec[(rec["kind"] <= 6) | (rec["kind"] == 9)]
+    rec = rec[(rec["kind"] <= 6) | (rec["kind"] >= 9)]
     np.save(out, rec)
     np.save(out.replace(".npy", "_raw.npy"), raw)
     props = torch.cuda.get_device_properties(0)
@@ -53,7 +53,7 @@ def main():
         launches.append((rec[sysm]["start"].min(), -1, False, sysm))
     for J in sorted(set(rec["J"].tolist())):
         for is_diag in (True, False):
-            m = (rec["J"] == J) & (((rec["kind"] == 1) | (rec["kind"] == 9)) == is_diag) & ~sysm
+            m = (rec["J"] == J) & (np.isin(rec["kind"], (1, 9, 10)) == is_diag) & ~sysm
             if not m.any():
                 continue
             launches.append((rec[m]["start"].min(), J, is_diag, m))
@@ -82,7 +82,7 @@ def main():
               f"gap {gap * 1e6:5.1f} util {util:.2f}{first_tile} | " + "; ".join(parts))
     print(f"sum of launch spans {tot * 1e6:.1f} us, first start to last end {(prev_end - t0) * 1e6:.1f} us")
     # phase stamps of diagonal workgroup 0 (tblup_internal.h DTR_RECS): per wave, 30 slots.  They
-    # follow the diagonal launch's own records (B x (1 + D-units beside it)), so locate them from
+    # follow the diagonal launch's own records (B x (1 + D-units beside it) + E-units), so locate them from
     # the last diagonal record of launch J (the units per launch depend on the schedule policy)
     NT = 8
     names = ["start", "pre-barrier", "post-barrier"] + [f"{x}{p}" for p in range(8) for x in ("a", "b", "w")] + [
@@ -92,7 +92,7 @@ def main():
     rkind = (raw[:, 2] >> np.uint64(56)).astype(np.int64)
     rJ = (raw[:, 3] & np.uint64(0xFFFF)).astype(np.int64)
     for J in range(NT):
-        diag_rows = np.nonzero(((rkind == 1) | (rkind == 9)) & (rJ == J))[0]
+        diag_rows = np.nonzero(np.isin(rkind, (1, 9, 10)) & (rJ == J))[0]
         if not len(diag_rows):
             continue
         pos = int(diag_rows.max()) + 1
