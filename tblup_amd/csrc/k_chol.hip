@@ -2135,11 +2135,8 @@ __global__ __launch_bounds__(64 * STW) void k_stats_diag_counts(CholArgs a, Stat
       cnt[m][n] = v4f{(float)(int16_t)(p.x & 0xffff), (float)(int16_t)(p.x >> 16), (float)(int16_t)(p.y & 0xffff),
                       (float)(int16_t)(p.y >> 16)};
     }
-  // the u / rhs rows split between the individual's two workgroups
-  const int64_t half = (a.ns / 2 + 63) & ~(int64_t)63;
-  stats_wg(a.idx, a.off, a.ft, x.csA, x.n, x.nT, a.ytp, a.P, a.form, a.ns, a.padfirst, a.nt, x.branch, x.h2, b,
-           J == 0 ? x.scal : nullptr, x.u, x.rhs, x.err, sh, J == 0 ? 0 : half, J == 0 ? half : a.ns);
-  // u_a = s_a of tile J's rows (stats_wg's u, from the same loads)
+  // u_a = s_a of tile J's rows (stats_wg's u values, gathered here before its reduction so that
+  // these loads overlap it)
   if (t < TILE) {
     const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
     const int64_t pad = a.padfirst ? a.ns - k : 0;
@@ -2147,9 +2144,15 @@ __global__ __launch_bounds__(64 * STW) void k_stats_diag_counts(CholArgs a, Stat
     const int32_t* csT = a.ft.csT[fold_of(a.ft, b)];
     u_sh[t] = (r < a.ns && sys_real(r, pad, k)) ? (double)csT[snp_col(a.idx[o0 + r - pad], a.P)] : 0.0;
   }
-  __syncthreads();
-  if (!tile) return;
-  sys_diag_epilogue_src(a, cnt, b, J, qr, qc, l, sh.sc, u_sh);
+  // (stats_wg's barriers also publish u_sh)
+  stats_wg(a.idx, a.off, a.ft, x.csA, x.n, x.nT, a.ytp, a.P, a.form, a.ns, a.padfirst, a.nt, x.branch, x.h2, b,
+           J == 0 ? x.scal : nullptr, x.err, sh);
+  if (tile) sys_diag_epilogue_src(a, cnt, b, J, qr, qc, l, sh.sc, u_sh);
+  // then the u / rhs rows, split between the individual's two workgroups (their stores overlap the
+  // epilogue's)
+  const int64_t half = (a.ns / 2 + 63) & ~(int64_t)63;
+  stats_rows(a.idx, a.off, a.ft, a.P, a.ns, a.padfirst, a.nt, b, x.u, x.rhs, sh, J == 0 ? 0 : half,
+             J == 0 ? half : a.ns);
 }
 
 static CholArgs make_args(const CholLaunch& c, int J) {

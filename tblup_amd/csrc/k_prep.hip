@@ -164,8 +164,8 @@ __global__ __launch_bounds__(STATS_THREADS) void k_indiv_stats(const int64_t* __
                                                                double* __restrict__ scal, double* __restrict__ u,
                                                                double* __restrict__ rhs, int32_t* __restrict__ err) {
   __shared__ StatsShared sh;
-  stats_wg(idx, off, ft, csA, n, nT, nTp, P, form, ns, pad_first, nt, branch, h2, blockIdx.x, scal, u, rhs, err, sh, 0,
-           ns);
+  stats_wg(idx, off, ft, csA, n, nT, nTp, P, form, ns, pad_first, nt, branch, h2, blockIdx.x, scal, err, sh);
+  if (form == FORM_PRIMAL) stats_rows(idx, off, ft, P, ns, pad_first, nt, blockIdx.x, u, rhs, sh, 0, ns);
 }
 
 hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B, const FoldTab& ft,

@@ -14,24 +14,21 @@ constexpr int STATS_THREADS = 256;
 
 // LDS of stats_wg
 struct StatsShared {
-  int64_t r1[STATS_THREADS], r2[STATS_THREADS];
+  int64_t r1[STATS_THREADS / 64], r2[STATS_THREADS / 64];   // per-wave partial sums
   double sc[SCAL];
 };
 
 // Individual (system) b: branch, 1/N, q/N^2, 1/d, mu flag, lambda ... into sh.sc (every thread reads
-// them after the call) and, scal != null, into scal[b]; rhs != null (primal form): u[b][a] = s_a and
-// rhs[b][t][a] = xty[t][p_a] / d over the system rows a0 <= a < a1 (zero on padding rows).  An index
-// outside [-P, P) sets *err (vector store; every writer stores 1) and SC_BAD.
+// them after the call) and, scal != null, into scal[b].  An index outside [-P, P) sets *err (vector
+// store; every writer stores 1) and SC_BAD.
 __device__ __forceinline__ void stats_wg(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
                                          const FoldTab& ft, const int32_t* __restrict__ csA, int64_t n, int64_t nT,
                                          int64_t nTp, int64_t P, int form, int64_t ns, int pad_first, int nt,
                                          int branch, double h2, int64_t b, double* __restrict__ scal,
-                                         double* __restrict__ u, double* __restrict__ rhs, int32_t* __restrict__ err,
-                                         StatsShared& sh, int64_t a0, int64_t a1) {
+                                         int32_t* __restrict__ err, StatsShared& sh) {
   const int t = threadIdx.x;
   const int64_t o0 = off[b], k = off[b + 1] - o0;
   const int32_t* __restrict__ csT = ft.csT[fold_of(ft, b)];   // the system's split
-  const double* __restrict__ xty = ft.xty[fold_of(ft, b)];
   int mode = branch;
   if (mode == 0) mode = (k > n) ? 1 : 2;  // evaluator.py:257
   const int32_t* cs = (mode == 1) ? csA : csT;
@@ -45,20 +42,26 @@ __device__ __forceinline__ void stats_wg(const int64_t* __restrict__ idx, const 
     m1 += m;
     q += m * m;
   }
-  sh.r1[t] = m1;
-  sh.r2[t] = q;
+  // exact integer sums: wave shuffles, then the four waves' partials through LDS
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m1 += __shfl_xor(m1, o);
+    q += __shfl_xor(q, o);
+  }
+  if ((t & 63) == 0) {
+    sh.r1[t >> 6] = m1;
+    sh.r2[t >> 6] = q;
+  }
   const int any_bad = __syncthreads_or(bad);
   if (any_bad && t == 0) *err = 1;
-  for (int st = STATS_THREADS / 2; st > 0; st >>= 1) {
-    if (t < st) {
-      sh.r1[t] += sh.r1[t + st];
-      sh.r2[t] += sh.r2[t + st];
-    }
-    __syncthreads();
-  }
   if (t == 0) {
+    int64_t s1 = 0, s2 = 0;
+    for (int w = 0; w < STATS_THREADS / 64; ++w) {
+      s1 += sh.r1[w];
+      s2 += sh.r2[w];
+    }
     const double N = (mode == 1) ? (double)n : (double)nT;
-    const double M1 = (double)sh.r1[0], Q = (double)sh.r2[0];
+    const double M1 = (double)s1, Q = (double)s2;
     const double d = M1 / N - Q / (2.0 * N * N);  // 2 sum p(1-p)
     double* sc = sh.sc;
     // primal (SNP-space) form: C_ab = (X^T X)_ab - s_a s_b / n_T over train rows
@@ -79,7 +82,18 @@ __device__ __forceinline__ void stats_wg(const int64_t* __restrict__ idx, const 
   }
   __syncthreads();
   if (scal && t < SCAL && t <= SC_PAD) scal[b * SCAL + t] = sh.sc[t];
-  if (!primal || rhs == nullptr) return;
+}
+
+// Primal form, after stats_wg: u[b][a] = s_a and rhs[b][t][a] = xty[t][p_a] / d over the system rows
+// a0 <= a < a1 (zero on padding rows)
+__device__ __forceinline__ void stats_rows(const int64_t* __restrict__ idx, const int64_t* __restrict__ off,
+                                           const FoldTab& ft, int64_t P, int64_t ns, int pad_first, int nt,
+                                           int64_t b, double* __restrict__ u, double* __restrict__ rhs,
+                                           const StatsShared& sh, int64_t a0, int64_t a1) {
+  const int t = threadIdx.x;
+  const int64_t o0 = off[b], k = off[b + 1] - o0;
+  const int32_t* __restrict__ csT = ft.csT[fold_of(ft, b)];
+  const double* __restrict__ xty = ft.xty[fold_of(ft, b)];
   // u_a = s_a (train allele count), rhs_ta = X_c^T (y_T,t - mu_t) / d = xty[t][p_a] / d
   // (the sklearn primal right-hand side in 1/d units); zero on padding rows (system row a holds
   // selected SNP a - pad)
