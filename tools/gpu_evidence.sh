@@ -11,6 +11,9 @@ if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/gputest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/gputest_$TAG.log; tail -3 $O/gputest_$TAG.log; [ $rc -eq 0 ] || exit 1
 fi
+# PART=a: everything but the generation / IntraGCV / knockout / timeline runs; PART=b (with
+# SKIP_TESTS=1): only those -- two GPU calls under one tag when one would run too long
+if [ "$PART" != "b" ]; then
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmcf_$TAG -o pmc --output-format csv -- $B > $O/pmcf_$TAG.log 2>&1 || { echo "pmc fetch failed"; tail -5 $O/pmcf_$TAG.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmcw_$TAG -o pmc --output-format csv -- $B > $O/pmcw_$TAG.log 2>&1 || { echo "pmc write failed"; tail -5 $O/pmcw_$TAG.log; exit 1; }
@@ -24,6 +27,8 @@ python3 tools/pmc_mfma.py $M --out $O/pmc_mfma_$TAG.json || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o trace --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --pmc-json $O/pmc_traffic_$TAG.json --pmc-mfma-json $O/pmc_mfma_$TAG.json > $O/prof_bench_$TAG.log 2>&1 || { echo "kernel-trace failed"; tail -20 $O/prof_bench_$TAG.log; exit 1; }
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --pmc-json $O/pmc_traffic_$TAG.json --pmc-mfma-json $O/pmc_mfma_$TAG.json > $O/bench_$TAG.log 2> $O/bench_$TAG.err || { tail -20 $O/bench_$TAG.err; exit 1; }
 tail -1 $O/bench_$TAG.log | cut -c1-300
+fi
+if [ "$PART" != "a" ]; then
 timeout -k 10 300 python tools/generation_bench.py 24 > $O/generation_$TAG.log 2>&1 || { tail -20 $O/generation_$TAG.log; exit 1; }
 tail -1 $O/generation_$TAG.log
 # the multi-rank generation path on this one GPU (gloo): 2 and 4 ranks, config 2 and config 3 populations
@@ -38,6 +43,8 @@ timeout -k 10 300 python tools/knockout_bench.py > $O/knockout_$TAG.log 2>&1 || 
 tail -1 $O/knockout_$TAG.log
 timeout -k 10 200 python tools/wg_trace.py $O/wg_trace_$TAG.npy > $O/wg_trace_$TAG.txt 2>&1 || { tail -20 $O/wg_trace_$TAG.txt; exit 1; }
 timeout -k 10 200 python tools/wg_trace.py $O/wg_trace128_$TAG.npy --pop 128 > $O/wg_trace128_$TAG.txt 2>&1 || { tail -20 $O/wg_trace128_$TAG.txt; exit 1; }
+fi
+[ "$PART" = "b" ] && { echo "evidence part b done"; exit 0; }
 timeout -k 10 400 python bench.py --config config4 --steps 5 --warmup 2 > $O/bench_config4_$TAG.log 2> $O/bench_config4_$TAG.err || { tail -20 $O/bench_config4_$TAG.err; exit 1; }
 timeout -k 10 300 python bench.py --config config5 --steps 20 --warmup 5 > $O/bench_config5_$TAG.log 2> $O/bench_config5_$TAG.err || { tail -20 $O/bench_config5_$TAG.err; exit 1; }
 for P in 32 64 128; do
