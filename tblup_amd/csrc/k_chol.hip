@@ -1638,6 +1638,15 @@ __device__ void sys_diag_epilogue(const CholArgs& a, const v4f (&cnt)[4][4], int
 // a diagonal tile's counts as int16 (diag): its 36 lower blocks (cb >= ib) only, packed block
 // e = cb (cb + 1) / 2 + ib, lane order of the f64 C layout (kd_load / kd_block read them); an
 // off-diagonal tile's: store_counts16's layout
+// The super-tile kernel's counted ring waits (k_sys_tiles_st) leave the VMEM ops younger than the
+// stage they wait for outstanding: ST_STAGE_OPS LDS-DMA loads per lane for each later stage (issue():
+// two rows x A and B) and, after a unit of two off-diagonal tiles, this function's stores -- one 8-B
+// store per 16 x 16 block of the wave's 4 x 4 quadrant (all 16 off the diagonal: addresses 512 B
+// apart within a lane, never merged).  A count above the real number only waits for more.
+constexpr int ST_STAGE_OPS = 4;
+constexpr int ST_TILE_STORES = 4 * 4;
+constexpr int ST_UNIT_STORES = 2 * ST_TILE_STORES;
+static_assert(2 * ST_STAGE_OPS + ST_UNIT_STORES < 64, "vmcnt holds 6 bits");
 __device__ __forceinline__ void store_counts16_any(int16_t* kt, const v4f (&cnt)[4][4], int qr, int qc, int l,
                                                    bool diag) {
 #pragma unroll
@@ -1881,14 +1890,14 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
     const int ahead = min(D - 2, nstages - 1 - g);   // stages issued after stage g
     if (ahead >= 2) {
       if (stored_full)
-        asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * ST_STAGE_OPS + ST_UNIT_STORES) : "memory");
       else
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * ST_STAGE_OPS) : "memory");
     } else if (ahead == 1) {
       if (stored_full)
-        asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(ST_STAGE_OPS + ST_UNIT_STORES) : "memory");
       else
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(ST_STAGE_OPS) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
