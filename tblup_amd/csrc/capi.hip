@@ -186,16 +186,16 @@ OffPlan tblup::off_plan(int64_t B, int NT, int J, bool st, int ahead, int nrs_po
   }
   // E-units: column J's GEMM1 term L = Ls0 of its first tiles, on the CUs the diagonal launch J
   // leaves idle (its B diagonal workgroups and D-units take one CU each: 144 KiB of LDS).  One term
-  // (29 us alone on a CU, measured) ends inside the ~45 us diagonal launch.  Auto: every idle CU
-  // when the column's tiles all get one or the idle CUs are >= 2B; else none -- an off-diagonal
-  // launch of one round is as long as its longest units, so shortening a third of the tiles gains
-  // nothing while the E-units' loads slow the diagonal launch (A/B, profiles/r05_epol_ab.txt: pop 32
-  // +8.5%, 64 +2.6% with partial columns vs +0.8% without, 96 / 160 partial columns -0.5 / -1%).
-  // 2: only columns whose every tile gets one.
-  if (J >= 1 && (diag_e == 1 || ((diag_e < 0 || diag_e == 2) && ncu > 0))) {
+  // (29 us alone on a CU, measured) ends inside the ~45 us diagonal launch.  Auto: one per idle CU.
+  // The off-diagonal launch dispatches the tiles they started last, so that (the dispatcher filling
+  // every CU's first slot, then its second) a CU pairs a whole tile with a shortened one or with a
+  // lighter unit class -- an off-diagonal launch of one round lasts as long as its busiest CU.  (In
+  // the tiles' plain order, columns covered only in part gained nothing: A/B, profiles/r05_epol_ab.txt,
+  // r05_eord_ab.txt -- with the order pop 96 +1.9%, 160 +0.3%, 128 +0.2%.)  2: only whole columns.
+  if (J >= 1 && (diag_e == 1 || (diag_e != 0 && ncu > 0))) {
     const int64_t idle = std::max<int64_t>(0, ncu - B * (1 + p.ndd));
     p.ne = diag_e == 1 ? B * p.nI : std::min<int64_t>(B * p.nI, idle);
-    if (p.ne < B * p.nI && (diag_e == 2 || idle < 2 * B)) p.ne = 0;
+    if (diag_e == 2 && p.ne < B * p.nI) p.ne = 0;
   }
   p.nrs = 1;
   p.nds = dt;

@@ -1555,6 +1555,14 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
         b = lg / (p.nI - 1);
         I = a.J + 2 + (int)(lg % (p.nI - 1));
       }
+    } else if (p.ne > 0 && p.ne < n_t) {
+      // some tiles started by E-units: the others first, those last (with the dispatcher's
+      // round-robin a CU then pairs a whole tile with a shortened one or with a lighter class),
+      // each class in the E-units' own order (tile e, I-major: its E-unit's XCD)
+      const int64_t nne = n_t - p.ne;
+      const int64_t e = bid < nne ? p.ne + xcd_remap(bid, nne) : xcd_remap(bid - nne, p.ne);
+      b = e % a.B;
+      I = a.J + 1 + (int)(e / a.B);
     } else {
       const int64_t lg = xcd_remap(bid, n_t);
       b = lg / p.nI;

@@ -272,8 +272,8 @@ constexpr int64_t DD_MAX_B = 128;
 #endif
 constexpr int DD_MAX_J = TBLUP_AB_DD_MAX_J;
 // diag_e: E-units in the diagonal launch, -1 auto (one per CU the launch's other workgroups leave
-// idle, ncu - B (1 + ndd), when that covers every tile of the column or is >= 2B; so none at
-// B >= ncu), 0 never, 1 every tile of the column (tests), 2 only columns covered whole
+// idle, ncu - B (1 + ndd), up to the column's tiles; so none at B >= ncu), 0 never, 1 every tile of
+// the column (tests), 2 only columns covered whole
 OffPlan off_plan(int64_t B, int NT, int J, bool sys_tiles, int ahead, int nrs, int64_t slots = AHEAD_SLOTS,
                  int diag_d = 0, int dd_maxj = DD_MAX_J, int diag_e = 0, int64_t ncu = 0);
 // multiprocessor count of the current device (256 when the query fails)
