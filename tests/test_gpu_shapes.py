@@ -92,10 +92,11 @@ def test_config5_pop256_primal_multitrait_solve(panel):
     np.testing.assert_array_equal(chained[1], ebv)
 
 
-@pytest.mark.parametrize("B", [128, 32])
+@pytest.mark.parametrize("B", [128, 32, 96, 160])
 def test_config3_shard_auto_policies(panel, B):
     """B individuals in one batch with every automatic schedule policy at once, against the
-    oracle and against every policy switched off, bit for bit."""
+    oracle and against every policy switched off, bit for bit.  (96 / 160: E-units covering
+    columns in part, their tiles dispatched last; 128: in part and whole; 32: whole.)"""
     p = panel
     genomes = p["genomes"][:B]
     fit, ebv = _run(p, genomes)
