@@ -197,11 +197,15 @@ class GpuDEStep:
             GpuDEStep._instances.pop(self.device, None)
 
 
+_F64 = np.dtype(np.float64)
+
+
 def _child_dtypes(genomes, donors, strategy, mi, clip):
     """Per-child dtype numpy gives the reference: np.where(mask, mutant, target) (+ np.clip);
     None when every child is float64 (the usual RandomKey case)."""
-    dts = [np.asarray(g).dtype for g in genomes]
-    if all(dt == np.float64 for dt in dts):
+    dts = [g.dtype if isinstance(g, np.ndarray) else np.asarray(g).dtype for g in genomes]
+    f64 = _F64
+    if all(dt is f64 or dt == f64 for dt in dts):
         return None
     out = []
     e = np.zeros(0, dtype=bool)
@@ -426,12 +430,19 @@ def _copy_individual(indv):
         indv._genome = g
 
 
-def _common_length(population):
-    n = len(population)
-    L = len(population[0].get_internal_genome()) if n else 0
-    if any(len(population[i].get_internal_genome()) != L for i in range(n)):
+def _members(population):
+    """The population's individuals and their internal genomes, one pass, and the common genome
+    length (DE needs one: numpy broadcasting in evolver.py:132)."""
+    inds = [population[i] for i in range(len(population))]
+    genomes = [x.get_internal_genome() for x in inds]
+    L = len(genomes[0]) if genomes else 0
+    if any(len(g) != L for g in genomes):
         raise ValueError("DE needs internal genomes of one length (numpy broadcasting in evolver.py:132)")
-    return L
+    return inds, genomes, L
+
+
+def _common_length(population):
+    return _members(population)[2]
 
 
 class Evolver(abc.ABC):
@@ -462,24 +473,22 @@ class _GpuDEEvolver(Evolver):
         import time
         t = time.perf_counter()
         mi = 5 if population.generation % 5 == 0 else self.mutation_intensity
-        L = _common_length(population)
-        donors, fixed = self._donors(population, L)
+        members = _members(population)
+        donors, fixed = self._donors(population, members[2])
         return self._gpu_generation(population, t, donors, fixed, self.strategy, mi, self.crossover_rate,
-                                    self._clip())
+                                    self._clip(), members)
 
-    def _gpu_generation(self, population, t, donors, fixed, strategy, mi, cr, clip):
+    def _gpu_generation(self, population, t, donors, fixed, strategy, mi, cr, clip, members=None):
         """The children of one generation (donors / fixed: the python-`random` draws already made;
-        strategy, mi, cr: scalars or one per individual) through the GPU DE step."""
-        n = len(population)
+        strategy, mi, cr: scalars or one per individual; members: _members(population) when the
+        caller has it) through the GPU DE step."""
         import torch
-        genomes = [population[i].get_internal_genome() for i in range(n)]
-        L = len(genomes[0])
+        inds, genomes, L = members if members is not None else _members(population)
+        n = len(inds)
         dtypes = _child_dtypes(genomes, donors, strategy, mi, clip)
         t = _mark(t, "ev_donors")
         step = GpuDEStep.get(self.device)
-        import torch
         store = DeviceKeyStore.get(step.device)
-        inds = [population[i] for i in range(n)]
         with torch.cuda.device(step.device), torch.cuda.stream(work_stream(step.device)):
             parents = store.gather(inds, L, host_rows=lambda i: genomes[i],
                                    copy_rows=step.gather_rows)   # device-resident parents
@@ -789,7 +798,8 @@ class SaDE(AdaptiveEvolver, _GpuDEEvolver):
         self.recalculate_p(population)
         f = self.generate_f()
         n = len(population)
-        L = _common_length(population)
+        members = _members(population)
+        L = members[2]
         best = max(population, key=lambda indv: indv.fitness)
         best_index = population.population.index(best)
         strategies = np.empty(n, dtype=np.int32)
@@ -809,7 +819,7 @@ class SaDE(AdaptiveEvolver, _GpuDEEvolver):
                 donors[i] = (best_index, a, exclusive_randrange(0, n, [i, best_index, a]))
             fixed[i] = random.randrange(0, L)   # the crossover's forced position (evolver.py:76)
         crs = np.array([float(c) for c in self.crs[:n]], dtype=np.float64)
-        return self._gpu_generation(population, t, donors, fixed, strategies, f, crs, self.clip)
+        return self._gpu_generation(population, t, donors, fixed, strategies, f, crs, self.clip, members)
 
 
 class MDE_pBX(AdaptiveEvolver):

@@ -244,7 +244,7 @@ def test_sade_host_side_matches_reference(name, tmp_path, monkeypatch):
     from copy import deepcopy
     from tblup_amd import evolver as EV
 
-    def host_generation(self, population, t, donors, fixed, strategy, mi, cr, clip):
+    def host_generation(self, population, t, donors, fixed, strategy, mi, cr, clip, members=None):
         genomes = [population[i].get_internal_genome() for i in range(len(population))]
         kids = D.de_children(genomes, strategy, donors, fixed, mi, cr, clip, self.dimensionality - 1)
         out = []
