@@ -185,9 +185,9 @@ class GpuDEStep:
         """out[i] = the device row at address ptrs[i] (this device), on torch's current stream."""
         import torch
         n, L = out.shape
-        tab = (ctypes.c_void_p * n)(*ptrs)
+        tab = np.array(ptrs, dtype=np.uint64)   # host array of n device addresses (one C conversion)
         _native.check("tblup_gather_rows", self._lib.tblup_gather_rows(
-            self._ctx, ctypes.c_void_p(out.data_ptr()), n, L, out.stride(0), tab,
+            self._ctx, ctypes.c_void_p(out.data_ptr()), n, L, out.stride(0), ctypes.c_void_p(tab.ctypes.data),
             ctypes.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)))
 
     def close(self):

@@ -258,8 +258,22 @@ class DeviceKeyStore:
             self._entries[indv.uid] = (e[0], e[1], weakref.ref(new), e[3])
 
     def rows(self, individuals):
-        """(tensor, row) per individual (None where absent)."""
-        return [self.lookup(i) for i in individuals]
+        """(tensor, row) per individual (None where absent): lookup() inlined over the batch."""
+        ent = self._entries
+        out = []
+        for indv in individuals:
+            e = ent.get(indv.uid)
+            if e is not None:
+                tensor, row, ref, length = e
+                g = ref()
+                k = getattr(indv, "_genome", None)
+                if (g is not None and g is k and isinstance(k, np.ndarray) and not g._stale
+                        and getattr(indv, "length", None) == length):
+                    out.append((tensor, row))
+                    continue
+                del ent[indv.uid]
+            out.append(None)
+        return out
 
     def gather(self, individuals, L, host_rows=None, copy_rows=None):
         """A contiguous (len(individuals) x L) float64 device tensor of their internal genomes;
@@ -276,29 +290,37 @@ class DeviceKeyStore:
         if host_rows is None and any(h is None for h in hits):
             return None
         out = torch.empty((n, L), dtype=torch.float64, device="cuda:%d" % self.device)
-        # (base address, row pitch in bytes) per distinct device tensor, None if not a plain
-        # row-major (., L) float64 matrix: torch's accessors once per tensor, not per row
-        geo = {}
-        for h in hits:
-            if h is not None and id(h[0]) not in geo:
-                t = h[0]
-                geo[id(t)] = ((t.data_ptr(), 8 * t.stride(0))
-                              if t.dim() == 2 and t.shape[1] == L and t.stride(1) == 1 else None)
-        if copy_rows is not None and all(g is not None for g in geo.values()):
-            ptrs = []
-            for h in hits:
+        # every row's device address in one pass: (base address, row pitch in bytes) per distinct
+        # device tensor (torch's accessors once per tensor, not per row), None if that tensor is not
+        # a plain row-major (., L) float64 matrix
+        if copy_rows is not None:
+            geo = {}
+            ptrs = [0] * n
+            missing = []
+            plain = True
+            for i, h in enumerate(hits):
                 if h is None:
-                    ptrs.append(0)
-                else:
-                    base, pitch = geo[id(h[0])]
-                    ptrs.append(base + pitch * h[1])
-            missing = [i for i, q in enumerate(ptrs) if not q]
-            if len(missing) < n:
-                any_row = next(q for q in ptrs if q)
-                copy_rows(out, [q if q else any_row for q in ptrs])   # missing slots overwritten below
-            if missing:
-                self._fill_missing(out, missing, host_rows)
-            return out
+                    missing.append(i)
+                    continue
+                t, row = h
+                g = geo.get(id(t))
+                if g is None:
+                    g = geo[id(t)] = ((t.data_ptr(), 8 * t.stride(0))
+                                      if t.dim() == 2 and t.shape[1] == L and t.stride(1) == 1 else ())
+                if not g:
+                    plain = False
+                    break
+                ptrs[i] = g[0] + g[1] * row
+            if plain:
+                if len(missing) < n:
+                    if missing:   # missing slots: any recorded row, overwritten below
+                        any_row = next(q for q in ptrs if q)
+                        for i in missing:
+                            ptrs[i] = any_row
+                    copy_rows(out, ptrs)
+                if missing:
+                    self._fill_missing(out, missing, host_rows)
+                return out
         by_tensor = {}
         missing = []
         for i, h in enumerate(hits):
