@@ -173,9 +173,16 @@ static int de_step_async(tblup_ctx* c, int strategy, const int32_t* strat_i, con
   const size_t o_keyo = 624 * 4, o_pos = 2 * 624 * 4, o_don = o_pos + 16, o_fix = o_don + (size_t)round_up(12 * pop, 16);
   const size_t o_str = o_fix + 8 * (size_t)pop, o_F = o_str + (size_t)round_up(4 * pop, 16), o_cr = o_F + 8 * (size_t)pop;
   const size_t small = o_cr + 8 * (size_t)pop;
-  if (small > c->de_small.bytes) {
+  // device-only scratch of the three-launch form (large populations): base sequence + windows
+  // (from more individuals than CUs: both forms need a second round of jump workgroups there, and the
+  // split form's mask and stream run several per CU; TBLUP_DE_SPLIT = the smallest split population)
+  static const int64_t split_min = getenv("TBLUP_DE_SPLIT") ? atoll(getenv("TBLUP_DE_SPLIT")) : cu_count() + 1;
+  const bool split = pop >= split_min;
+  const size_t o_scr = (size_t)round_up((int64_t)small, 256);
+  const size_t need = split ? o_scr + 4 * (size_t)(DE_SEQ_SCRATCH + 624 * pop) : small;
+  if (need > c->de_small.bytes) {
     HIPCHK(hipStreamSynchronize(s));
-    if (int rc = dev_alloc(c, c->de_small, small)) return rc;
+    if (int rc = dev_alloc(c, c->de_small, need)) return rc;
   }
   char* base = (char*)c->de_small.p;
   // page-locked staging that outlives this call (the copy is asynchronous); the previous call's
@@ -201,7 +208,8 @@ static int de_step_async(tblup_ctx* c, int strategy, const int32_t* strat_i, con
                         e.pos, d_parents, ld, (const int32_t*)(base + o_don), (const int64_t*)(base + o_fix), strategy,
                         F, cr, clip ? 1 : 0, clip_hi, L, (int)pop, d_children, ldc, (uint32_t*)(base + o_keyo),
                         (int32_t*)(base + o_pos), s, strat_i ? (const int32_t*)(base + o_str) : nullptr,
-                        F_i ? (const double*)(base + o_F) : nullptr, cr_i ? (const double*)(base + o_cr) : nullptr));
+                        F_i ? (const double*)(base + o_F) : nullptr, cr_i ? (const double*)(base + o_cr) : nullptr,
+                        split ? (uint32_t*)(base + o_scr) : nullptr));
   if (!c->de_host) HIPCHK(hipHostMalloc((void**)&c->de_host, 625 * 4, hipHostMallocDefault));
   if (!c->de_ev) HIPCHK(hipEventCreateWithFlags(&c->de_ev, hipEventDisableTiming));
   HIPCHK(hipMemcpyAsync(c->de_host, base + o_keyo, 624 * 4 + 4, hipMemcpyDeviceToHost, s));

@@ -13,7 +13,10 @@
 // LDS, jumps to its own offset by the GF(2) correlation W'[j] = XOR_k p_k x[k+j]
 // with its jump polynomial (mt_jump.cpp), and then runs the MT19937 recurrence
 // forward in a two-block LDS ring, 312 doubles per 624-word block.  Workgroup `pop`
-// produces numpy's (key, pos) after the whole generation's draws.
+// produces numpy's (key, pos) after the whole generation's draws.  Populations larger than
+// the CU count run the same steps as three launches (k_de_seq / k_de_jump / k_de_mask): the
+// 85 KB sequence buffer holds the fused kernel at one workgroup per CU, while the mask
+// recurrence -- a chain of barriers -- wants several workgroups per CU to hide each other's.
 #include <cstdlib>
 
 #include "mt_jump.h"
@@ -89,37 +92,39 @@ struct DeArgs {
   const double* cr_i;
 };
 
-__global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
-#pragma clang fp contract(off)
-  // sequence buffer, 16-B aligned at word pos0 (sq = seq + sh) so the correlation reads b128s;
-  // the slack covers the correlation's trailing loads (bits past degree 19936 are zero)
-  __shared__ __attribute__((aligned(16))) uint32_t seq[SEQ_ALLOC];
-  __shared__ uint32_t ring[2 * MTN];
-  const int tid = threadIdx.x;
-  const int i = blockIdx.x;
-  const bool is_end = i == a.pop;
-  const bool jump = is_end ? a.end_jump != 0 : i > 0;
-  uint32_t* sq = seq + ((4 - (a.pos0 & 3)) & 3);
-
-  // 1. the sequence that continues the base window, as far as this workgroup reads it
-  for (int t = tid; t < MTN; t += DE_THREADS) sq[t] = a.key[t];
-  const int need = jump ? a.pos0 + tblup_mt::MT_DEG + MTN - 1 : (i == 0 ? a.pos0 + MTN : MTN);
+// 1. the sequence that continues the base window, words [0, need) of sq
+__device__ __forceinline__ void de_sequence(const uint32_t* key, uint32_t* sq, int need, int tid) {
+  for (int t = tid; t < MTN; t += DE_THREADS) sq[t] = key[t];
   for (int t0 = MTN; t0 < need; t0 += 227) {
     __syncthreads();
     const int t = t0 + tid;
     if (tid < 227 && t < need) sq[t] = mt_twist(sq[t - 624], sq[t - 623], sq[t - 227]);
   }
   __syncthreads();
+}
 
-  // 2. this workgroup's start window: W[j] = XOR_{k: p_k} x[pos0 + k + j].  Wave g (of NW)
-  // takes poly words [624g/NW, 624(g+1)/NW); lane l < 63 owns outputs 10l .. 10l+9 and holds
-  // the 42 sequence words they read for one poly word in registers, so a set bit costs 10
-  // register XORs (scalar branch on the wave-uniform poly bit); the waves' partial windows are
-  // XOR-reduced through LDS.  VALU-bound: 624 x ~10k set bits XORs per workgroup.
+// acc ^= x in place: the tied operand keeps each accumulator in one register across the
+// wave-uniform branches (plain ^= left the register allocator copying all R accumulators after
+// every bit once the kernel's helpers were split out)
+__device__ __forceinline__ void acc_xor(uint32_t& acc, uint32_t x) {
+  asm("v_xor_b32 %0, %0, %1" : "+v"(acc) : "v"(x));
+}
+
+// 2. workgroup i's start window into ring slot 0: W[j] = XOR_{k: p_k} x[pos0 + k + j].  Wave g
+// (of NW) takes poly words [624g/NW, 624(g+1)/NW); lane l < 63 owns outputs 10l .. 10l+9 and holds
+// the 42 sequence words they read for one poly word in registers, so a set bit costs 10 register
+// XORs (scalar branch on the wave-uniform poly bit); the waves' partial windows are XOR-reduced
+// through LDS (seq, reused).  VALU-bound: 624 x ~10k set bits XORs per workgroup.
+__device__ __forceinline__ void de_window(const DeArgs& a, uint32_t* seq, const uint32_t* sq, uint32_t* ring, int i,
+                                          bool is_end, bool jump, int tid) {
   uint32_t w = 0;
   if (jump && !(a.dbg & 1)) {
     constexpr int NW = DE_THREADS / 64, R = 10, NL = (MTN + R - 1) / R;   // 63 lanes
-    const uint32_t* poly = a.polys + (int64_t)(is_end ? a.pop - 1 : i - 1) * MTN;
+    // the constant address space: the compiler's uniformity / no-clobber analysis does not carry
+    // through the split kernels' helpers, and a vector load of the poly word (+ readfirstlane) costs
+    // a vmcnt(0) wait per word -- this keeps it a scalar load
+    typedef __attribute__((address_space(4))) const uint32_t cu32;
+    cu32* poly = (cu32*)(a.polys + (int64_t)(is_end ? a.pop - 1 : i - 1) * MTN);
     const int g = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int pw0 = MTN * g / NW, pw1 = MTN * (g + 1) / NW;
     uint32_t acc[R];
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
         for (int b = 0; b < 32; ++b)
           if ((cw >> b) & 1u) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] ^= v[b + r];
+            for (int r = 0; r < R; ++r) acc_xor(acc[r], v[b + r]);
           }
       }
     }
@@ -157,18 +162,23 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
   }
   if (tid < MTN) ring[tid] = w;   // block 0 in slot 0
   __syncthreads();
+}
 
-  if (is_end) {
-    mt_block(ring, 1, tid);
-    if (tid < MTN) a.key_out[tid] = ring[a.end_s + tid];
-    if (tid == 0) *a.pos_out = a.end_pos;
-    return;
-  }
+// the end workgroup (i = pop): numpy's (key, pos) after the generation's draws
+__device__ __forceinline__ void de_end_state(const DeArgs& a, uint32_t* ring, int tid) {
+  mt_block(ring, 1, tid);
+  if (tid < MTN) a.key_out[tid] = ring[a.end_s + tid];
+  if (tid == 0) *a.pos_out = a.end_pos;
+}
 
-  // 3. crossover mask, then the elementwise mutant / crossover / clip stream.  The mask of a
-  // segment of up to SEG elements is built in LDS (the sequence buffer is free now) from the
-  // MT19937 words [f, f + 2L) of this window, one double per word pair; the segment is then
-  // streamed with every thread (coalesced loads, many in flight) instead of 312 lanes per block.
+// 3. crossover mask, then the elementwise mutant / crossover / clip stream, NTHR threads.  The mask
+// of a segment of up to MASKW x 32 elements is built in LDS from the MT19937 words [f, f + 2L) of
+// the window in ring slot 0, one double per word pair; the segment is then streamed with every
+// thread (coalesced loads, many in flight) instead of 312 lanes per block.
+template <int NTHR>
+__device__ __forceinline__ void de_stream(const DeArgs& a, uint32_t* ring, uint32_t* mask, int maskw, int i, int tid) {
+#pragma clang fp contract(off)   // numpy's separate multiply and add (the pragma is scoped: here, not the caller)
+  static_assert(NTHR >= MTN / 2, "one thread per word pair of a block");
   const int f = i == 0 ? 0 : 2;
   const int64_t L = a.L;
   const int strategy = a.strat_i ? a.strat_i[i] : a.strategy;
@@ -180,13 +190,12 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
   const double* X1 = a.parent + (int64_t)d1 * a.ldp;
   const double* X2 = a.parent + (int64_t)d2 * a.ldp;
   const int64_t fixed = a.fixed[i];
-  uint32_t* mask = seq;                      // SEG bits
-  constexpr int64_t SEG = (int64_t)SEQ_WORDS * 32;
+  const int64_t SEG = (int64_t)maskw * 32;
   int64_t b = 0;                             // next ring block to consume (block 0 = the window)
   for (int64_t lo = 0; lo < L; lo += SEG) {
     const int64_t hi = lo + SEG < L ? lo + SEG : L;
     __syncthreads();   // previous segment's stream has finished reading the mask
-    for (int t = tid; t < SEQ_WORDS; t += DE_THREADS) mask[t] = 0u;
+    for (int t = tid; t < maskw; t += NTHR) mask[t] = 0u;
     __syncthreads();
     // element j = 312 b + q - f/2 comes from block b, pair q.  (A one-wave recurrence without
     // s_barrier -- a wave's LDS operations execute in order -- measured slower: 0.42 vs
@@ -215,12 +224,12 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
     }
     __syncthreads();
     constexpr int U = 4;
-    for (int64_t j0 = lo + tid; !(a.dbg & 4) && j0 < hi; j0 += (int64_t)U * DE_THREADS) {
+    for (int64_t j0 = lo + tid; !(a.dbg & 4) && j0 < hi; j0 += (int64_t)U * NTHR) {
       double x[U], y0[U], y1[U], y2[U];
       bool m[U];
 #pragma unroll
       for (int r = 0; r < U; ++r) {
-        const int64_t j = j0 + (int64_t)r * DE_THREADS;
+        const int64_t j = j0 + (int64_t)r * NTHR;
         m[r] = false;
         if (j < hi) {
           x[r] = P[j];
@@ -234,7 +243,7 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
       }
 #pragma unroll
       for (int r = 0; r < U; ++r) {
-        const int64_t j = j0 + (int64_t)r * DE_THREADS;
+        const int64_t j = j0 + (int64_t)r * NTHR;
         if (j >= hi) continue;
         double v = x[r];
         if (m[r]) {
@@ -251,13 +260,80 @@ __global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
   }
 }
 
+// One launch per generation (small populations): every workgroup rebuilds the sequence, jumps, and
+// streams its child with the sequence buffer as the mask.
+__global__ __launch_bounds__(DE_THREADS) void k_de_step(DeArgs a) {
+  // sequence buffer, 16-B aligned at word pos0 (sq = seq + sh) so the correlation reads b128s;
+  // the slack covers the correlation's trailing loads (bits past degree 19936 are zero)
+  __shared__ __attribute__((aligned(16))) uint32_t seq[SEQ_ALLOC];
+  __shared__ uint32_t ring[2 * MTN];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x;
+  const bool is_end = i == a.pop;
+  const bool jump = is_end ? a.end_jump != 0 : i > 0;
+  uint32_t* sq = seq + ((4 - (a.pos0 & 3)) & 3);
+  de_sequence(a.key, sq, jump ? a.pos0 + tblup_mt::MT_DEG + MTN - 1 : (i == 0 ? a.pos0 + MTN : MTN), tid);
+  de_window(a, seq, sq, ring, i, is_end, jump, tid);
+  if (is_end) {
+    de_end_state(a, ring, tid);
+    return;
+  }
+  de_stream<DE_THREADS>(a, ring, seq, SEQ_WORDS, i, tid);
+}
+
+// Large populations, three launches: the base sequence once (one workgroup, into gseq), then every
+// workgroup's jump (its window into gwin; the sequence buffer keeps these at one per CU), then the
+// mask and stream on 320 threads with a small LDS footprint, several workgroups per CU -- the mask
+// recurrence is a chain of barriers, so co-resident workgroups hide each other's.  The same
+// arithmetic in the same order as k_de_step: the same bits.
+__global__ __launch_bounds__(DE_THREADS) void k_de_seq(DeArgs a, uint32_t* __restrict__ gseq) {
+  __shared__ __attribute__((aligned(16))) uint32_t seq[SEQ_ALLOC];
+  const int tid = threadIdx.x;
+  uint32_t* sq = seq + ((4 - (a.pos0 & 3)) & 3);
+  const int need = a.pos0 + tblup_mt::MT_DEG + MTN - 1;
+  de_sequence(a.key, sq, need, tid);
+  for (int t = tid; t < need; t += DE_THREADS) gseq[t] = sq[t];
+}
+
+__global__ __launch_bounds__(DE_THREADS) void k_de_jump(DeArgs a, const uint32_t* __restrict__ gseq,
+                                                        uint32_t* __restrict__ gwin) {
+  __shared__ __attribute__((aligned(16))) uint32_t seq[SEQ_ALLOC];
+  __shared__ uint32_t ring[2 * MTN];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x;
+  const bool is_end = i == a.pop;
+  const bool jump = is_end ? a.end_jump != 0 : i > 0;
+  uint32_t* sq = seq + ((4 - (a.pos0 & 3)) & 3);
+  const int need = jump ? a.pos0 + tblup_mt::MT_DEG + MTN - 1 : (i == 0 ? a.pos0 + MTN : MTN);
+  for (int t = tid; t < need; t += DE_THREADS) sq[t] = gseq[t];
+  __syncthreads();
+  de_window(a, seq, sq, ring, i, is_end, jump, tid);
+  if (is_end) {
+    de_end_state(a, ring, tid);
+    return;
+  }
+  if (tid < MTN) gwin[(int64_t)i * MTN + tid] = ring[tid];
+}
+
+constexpr int DE_MASK_THREADS = 320;
+constexpr int DE_MASK_WORDS = 2048;   // 65536 elements per mask segment (8 KiB)
+__global__ __launch_bounds__(DE_MASK_THREADS) void k_de_mask(DeArgs a, const uint32_t* __restrict__ gwin) {
+  __shared__ uint32_t ring[2 * MTN];
+  __shared__ uint32_t mask[DE_MASK_WORDS];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x;
+  for (int t = tid; t < MTN; t += DE_MASK_THREADS) ring[t] = gwin[(int64_t)i * MTN + t];
+  __syncthreads();
+  de_stream<DE_MASK_THREADS>(a, ring, mask, DE_MASK_WORDS, i, tid);
+}
+
 }  // namespace
 
 hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, int end_jump, int end_s, int end_pos,
                           const double* parent, int64_t ldp, const int32_t* donors, const int64_t* fixed, int strategy,
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
                           uint32_t* key_out, int32_t* pos_out, hipStream_t s, const int32_t* strat_i,
-                          const double* F_i, const double* cr_i) {
+                          const double* F_i, const double* cr_i, uint32_t* scratch) {
 #ifdef TBLUP_DIAG_BUILD   // phase ablation (results wrong when set): diagnostic builds only
   static const int dbg = getenv("TBLUP_DE_DBG") ? atoi(getenv("TBLUP_DE_DBG")) : 0;
 #else
@@ -265,7 +341,17 @@ hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, 
 #endif
   DeArgs a{key, pos0, polys, end_jump, end_s, end_pos, parent, ldp, donors, fixed, strategy, F, cr, clip, hi, L, pop,
            child, ldc, key_out, pos_out, dbg, strat_i, F_i, cr_i};
-  hipLaunchKernelGGL(k_de_step, dim3(pop + 1), dim3(DE_THREADS), 0, s, a);
+  if (scratch == nullptr) {
+    hipLaunchKernelGGL(k_de_step, dim3(pop + 1), dim3(DE_THREADS), 0, s, a);
+    return hipGetLastError();
+  }
+  uint32_t* gseq = scratch;
+  uint32_t* gwin = scratch + DE_SEQ_SCRATCH;
+  hipLaunchKernelGGL(k_de_seq, dim3(1), dim3(DE_THREADS), 0, s, a, gseq);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL(k_de_jump, dim3(pop + 1), dim3(DE_THREADS), 0, s, a, gseq, gwin);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL(k_de_mask, dim3(pop), dim3(DE_MASK_THREADS), 0, s, a, gwin);
   return hipGetLastError();
 }
 

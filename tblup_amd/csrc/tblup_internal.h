@@ -338,7 +338,10 @@ hipError_t launch_de_step(const uint32_t* key, int pos0, const uint32_t* polys, 
                           const double* parent, int64_t ldp, const int32_t* donors, const int64_t* fixed, int strategy,
                           double F, double cr, int clip, double hi, int64_t L, int pop, double* child, int64_t ldc,
                           uint32_t* key_out, int32_t* pos_out, hipStream_t s, const int32_t* strat_i = nullptr,
-                          const double* F_i = nullptr, const double* cr_i = nullptr);
+                          const double* F_i = nullptr, const double* cr_i = nullptr, uint32_t* scratch = nullptr);
+// scratch (null: one launch, k_de_step): DE_SEQ_SCRATCH words for the base sequence + pop x 624 for
+// the workgroups' windows -- the three-launch form for large populations (k_de.hip)
+constexpr int64_t DE_SEQ_SCRATCH = 624 + 19937 + 624 + 64;
 
 // ---- launcher (k_de.hip): rows from scattered device rows into one matrix (up to ROWPTRS rows
 //      per launch, source pointers in the kernel arguments) ----

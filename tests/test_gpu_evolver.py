@@ -79,10 +79,11 @@ def test_gpu_de_big_goldens(gold, strat):
     assert random.random() == float(gold[p + "py_next"])
 
 
-@pytest.mark.parametrize("gen,pre", [(1, 0), (5, 623), (7, 624)])
-def test_gpu_de_config2_vs_oracle(gpu, gen, pre):
-    """pop 256 x d 50000 (BASELINE config 2), three generations in a row against the oracle."""
-    d, pop = 50000, 256
+@pytest.mark.parametrize("gen,pre,pop", [(1, 0, 256), (5, 623, 256), (7, 624, 256), (2, 17, 512)])
+def test_gpu_de_config2_vs_oracle(gpu, gen, pre, pop):
+    """pop 256 x d 50000 (BASELINE config 2), three generations in a row against the oracle; pop 512:
+    the three-launch form (sequence, jumps, mask and stream: more individuals than CUs)."""
+    d = 50000
     rng = np.random.default_rng(gen)
     keys = rng.uniform(size=(pop, d))
     fit = list(rng.uniform(size=pop))
@@ -216,10 +217,13 @@ def test_gpu_generations_with_device_keystore(gpu, tmp_path):
 
 
 @pytest.mark.parametrize("L,pop,pre", [(1, 4, 0), (10, 4, 3), (100, 5, 624), (311, 4, 1), (312, 7, 0),
-                                       (313, 6, 622), (1000, 33, 100)])
+                                       (313, 6, 622), (1000, 33, 100), (1, 400, 0), (313, 384, 622),
+                                       (70000, 384, 5)])
 def test_gpu_de_small_shapes_vs_oracle(gpu, L, pop, pre):
     """Tiny generations (< 625 stream words: the end state is rebuilt from the base window
-    without a jump), block-boundary lengths and every numpy position class."""
+    without a jump), block-boundary lengths and every numpy position class; pop >= 384: the
+    three-launch form (more individuals than the 256 CUs), L = 70000 across two of its
+    65536-element mask segments."""
     rng = np.random.default_rng(L * 7 + pop)
     keys = rng.uniform(size=(pop, L))
     fit = list(rng.uniform(size=pop))
