@@ -364,11 +364,17 @@ __device__ __forceinline__ void dstamp(const CholArgs& a, int slot) {
 struct WgTrace {
   uint64_t* rec;
   uint64_t t0;
-  __device__ __forceinline__ explicit WgTrace(uint64_t* base) : rec(nullptr), t0(0) {
+  uint64_t ph;   // up to three phase marks of wave 0 (10-ns ticks from the start, 16 bits each)
+  __device__ __forceinline__ explicit WgTrace(uint64_t* base) : rec(nullptr), t0(0), ph(0) {
     if (base) {
       rec = base + (int64_t)blockIdx.x * WGT_REC;
       t0 = __builtin_amdgcn_s_memrealtime();
     }
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (!rec) return;
+    const uint64_t d = __builtin_amdgcn_s_memrealtime() - t0;
+    ph |= (d < 0xffff ? d : 0xffff) << (16 * k);
   }
   __device__ __forceinline__ void done(int kind, int J, int I, int64_t b) {
     if (!rec) return;
@@ -378,7 +384,7 @@ struct WgTrace {
       rec[0] = t0;
       rec[1] = t1;
       rec[2] = ((uint64_t)kind << 56) | ((uint64_t)I << 40) | (uint64_t)b;
-      rec[3] = (uint64_t)J;
+      rec[3] = (uint64_t)J | (ph << 16);
     }
   }
 };
@@ -1172,16 +1178,39 @@ __device__ __forceinline__ void kc_issue(const CholArgs& a, int64_t b, int I, in
   for (int cb = 0; cb < NCB; ++cb) kcv[cb] = nt_load2(kt + ((cb0 + cb) * 64 + l) * 4);
 }
 
+// K_ij = (c - (u_i + u_j) sa - u_i u_j sm + cN) / d regrouped around the column j: c / d + P_j u_i +
+// Q_j, P_j = -(sa + sm u_j) / d, Q_j = (cN - sa u_j) / d, with P_j = Q_j = 0 on padding columns (whose
+// counts are 0): per element an LDS pair, a conversion and two fmas, where the plain formula took
+// seven fp64 ops and a 64-bit compare -- an fp64 VALU op waits for the matrix pipe while the CU's
+// other waves stream MFMAs (gfx950 does not dual-issue them).  Only the off-diagonal tiles' K comes
+// from here (T-, P- and E-units alike), so every schedule agrees.  k_stage (threads t < TILE, before
+// the unit's barrier): the column pairs of tile Jt and the row sums u_i of tile I.
+__device__ __forceinline__ void k_stage(const CholArgs& a, int64_t b, int64_t i0, int64_t j0, double* pq_sh,
+                                        double* ui_sh) {
+  const int t = threadIdx.x;
+  if (t < TILE) {
+    const double* sc = a.scal + b * SCAL;
+    const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], sm = sc[SC_SM];
+    const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
+    const double uj = a.u[b * a.prow + j0 + t];
+    const bool rj = sys_real(j0 + t, pad, nrow);
+    reinterpret_cast<v2d*>(pq_sh)[t] = rj ? v2d{-invd * (sa + sm * uj), invd * (cN - sa * uj)} : v2d{0.0, 0.0};
+    ui_sh[t] = a.u[b * a.prow + i0 + t];
+  }
+}
+
 template <int NCB>
 __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int Jt, int cb0, const int2 (&kcv)[NCB],
-                                      uint8_t* lds8, const double* uj_sh, const double* ui_sh, v4d (&acc)[NCB]) {
+                                      uint8_t* lds8, const double* pq_sh, const double* ui_sh, v4d (&acc)[NCB]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)Jt * TILE;
   const double* sc = a.scal + b * SCAL;
-  const double sa = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], sm = sc[SC_SM];
+  const double invd = sc[SC_INVD];
   const int64_t nrow = (int64_t)sc[SC_NROW], pad = (int64_t)sc[SC_PAD];
   const int il = 16 * w + (l & 15);
   const bool ireal = sys_real(i0 + il, pad, nrow);
+  const double ui = ui_sh[il];
+  const v2d* pq = reinterpret_cast<const v2d*>(pq_sh);
   if (a.kc) {
     // counts issued before the u / z loads landed; exact ints -> fp64 K
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1192,8 +1221,9 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * (cb0 + cb) + (l >> 4) + 4 * r;
-        const double v = grm_value(c4[r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
-        acc[cb][r] = (ireal && sys_real(j0 + cl, pad, nrow)) ? v : 0.0;
+        const v2d q = pq[cl];
+        const double v = __builtin_fma((double)c4[r], invd, __builtin_fma(q[0], ui, q[1]));
+        acc[cb][r] = ireal ? v : 0.0;
       }
     }
     return;
@@ -1219,8 +1249,9 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * cb + (l >> 4) + 4 * r;
-        const double v = grm_value(cnt[cb][r], uj_sh[cl], ui_sh[il], sa, cN, invd, sm);
-        acc[cb][r] = (ireal && sys_real(j0 + cl, pad, nrow)) ? v : 0.0;
+        const v2d q = pq[cl];
+        const double v = __builtin_fma((double)cnt[cb][r], invd, __builtin_fma(q[0], ui, q[1]));
+        acc[cb][r] = ireal ? v : 0.0;
       }
     }
   }
@@ -1240,10 +1271,7 @@ __device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, i
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)Jt * TILE;
   int2 kcv[NCB];
   if (a.kc) kc_issue<NCB>(a, b, I, Jt, cb0, kcv);
-  if (t < TILE) {
-    uj_sh[t] = a.u[b * a.prow + j0 + t];
-    ui_sh[t] = a.u[b * a.prow + i0 + t];
-  }
+  k_stage(a, b, i0, j0, uj_sh, ui_sh);
   __syncthreads();
   v4d acc[NCB];
   k_acc<NCB>(a, b, I, Jt, cb0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
@@ -1260,8 +1288,9 @@ __device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, i
 }
 
 // T-unit: tile (I, J).
+template <int NTR>   // traits the w update runs over: 1, or MAXT (the zero traits' FMAs wait on the matrix pipe too)
 __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, int ahead_cur, int edone, double* lds,
-                                          double* uj_sh, double* ui_sh, double (*zj_sh)[TILE]) {
+                                          double* uj_sh, double* ui_sh, double (*zj_sh)[TILE], WgTrace& tr) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int J = a.J, NT = a.NT;
   const int64_t ns = a.ns;
@@ -1281,21 +1310,22 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
   } else if (a.kc) {
     kc_issue<8>(a, b, I, J, 0, kcv);
   }
+  if (!from_part) k_stage(a, b, i0, j0, uj_sh, ui_sh);
   if (t < TILE) {
-    uj_sh[t] = a.u[b * a.prow + j0 + t];
-    ui_sh[t] = a.u[b * a.prow + i0 + t];
 #pragma unroll
     for (int tr = 0; tr < MAXT; ++tr)
       zj_sh[tr][t] = (tr < a.nt) ? a.z[(b * a.nt + tr) * ns + j0 + t] : 0.0;
   }
   __syncthreads();
   if (!from_part) k_acc<8>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
+  tr.mark(0);
 
   // 1. T^T = K_JI - sum_L L_JL L_IL^T over the L not summed by launch J-1 or this tile's E-unit
   const int Ls = (ahead_cur ? J - 1 : 0) + edone;
   if (J > Ls && !(a.skip & 64))
     gemm1_a32<8>(Lb + (int64_t)J * NT * TT + (int64_t)Ls * TT, Lb + (int64_t)I * NT * TT + (int64_t)Ls * TT, J - Ls, 0,
                  lds, acc, Ls == 0 ? skip_rows(a, b) : 0);
+  tr.mark(1);
 
   // 2. L_IJ^T = X T^T by 16-row blocks of X (X[j][c] = 0 for c > j).  Dinv holds X in the
   //    packed block layout (blocks transposed): all 36 blocks (72 KiB) land in LDS in one
@@ -1312,6 +1342,7 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  tr.mark(2);
   double wacc[MAXT] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
   for (int jb = 0; jb < NBLK; ++jb) {
@@ -1331,12 +1362,12 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
       const int jl = 16 * jb + (l >> 4) + 4 * r, il = 16 * w + (l & 15);
       Lout[jl * TILE + il] = o[r];
 #pragma unroll
-      for (int tr = 0; tr < MAXT; ++tr) wacc[tr] += o[r] * zj_sh[tr][jl];
+      for (int tr = 0; tr < NTR; ++tr) wacc[tr] += o[r] * zj_sh[tr][jl];
     }
   }
   // w_I[i] += sum_j L_IJ[i][j] z_J[j]: reduce the 4 lane groups that share a column i
 #pragma unroll
-  for (int tr = 0; tr < MAXT; ++tr) {
+  for (int tr = 0; tr < NTR; ++tr) {
     if (tr < a.nt) {
       double v = wacc[tr];
       v += __shfl_xor(v, 16);
@@ -1370,7 +1401,7 @@ __device__ __forceinline__ void e_unit(const CholArgs& a, int64_t b, int I, int 
   const int J = a.J, NT = a.NT;
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
   double* uj_sh = lds + NPACK * BLKD;   // past the GEMM1 ring (2 x 32 KiB) and k_acc's int8 ring
-  double* ui_sh = uj_sh + TILE;
+  double* ui_sh = uj_sh + 2 * TILE;
   double* pd = part_ptr(a, b, I, J);
   v4d acc[8];
   if (ls0 > 0) {
@@ -1383,10 +1414,7 @@ __device__ __forceinline__ void e_unit(const CholArgs& a, int64_t b, int I, int 
   } else {
     int2 kcv[8];
     if (a.kc) kc_issue<8>(a, b, I, J, 0, kcv);
-    if (t < TILE) {
-      uj_sh[t] = a.u[b * a.prow + j0 + t];
-      ui_sh[t] = a.u[b * a.prow + i0 + t];
-    }
+    k_stage(a, b, i0, j0, uj_sh, ui_sh);
     __syncthreads();
     k_acc<8>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
   }
@@ -1515,7 +1543,8 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
 // kernel form only, the K_JJ workgroups for J >= 2 at the end.
 __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) {
   __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
-  __shared__ double uj_sh[TILE], ui_sh[TILE], zj_sh[MAXT][TILE];
+  __shared__ __attribute__((aligned(16))) double uj_sh[2 * TILE];   // k_stage's column pairs (P_j, Q_j)
+  __shared__ double ui_sh[TILE], zj_sh[MAXT][TILE];
   const int64_t npu = (int64_t)p.nP * p.nrs;
   const int64_t n_p = a.B * npu, n_d = a.B * p.nds, n_t = a.B * p.nI;
   int64_t bid = blockIdx.x;
@@ -1570,7 +1599,8 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
     }
     // an E-unit of the diagonal launch summed the term L = Ls0 of the first ne tiles (I-major)
     const int ed = (int64_t)(I - a.J - 1) * a.B + b < p.ne ? 1 : 0;
-    tile_unit(a, b, I, p.ahead_cur, ed, lds, uj_sh, ui_sh, zj_sh);
+    if (a.nt == 1) tile_unit<1>(a, b, I, p.ahead_cur, ed, lds, uj_sh, ui_sh, zj_sh, tr);
+    else tile_unit<MAXT>(a, b, I, p.ahead_cur, ed, lds, uj_sh, ui_sh, zj_sh, tr);
     tr.done(WGT_TILE, a.J, I, b);
     return;
   }

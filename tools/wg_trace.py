@@ -81,6 +81,21 @@ def main():
         print(f"{'diag' if is_diag else 'off '} J={J}: start +{(st - t0) * 1e6:8.1f} span {span * 1e6:7.1f} us "
               f"gap {gap * 1e6:5.1f} util {util:.2f}{first_tile} | " + "; ".join(parts))
     print(f"sum of launch spans {tot * 1e6:.1f} us, first start to last end {(prev_end - t0) * 1e6:.1f} us")
+    # T-unit phases (wave 0's marks, k_chol.hip tile_unit): K / partial in registers, GEMM1 done,
+    # X staged (after the barrier that waits for every wave's GEMM1), end (GEMM2, stores, w update)
+    rk2 = (raw[:, 2] >> np.uint64(56)).astype(np.int64)
+    tiles = raw[rk2 == 2]
+    if len(tiles):
+        ph = tiles[:, 3] >> np.uint64(16)
+        p = np.stack([(ph >> np.uint64(16 * k)) & np.uint64(0xFFFF) for k in range(3)], 1).astype(np.float64) / 100.0
+        tot_us = (tiles[:, 1].astype(np.int64) - tiles[:, 0].astype(np.int64)) / 100.0
+        tJ = (tiles[:, 3] & np.uint64(0xFFFF)).astype(np.int64)
+        print("T-unit phases (us, means over the launch's tiles): K-ready, GEMM1 (wave 0), wait for the waves + X staged, GEMM2 + stores")
+        for J in sorted(set(tJ.tolist())):
+            m = tJ == J
+            k0, g1, xs, en = p[m, 0], p[m, 1], p[m, 2], tot_us[m]
+            print(f"  J={J}: n={int(m.sum()):5d}  K {k0.mean():6.1f}  GEMM1 {(g1 - k0).mean():6.1f}  "
+                  f"X {(xs - g1).mean():5.1f}  GEMM2+ {(en - xs).mean():5.1f}  total {en.mean():6.1f}")
     # phase stamps of diagonal workgroup 0 (tblup_internal.h DTR_RECS): per wave, 30 slots.  They
     # follow the diagonal launch's own records (B x (1 + D-units beside it) + E-units), so locate them from
     # the last diagonal record of launch J (the units per launch depend on the schedule policy)
