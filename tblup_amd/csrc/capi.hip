@@ -249,10 +249,15 @@ bool uses_part(const tblup_ctx* c, int64_t B, int NT, bool st) {
 // SNP-form solve: the chained kernel up to CHAIN_MAX_B individuals (measured at config 2: solve
 // 0.175 -> 0.071 ms at B = 32, 0.184 -> 0.092 at 64, 0.199 -> 0.151 at 128 (round 4's block-row
 // units; round 3's tile units: 0.078 / 0.102 / 0.162), even at 192 (round 3), 0.238 -> 0.274 at
-// 256, where one workgroup per individual already streams L near the HBM rate)
+// 256, where one workgroup per individual already streams L near the HBM rate).  Round 5's pull
+// units (one trait; profiles/r05_solve_pull_ab.txt): 0.061 -> 0.049 ms at 32, 0.079 -> 0.068 at 64,
+// 0.128 -> 0.125 at 128, even at 160, 0.188 (k_solve) -> 0.180 at 192, even at 256 -- bound 192
 constexpr int64_t CHAIN_MAX_B = 160;
-bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B) {
-  return sd.form == FORM_PRIMAL && (c->solve_chain == 1 || (c->solve_chain < 0 && B <= CHAIN_MAX_B));
+constexpr int64_t CHAIN_PULL_MAX_B = 192;
+bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B, int64_t nt) {
+  const bool pull = c->solve_pull == 1 || (c->solve_pull < 0 && nt == 1);
+  return sd.form == FORM_PRIMAL &&
+         (c->solve_chain == 1 || (c->solve_chain < 0 && B <= (pull ? CHAIN_PULL_MAX_B : CHAIN_MAX_B)));
 }
 
 // Last-term mode: the diagonal tile's last SYRK term computed by the previous launch's tile
@@ -293,7 +298,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * KD_TILE * 2 : 0);  // their int16 counts (k_sys_tiles)
   add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
   add(uses_part(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
-  if (use_chain(c, sd, B)) {                                    // chained solve: beta, c_{J->I}, EBV shares
+  if (use_chain(c, sd, B, d.nt)) {                                    // chained solve: beta, c_{J->I}, EBV shares
     add((size_t)B * d.nt * sd.ns * 8);
     add((size_t)B * sd.NT * sd.NT * d.nt * TILE * 8);
     add((size_t)B * sd.NT * d.nt * d.nV * 8);
@@ -469,7 +474,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     int64_t nwg = 0;
     for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + plan[J].ne + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
-    if (use_chain(c, sd, B)) nwg += B * sd.NT;   // chained solve units
+    if (use_chain(c, sd, B, d.nt)) nwg += B * sd.NT;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
     wgt = (uint64_t*)c->wgt.p;
@@ -553,7 +558,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
                                  kbar * (double)(d.nT + d.nV));
   SolveChain ch{};
   const SolveChain* chp = nullptr;
-  if (!redo && use_chain(c, sd, B)) {
+  if (!redo && use_chain(c, sd, B, d.nt)) {
     const size_t fbytes = ((size_t)B * chain_flags(sd.NT) + CHAIN_ERR_RING + 1) * 4;
     if (c->chain.bytes < fbytes || c->chain_seq >= INT32_MAX - 1) {
       HIPCHK(hipStreamSynchronize(s));   // the flags may still be read by an earlier chained solve
@@ -574,6 +579,8 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     ch.expired = c->host_entry ? ring + CHAIN_ERR_RING : (int32_t*)c->status.p + ST_SOLVE;
     c->last_chain_seq = ch.seq;
     ch.mode = c->chain_sync;
+    // pull units for one trait (several traits: their registers spill at two units per CU)
+    ch.pull = c->solve_pull == 1 || (c->solve_pull < 0 && d.nt == 1);
     ch.spin_max = CHAIN_SPIN_MAX;
     ch.delay = 0;
     if (c->chain_dbg_shots > 0) {
@@ -667,6 +674,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   c->form_pref = fp ? std::max(0, std::min(2, atoi(fp))) : 0;
   if (const char* e = getenv("TBLUP_AHEAD")) c->ahead = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_SOLVE_CHAIN")) c->solve_chain = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_SOLVE_PULL")) c->solve_pull = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_CHAIN_SYNC")) c->chain_sync = atoi(e);
   if (const char* e = getenv("TBLUP_LAST_TERM")) c->last_term = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_LT_MASK")) c->lt_mask = (int)strtol(e, nullptr, 0);

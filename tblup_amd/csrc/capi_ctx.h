@@ -99,6 +99,9 @@ struct tblup_ctx {
   int lt_mask = -1;      // TBLUP_LT_MASK: the diagonal launches in last-term mode by bit (A/B timing; -1 auto)
   int solve_chain = -1;  // TBLUP_SOLVE_CHAIN: SNP-form back substitution spread over the chip (k_solve_chain):
                          // -1 auto (B <= CHAIN_MAX_B), 0 never, 1 always -- bit-identical results either way
+  int solve_pull = -1;   // TBLUP_SOLVE_PULL: the chained solve's units pull beta_K and the tiles of their block
+                         // column (1; -1 auto: one trait) or push the tile products of their block row (0)
+                         // -- the same bits
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
   int fold_share = 1;    // TBLUP_FOLD_SHARE: 0 builds every fold's system tiles from its own rows
   int sys_st = -1;       // TBLUP_SYS_ST: system tiles by the persistent super-tile kernel (k_sys_tiles_st):

@@ -258,14 +258,14 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   for (int64_t i = t; i < nt * ns; i += NTH) alpha[i] = c.z[b * nt * ns + i];
   __syncthreads();
   for (int I = NT - 1; I >= 0; --I) {
-    // s = sum_{J > I} (L_JI^T alpha_J), one tile's row partial at a time, J ascending (the
-    // chained solve's order)
+    // s = sum_{J > I} (L_JI^T alpha_J), one tile's row partial at a time, J descending (the
+    // chained solve's order: its pull units get alpha_J from the bottom up)
     double s[NTR] = {};
     // two tiles per step: 256 B per thread (256 KiB per workgroup) in flight
-    for (int J = I + 1; J < ((c.skip & 1024) ? 0 : NT); J += 2) {
-      const bool two = J + 1 < NT;
+    for (int J = (c.skip & 1024) ? I : NT - 1; J > I; J -= 2) {
+      const bool two = J - 1 > I;
       const double* row0 = Lb + ((int64_t)J * NT + I) * TILE * TILE + rc * TILE + 2 * seg;
-      const double* row1 = two ? row0 + (int64_t)NT * TILE * TILE : row0;
+      const double* row1 = two ? row0 - (int64_t)NT * TILE * TILE : row0;
       v2d x0[8], x1[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) x0[e] = *reinterpret_cast<const v2d*>(row0 + 16 * e);
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 #pragma unroll
       for (int tr = 0; tr < NTR; ++tr) s[tr] += p[tr];
       if (two) {
-        tile_row_partial<NTR>(x1, alpha + (J + 1) * TILE, ns, seg, p);
+        tile_row_partial<NTR>(x1, alpha + (J - 1) * TILE, ns, seg, p);
 #pragma unroll
         for (int tr = 0; tr < NTR; ++tr) s[tr] += p[tr];
       }
@@ -431,6 +431,15 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 // runs on its own CU beside the chain.  (Round 3's form -- a unit per tile, each holding its tile in
 // registers until beta_J arrived, and two hand-offs per block row (F -> T -> F) -- spent most of its
 // time with the chip's unit slots full of waiting tile units: 0.162 ms at pop 128.)
+// Pull units (round 5, the default; TBLUP_SOLVE_PULL=0 keeps the push units above): U(b, J) takes
+// the tiles of its block COLUMN instead -- it publishes only beta_J (ch.beta, flag_beta), and pulls
+// c_{K->J} = L_KJ^T beta_K itself for K = NT-1 .. J+1 as the beta_K arrive (tile (K-1, J) loading while
+// it waits for beta_{K-1}), then v, beta_J = X_J^T v, beta_J published.  The chain still costs one
+// hand-off and one tile product per block row, but the work of a unit is 7 - J tiles instead of J:
+// the first-dispatched levels (large J) end at once and free their slots, where the push units of
+// level NT-1 streamed NT-1 tiles while the low levels, which the chain ends on, waited for a slot
+// (pop 128: 1024 units on 512 slots, levels 3 .. 0 dispatched 66-102 us in,
+// profiles/r04_solve_trace_pop128.txt).  Every c_{K->J} sum runs K descending, in k_solve too.
 // Grid order: level J = NT-1 .. 0, individuals within a level.  A unit waits only on units with
 // smaller block ids (U(b, J) on U(b, K > J)), and each XCD dispatches its share in block-id order, so
 // the waits drain.  Argument: let u be the smallest block id not yet dispatched.  u's XCD is full,
@@ -482,6 +491,10 @@ __device__ __forceinline__ int32_t* flag_part(const SolveChain& ch, int64_t b, i
 }
 __device__ __forceinline__ int32_t* flag_e(const SolveChain& ch, int64_t b, int NT, int J) {
   return ch.flags + b * chain_flags(NT) + NT + NT * NT + J;
+}
+// pull units: beta_K published (the first NT flags of an individual)
+__device__ __forceinline__ int32_t* flag_beta(const SolveChain& ch, int64_t b, int NT, int K) {
+  return ch.flags + b * chain_flags(NT) + K;
 }
 
 // Exchange through coherent (sc1) accesses: the producer stores its data and, once every wave's
@@ -552,7 +565,7 @@ __device__ __forceinline__ void chain_tile_load(const CholLaunch& c, int64_t b, 
     for (int e = 0; e < 8; ++e) x[h][e] = *reinterpret_cast<const v2d*>(tile + (rc + 64 * h) * TILE + 16 * e);
 }
 
-// c_{J->I} = L_JI^T beta_J (beta_J in bsh) -> cpart, then its flag
+// push units: c_{J->I} = L_JI^T beta_J (beta_J in bsh) -> cpart, then its flag
 template <int NTR>
 __device__ __forceinline__ void chain_tile_publish(const SolveChain& ch, int64_t b, int NT, int J, int I,
                                                    const v2d (&x)[2][8], const double (*bsh)[TILE], int rc,
@@ -569,7 +582,7 @@ __device__ __forceinline__ void chain_tile_publish(const SolveChain& ch, int64_t
 }
 
 // The unit of block row J.  xl: 72 KiB of LDS -- X_J, then (U(b, 0)) the EBVs.
-template <int NTR>
+template <int NTR, bool PULL>
 __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b, int J, double* fit, double* ebv,
                            double* xl, int* sh, ChainTrace& tr_) {
   __shared__ double vsh[NTR][TPAD];   // z_J, then v (padded: vpi)
@@ -595,26 +608,72 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
     }
   }
   v2d x[2][8];
-  if (J > 0) chain_tile_load(c, b, J, J - 1, rc, seg, x);
+  constexpr bool pull = PULL;
+  if constexpr (pull) {
+    if (J + 1 < NT) chain_tile_load(c, b, NT - 1, J, rc, seg, x);   // the first tile pulled: (NT-1, J)
+  } else if (J > 0) {
+    chain_tile_load(c, b, J, J - 1, rc, seg, x);
+  }
   for (int i = t; i < NTR * TILE; i += CTH) vsh[i / TILE][vpi(i % TILE)] = c.z[(b * NTR + i / TILE) * ns + (int64_t)J * TILE + i % TILE];
   for (int r = t; r < nr; r += CTH) {
     const int64_t g = (int64_t)J * TILE + r;
     rowp[r] = (g < pad) ? (int32_t)c.d.P : (int32_t)snp_col(c.idx[o0 + g - pad], c.d.P);
   }
-  for (int K = J + 1; K < NT; ++K)
-    if (!chain_wait(flag_part(ch, b, NT, J, K), ch, sh)) {
-      if (J == 0 && t == 0) fit[b] = __builtin_nan("");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the X_J LDS-DMA lands before the workgroup ends
-      return;
+  if constexpr (pull) {
+    // c_{K->J} = L_KJ^T beta_K for K = NT-1 .. J+1 as the beta_K arrive, summed in that order (k_solve's):
+    // tile (K-1, J)'s rows are loaded into the registers each half of tile K frees, so the next
+    // tile is in flight while this unit waits for beta_{K-1}
+    double acc[2][NTR];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr) acc[h][tr] = 0.0;
+    for (int K = NT - 1; K > J; --K) {
+      if (!chain_wait(flag_beta(ch, b, NT, K), ch, sh)) {
+        if (J == 0 && t == 0) fit[b] = __builtin_nan("");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the X_J LDS-DMA lands before the workgroup ends
+        return;
+      }
+      if (t < NTR * TILE) bsh[t / TILE][t % TILE] = cload(ch.beta + (b * NTR + t / TILE) * ns + (int64_t)K * TILE + t % TILE);
+      __syncthreads();
+      const double* nxt = c.L + ((b * NT + K - 1) * (int64_t)NT + J) * TILE * TILE + 2 * seg;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double p[NTR];
+        tile_row_partial<NTR>(x[h], &bsh[0][0], TILE, seg, p);
+#pragma unroll
+        for (int tr = 0; tr < NTR; ++tr) acc[h][tr] += p[tr];
+        if (K - 1 > J) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[h][e] = *reinterpret_cast<const v2d*>(nxt + (rc + 64 * h) * TILE + 16 * e);
+        }
+      }
+      __syncthreads();   // bsh is overwritten by the next beta
     }
-  tr_.waited();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X_J in LDS, z_J, the row table
-  __syncthreads();
-  for (int i = t; i < NTR * TILE; i += CTH) {   // v = z_J - sum_{K > J} c_{K->J}, K ascending
-    const int tr = i / TILE, cc = i % TILE;
-    double acc = 0.0;
-    for (int K = J + 1; K < NT; ++K) acc += cload(ch.cpart + (((b * NT + J) * NT + K) * NTR + tr) * TILE + cc);
-    vsh[tr][vpi(cc)] = vsh[tr][vpi(cc)] - acc;
+    tr_.waited();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X_J in LDS, z_J, the row table
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)   // v = z_J - sum_{K > J} c_{K->J}
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr)
+        if (seg == 0) vsh[tr][vpi(rc + 64 * h)] = vsh[tr][vpi(rc + 64 * h)] - acc[h][tr];
+  } else {
+    for (int K = J + 1; K < NT; ++K)
+      if (!chain_wait(flag_part(ch, b, NT, J, K), ch, sh)) {
+        if (J == 0 && t == 0) fit[b] = __builtin_nan("");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the X_J LDS-DMA lands before the workgroup ends
+        return;
+      }
+    tr_.waited();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X_J in LDS, z_J, the row table
+    __syncthreads();
+    for (int i = t; i < NTR * TILE; i += CTH) {   // v = z_J - sum_{K > J} c_{K->J}, K descending
+      const int tr = i / TILE, cc = i % TILE;
+      double acc = 0.0;
+      for (int K = NT - 1; K > J; --K) acc += cload(ch.cpart + (((b * NT + J) * NT + K) * NTR + tr) * TILE + cc);
+      vsh[tr][vpi(cc)] = vsh[tr][vpi(cc)] - acc;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -632,6 +691,13 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
     if (ch.delay > 0 && b == 0 && J == NT - 1) {   // debug knob (expiry test): a late producer
       for (int i = 0; i < ch.delay; ++i) __builtin_amdgcn_s_sleep(127);
     }
+  }
+  if constexpr (pull) {
+    if (J > 0) {   // beta_J for the units of the block columns I < J
+      if (t < NTR * TILE) cstore(ch.beta + (b * NTR + t / TILE) * ns + (int64_t)J * TILE + t % TILE, bsh[t / TILE][t % TILE]);
+      chain_publish(flag_beta(ch, b, NT, J), ch.seq, ch.mode);
+    }
+  } else if (J > 0) {
     chain_tile_publish<NTR>(ch, b, NT, J, J - 1, x, bsh, rc, seg);
     for (int I = J - 2; I >= 0; --I) {
       chain_tile_load(c, b, J, I, rc, seg, x);
@@ -700,8 +766,8 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
   tr_.done(WGT_SROW, J, 1, b);
 }
 
-template <int NTR>
-__global__ __launch_bounds__(CTH) void k_solve_chain(CholLaunch c, SolveChain ch, double* __restrict__ fit,
+template <int NTR, bool PULL>
+__global__ __launch_bounds__(CTH, NTR < 4 ? 4 : 2) void k_solve_chain(CholLaunch c, SolveChain ch, double* __restrict__ fit,
                                                      double* __restrict__ ebv) {
   __shared__ __attribute__((aligned(16))) double xl[NPACK * BLKD];   // X_J, then (U(b, 0)) the EBVs
   __shared__ int sh;
@@ -709,7 +775,7 @@ __global__ __launch_bounds__(CTH) void k_solve_chain(CholLaunch c, SolveChain ch
   const int64_t g = blockIdx.x;
   const int J = NT - 1 - (int)(g / c.B);
   ChainTrace tr(c.wgt);
-  chain_unit<NTR>(c, ch, g % c.B, J, fit, ebv, xl, &sh, tr);
+  chain_unit<NTR, PULL>(c, ch, g % c.B, J, fit, ebv, xl, &sh, tr);
 }
 
 // whether the chained solve can run this batch: the EBVs of U(b, 0) fit its 72 KiB of LDS
@@ -731,11 +797,16 @@ hipError_t launch_solve(const CholLaunch& c, const SolveChain* ch, double* fitne
       hipLaunchKernelGGL(kernel, grid, dim3(CTH), 0, s, c, *ch, fitness, ebv);
       return hipGetLastError();
     };
-    switch (c.d.nt) {
-      case 1: return launch_chain(k_solve_chain<1>);
-      case 2: return launch_chain(k_solve_chain<2>);
-      case 3: return launch_chain(k_solve_chain<3>);
-      case 4: return launch_chain(k_solve_chain<4>);
+    const int sel = c.d.nt * 2 + (ch->pull ? 1 : 0);
+    switch (sel) {
+      case 2: return launch_chain(k_solve_chain<1, false>);
+      case 3: return launch_chain(k_solve_chain<1, true>);
+      case 4: return launch_chain(k_solve_chain<2, false>);
+      case 5: return launch_chain(k_solve_chain<2, true>);
+      case 6: return launch_chain(k_solve_chain<3, false>);
+      case 7: return launch_chain(k_solve_chain<3, true>);
+      case 8: return launch_chain(k_solve_chain<4, false>);
+      case 9: return launch_chain(k_solve_chain<4, true>);
       default: return hipErrorInvalidValue;
     }
   }

@@ -302,7 +302,7 @@ hipError_t launch_sys_tiles_folds(const CholLaunch& c, hipStream_t s);
 // per-call flags (SolveChain).
 struct SolveChain {
   int32_t* flags;   // [B][chain_flags(NT)], compared with seq (never reset)
-  double* beta;     // [B][nt][ns] (unused since the block-row units keep beta_J in LDS)
+  double* beta;     // [B][nt][ns]: beta_J, published by the pull units (flags [0, NT) of an individual)
   double* cpart;    // [B][NT (row I)][NT (tile J)][nt][128]: L_JI^T beta_J
   double* epart;    // [B][NT][nt][nV]: block J's share of X_V beta
   double* mbpart;   // [B][NT][nt]: block J's share of sum_a s_a beta_a
@@ -315,6 +315,7 @@ struct SolveChain {
   int32_t seq;      // this call's flag value
   int32_t mode;     // TBLUP_CHAIN_SYNC (k_solve.hip)
   int32_t spin_max; // polls before a wait gives up (CHAIN_SPIN_MAX; lowered only by the debug knob)
+  int32_t pull;     // 1: pull units (block column J: beta_K, K > J, and the tiles (K, J)); 0: push units
   int32_t delay;    // debug knob only: U(0, NT-1) sleeps this many s_sleep(127) rounds before
                     // publishing, so its consumers' waits expire (0 in production)
 };

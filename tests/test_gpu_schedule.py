@@ -9,7 +9,7 @@ the off-diagonal launch or beside the diagonal one, and a tile's GEMM1 term L = 
 T-unit or in an E-unit beside the diagonal launch, so fitness
 and EBVs must be bit-identical under every setting, for both system forms and for system sizes
 from 1 to 9 tile columns; and equal to the oracle.  (TBLUP_AHEAD / TBLUP_NRS / TBLUP_SOLVE_CHAIN /
-TBLUP_LAST_TERM / TBLUP_PAD_FIRST / TBLUP_DIAG_D / TBLUP_DIAG_E are read when a context is created.)"""
+TBLUP_SOLVE_PULL / TBLUP_LAST_TERM / TBLUP_PAD_FIRST / TBLUP_DIAG_D / TBLUP_DIAG_E are read when a context is created.)"""
 import os
 
 import numpy as np
@@ -27,6 +27,8 @@ SETTINGS = [
     {"TBLUP_AHEAD": "1", "TBLUP_NRS": "0"},
     {"TBLUP_AHEAD": "-1", "TBLUP_NRS": "0"},        # the defaults
     {"TBLUP_SOLVE_CHAIN": "1"},                     # SNP form: chained solve at every batch size
+    {"TBLUP_SOLVE_CHAIN": "1", "TBLUP_SOLVE_PULL": "0"},   # ... its push units (block rows)
+    {"TBLUP_SOLVE_CHAIN": "1", "TBLUP_SOLVE_PULL": "1"},   # ... its pull units (block columns), every trait count
     {"TBLUP_SOLVE_CHAIN": "0"},                     # one solve workgroup per individual
     {"TBLUP_LAST_TERM": "1"},                       # diagonal's last SYRK term in the previous launch
     {"TBLUP_LAST_TERM": "0"},                       # ... in the diagonal launch

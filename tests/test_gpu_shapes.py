@@ -87,16 +87,18 @@ def test_config5_pop256_primal_multitrait_solve(panel):
             assert _relmax(ebv[i, tr], e) <= EBV_RTOL, (i, tr)
             fs.append(f)
         assert abs(fit[i] - np.mean(fs)) <= FIT_ATOL, i
-    chained = _run(p, p["genomes"], {"TBLUP_SOLVE_CHAIN": "1"}, traits=True)
-    np.testing.assert_array_equal(chained[0], fit)
-    np.testing.assert_array_equal(chained[1], ebv)
+    for pull in ("0", "1"):   # the chained solve's push and pull units
+        chained = _run(p, p["genomes"], {"TBLUP_SOLVE_CHAIN": "1", "TBLUP_SOLVE_PULL": pull}, traits=True)
+        np.testing.assert_array_equal(chained[0], fit)
+        np.testing.assert_array_equal(chained[1], ebv)
 
 
-@pytest.mark.parametrize("B", [128, 32, 96, 160])
+@pytest.mark.parametrize("B", [128, 32, 96, 160, 192])
 def test_config3_shard_auto_policies(panel, B):
     """B individuals in one batch with every automatic schedule policy at once, against the
     oracle and against every policy switched off, bit for bit.  (96 / 160: E-units covering
-    columns in part, their tiles dispatched last; 128: in part and whole; 32: whole.)"""
+    columns in part, their tiles dispatched last; 128: in part and whole; 32: whole; 192: the
+    chained solve's pull units at their largest batch.)"""
     p = panel
     genomes = p["genomes"][:B]
     fit, ebv = _run(p, genomes)
