@@ -58,6 +58,31 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #ifndef TBLUP_AB_ASM_GEMM1   // the GEMM1 ring's DMA as inline asm
 #define TBLUP_AB_ASM_GEMM1 1
 #endif
+// Non-temporal result stores (round 5): the L tiles of the T-units, the partial sums (P- / E-units),
+// the diagonal targets S and last terms Q -- each read by a later launch, none by this one (the
+// last-term read-back aside), and every line a kernel leaves dirty in L2 is written back at its
+// end (the kernel boundary).  Interleaved A/B at config 2 (profiles/r05_nt_store_ab.txt): both on
+// +0.9% at pop 256 (off-diagonal 1.611 -> 1.594 ms), +1.0% at 128, +0.9% at 64 (the L tiles alone:
+// -0.3% at 64).  TBLUP_AB_NT_*: A/B builds only (tools/ab_build_defs.sh).
+#ifndef TBLUP_AB_NT_L
+#define TBLUP_AB_NT_L 1
+#endif
+#ifndef TBLUP_AB_NT_PART
+#define TBLUP_AB_NT_PART 1
+#endif
+#ifndef TBLUP_AB_NT_X   // the diagonal kernel's X_J (Dinv) stores
+#define TBLUP_AB_NT_X 0
+#endif
+#ifndef TBLUP_AB_NT_KD   // the K_JJ + lambda I tiles J < 2 of the system-tile epilogue
+#define TBLUP_AB_NT_KD 0
+#endif
+template <bool NT>
+__device__ __forceinline__ void st64(double* p, double v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
 #ifndef TBLUP_AB_ASM_I8   // the integer-count rings' DMA (int8 / packed tiles, per-tile system tiles) as inline asm
 #define TBLUP_AB_ASM_I8 1
 #endif
@@ -321,7 +346,7 @@ __device__ __forceinline__ void kd_block(const CholArgs& a, int64_t b, int J, in
     const double kv = grm_value(c4[r], ub[cl], uj, sa, cN, invd, sm);
     const double v = (sys_real(gi, pad, nrow) && sys_real(gj, pad, nrow)) ? kv + ((gi == gj) ? lam : 0.0)
                                                                          : ((gi == gj) ? 1.0 : 0.0);
-    dst[pk(q, sb) + bo((l >> 4) + 4 * r, l & 15)] = v - sub[r];
+    st64<TBLUP_AB_NT_PART>(dst + pk(q, sb) + bo((l >> 4) + 4 * r, l & 15), v - sub[r]);
   }
 }
 // The exact count tiles are written once (k_sys_tiles) and read once (the unit that forms their K):
@@ -836,7 +861,7 @@ __device__ __forceinline__ void store_syrk_blocks(double* dst, const double* bas
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = pk(q, sb) + bo((l >> 4) + 4 * r, l & 15);
-        dst[o] = base ? base[o] - acc[i][r] : acc[i][r];
+        st64<TBLUP_AB_NT_PART>(dst + o, base ? base[o] - acc[i][r] : acc[i][r]);
       }
     }
   }
@@ -1130,7 +1155,10 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       const int g = 2 * k, blk = g >> 8, o = g & 255, r = o >> 4;
       const int c0 = 2 * (((o & 15) >> 1) ^ ((r >> 1) & 7));
       const double* xb = Xp + blk * BLKD;
-      *reinterpret_cast<v2d*>(Xg + g) = v2d{xb[bo(c0, r)], xb[bo(c0 + 1, r)]};
+      if constexpr (TBLUP_AB_NT_X)
+        __builtin_nontemporal_store(v2d{xb[bo(c0, r)], xb[bo(c0 + 1, r)]}, reinterpret_cast<v2d*>(Xg + g));
+      else
+        *reinterpret_cast<v2d*>(Xg + g) = v2d{xb[bo(c0, r)], xb[bo(c0 + 1, r)]};
     }
   }
   if (a.skip & FLAG_WRITE_LJJ) {
@@ -1282,8 +1310,13 @@ __device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, i
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
     v2d* d = reinterpret_cast<v2d*>(pd + ((cb0 + cb) * 64 + l) * 4);
-    d[0] = v2d{acc[cb][0], acc[cb][1]};
-    d[1] = v2d{acc[cb][2], acc[cb][3]};
+    if constexpr (TBLUP_AB_NT_PART) {
+      __builtin_nontemporal_store(v2d{acc[cb][0], acc[cb][1]}, d);
+      __builtin_nontemporal_store(v2d{acc[cb][2], acc[cb][3]}, d + 1);
+    } else {
+      d[0] = v2d{acc[cb][0], acc[cb][1]};
+      d[1] = v2d{acc[cb][2], acc[cb][3]};
+    }
   }
 }
 
@@ -1360,7 +1393,7 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int jl = 16 * jb + (l >> 4) + 4 * r, il = 16 * w + (l & 15);
-      Lout[jl * TILE + il] = o[r];
+      st64<TBLUP_AB_NT_L>(Lout + jl * TILE + il, o[r]);
 #pragma unroll
       for (int tr = 0; tr < NTR; ++tr) wacc[tr] += o[r] * zj_sh[tr][jl];
     }
@@ -1425,8 +1458,13 @@ __device__ __forceinline__ void e_unit(const CholArgs& a, int64_t b, int I, int 
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) {
     v2d* d = reinterpret_cast<v2d*>(pd + (cb * 64 + l) * 4);
-    d[0] = v2d{acc[cb][0], acc[cb][1]};
-    d[1] = v2d{acc[cb][2], acc[cb][3]};
+    if constexpr (TBLUP_AB_NT_PART) {
+      __builtin_nontemporal_store(v2d{acc[cb][0], acc[cb][1]}, d);
+      __builtin_nontemporal_store(v2d{acc[cb][2], acc[cb][3]}, d + 1);
+    } else {
+      d[0] = v2d{acc[cb][0], acc[cb][1]};
+      d[1] = v2d{acc[cb][2], acc[cb][3]};
+    }
   }
 }
 
@@ -1663,7 +1701,7 @@ __device__ __forceinline__ void sys_diag_epilogue_src(const CholArgs& a, const v
         const double kv = grm_value((int32_t)cnt[m][n][r], ur[m][r], uc[n], sa_, cN, invd, sm);
         const double v = (sys_real(gi, pad, nrow) && sys_real(gj, pad, nrow)) ? kv + ((gi == gj) ? lam : 0.0)
                                                                               : ((gi == gj) ? 1.0 : 0.0);
-        Kd[pk(cb, ib) + bo(cl & 15, il & 15)] = v;
+        st64<TBLUP_AB_NT_KD>(Kd + pk(cb, ib) + bo(cl & 15, il & 15), v);
       }
     }
 }
