@@ -73,6 +73,9 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #ifndef TBLUP_AB_NT_X   // the diagonal kernel's X_J (Dinv) stores
 #define TBLUP_AB_NT_X 0
 #endif
+#ifndef TBLUP_AB_NT_PLD   // the partial sums' and S's loads non-temporal (each read once; A/B:
+#define TBLUP_AB_NT_PLD 1    // +0.7% at pop 128, +0.15% at 256, profiles/r05_nt_store_ab.txt)
+#endif
 #ifndef TBLUP_AB_NT_KD   // the K_JJ + lambda I tiles J < 2 of the system-tile epilogue
 #define TBLUP_AB_NT_KD 0
 #endif
@@ -1012,7 +1015,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 #pragma unroll
     for (int e = 0; e < NPACK * BLKD / 2 / DTHR; ++e) {   // 9 x 16 B per thread
       const int chunk = (e * DW + w) * 64;
-      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src + 2 * (chunk + l), (lds_ptr_t)(Tp + 2 * chunk), 16, 0, TBLUP_AB_NT_PLD ? 2 : 0);
     }
     if (J > L0 && a.q != nullptr) {
       // last-term mode: Q = L_{J,J-1} L_{J,J-1}^T came with launch J-1's tile (J, J-1)
@@ -1337,7 +1340,8 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb) {
       const v2d* s2 = reinterpret_cast<const v2d*>(pd + (cb * 64 + l) * 4);
-      const v2d lo = s2[0], hi = s2[1];
+      const v2d lo = TBLUP_AB_NT_PLD ? __builtin_nontemporal_load(s2) : s2[0];
+      const v2d hi = TBLUP_AB_NT_PLD ? __builtin_nontemporal_load(s2 + 1) : s2[1];
       acc[cb] = v4d{lo[0], lo[1], hi[0], hi[1]};
     }
   } else if (a.kc) {
@@ -1441,7 +1445,8 @@ __device__ __forceinline__ void e_unit(const CholArgs& a, int64_t b, int I, int 
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb) {
       const v2d* s2 = reinterpret_cast<const v2d*>(pd + (cb * 64 + l) * 4);
-      const v2d lo = s2[0], hi = s2[1];
+      const v2d lo = TBLUP_AB_NT_PLD ? __builtin_nontemporal_load(s2) : s2[0];
+      const v2d hi = TBLUP_AB_NT_PLD ? __builtin_nontemporal_load(s2 + 1) : s2[1];
       acc[cb] = v4d{lo[0], lo[1], hi[0], hi[1]};
     }
   } else {
