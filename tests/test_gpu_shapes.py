@@ -122,17 +122,19 @@ def test_chain_sync_modes_bit_identical(panel):
     np.testing.assert_array_equal(a[1], b[1])
 
 
-def test_chained_solve_expiry_recovers(panel):
+@pytest.mark.parametrize("pull", ["1", "0"])
+def test_chained_solve_expiry_recovers(panel, pull):
     """TBLUP_CHAIN_DEBUG=spin,delay,shots: the next `shots` chained solves poll at most `spin`
     times while one producer sleeps `delay` rounds, so a wait expires.  Host entry: the call
     re-solves the chunk's factor through k_solve and returns the reference bits (counted by
-    tblup_chain_recoveries); device entry: the solve-error flag; then the same context is clean."""
+    tblup_chain_recoveries); device entry: the solve-error flag; then the same context is clean.
+    Both kinds of chained-solve unit: pull (beta_J hand-offs) and push (tile products)."""
     import torch
     from tblup_amd.engine import GpuBlupEngine, concat_genomes
     p = panel
     genomes = p["genomes"][:8]                  # SNP form, B = 8 <= 160: the chained solve
     ref = _run(p, genomes)
-    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,2"}):
+    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,2", "TBLUP_SOLVE_PULL": pull}):
         eng = GpuBlupEngine(p["geno"], p["pheno"], device=0)
     try:
         fit, ebv = eng.evaluate(genomes, p["T"], p["V"], 0.4, return_ebv=True)   # shot 1: recovered
@@ -163,11 +165,11 @@ def test_chained_solve_expiry_recovers(panel):
         ref_f = eng.evaluate_folds(genomes, folds, 0.4)
     finally:
         eng.close()
-    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,1"}):
+    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,1", "TBLUP_SOLVE_PULL": pull}):
         with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
             np.testing.assert_array_equal(eng.evaluate_folds(genomes, folds, 0.4), ref_f)
             assert eng.chain_recoveries() == 1
-    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,2", "TBLUP_FOLD_FUSE": "0"}):
+    with _env({"TBLUP_CHAIN_DEBUG": "1000,20000,2", "TBLUP_FOLD_FUSE": "0", "TBLUP_SOLVE_PULL": pull}):
         with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:   # split by split: both folds again
             np.testing.assert_array_equal(eng.evaluate_folds(genomes, folds, 0.4), ref_f)
             assert eng.chain_recoveries() == 1
