@@ -270,13 +270,18 @@ bool use_chain(const tblup_ctx* c, const SysDims& sd, int64_t B, int64_t nt) {
 // 64 < B <= 160 only diagonal launches 1 and 3 -- the workgroup traces of round 4 (pop 128,
 // profiles/r04_wg_trace_pop128_auto.txt / _lastterm.txt) give, per launch, the off-diagonal launch's
 // extra time against the next diagonal launch's saving: J = 0: -1.1 / -9.1 us, J = 2: +0.5 / -5.6;
-// every other launch loses.
+// every other launch loses.  Late in round 5 (pull-unit solve, non-temporal stores; traces
+// profiles/r05i_wg_trace_pop128.txt: tiles (7, 6) and (6, 5) done 20 / 40 us before their launches
+// end) diagonal launches 6 and 7 too up to 128: pop 128 +0.8%, 96 +1.5%, 112 even, 160 -0.2%
+// (profiles/r05_lt_mask4_ab.txt).
 constexpr int64_t LT_MAX_B = 64;
+constexpr int64_t LT_LATE_MAX_B = 128;
 constexpr int64_t LT_PART_MAX_B = 160;
 uint32_t last_term_mask(const tblup_ctx* c, const SysDims& sd, int64_t B) {
   if (sd.NT < 2 || c->last_term == 0) return 0;
   if (c->lt_mask >= 0) return (uint32_t)c->lt_mask;
   if (c->last_term == 1 || B <= LT_MAX_B) return ~1u;   // every diagonal launch J >= 1
+  if (B <= LT_LATE_MAX_B) return (1u << 1) | (1u << 3) | (1u << 6) | (1u << 7);
   return B <= LT_PART_MAX_B ? (1u << 1) | (1u << 3) : 0u;
 }
 bool use_last_term(const tblup_ctx* c, const SysDims& sd, int64_t B) { return last_term_mask(c, sd, B) != 0; }
