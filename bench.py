@@ -39,6 +39,10 @@ CONFIGS = {
 }
 TRAITS = {"config5": 3}
 
+# the bench's own parity bound on the fitness (Pearson r) of every timed individual the CPU
+# baseline covered (the parity tests' FIT_ATOL; north_star asks 1e-5 relative on the EBVs)
+PARITY_ATOL = 1e-9
+
 # BASELINE.json's metric, verbatim
 METRIC = "GBLUP fitness evals/sec (whole node), 2k\u00d750k SNP, DE pop=256; 1/2/4/8 GPUs"
 
@@ -127,7 +131,9 @@ def cpu_baseline(geno, pheno, T, V, genomes, h2, target_s):
     from threadpoolctl import threadpool_limits
     from oracle.blup_oracle import blup
 
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    host_cpus = len(os.sched_getaffinity(0))
+    # at most 16 workers: the GPU box's CPU share per GPU (its affinity mask may show the whole host)
+    cores = max(1, min(16, host_cpus))
     _CPU.update(data=geno.astype(np.float64), pheno=pheno, T=T, V=V, genomes=genomes, h2=h2)
     with threadpool_limits(1):
         t0 = time.perf_counter()
@@ -139,14 +145,19 @@ def cpu_baseline(geno, pheno, T, V, genomes, h2, target_s):
     with ctx.Pool(cores, initializer=_cpu_init) as pool:
         pool.map(_cpu_eval, range(cores))        # warm the workers
         t0 = time.perf_counter()
-        pool.map(_cpu_eval, range(count), chunksize=max(1, count // (4 * cores)))
+        res = pool.map(_cpu_eval, range(count), chunksize=max(1, count // (4 * cores)))
         dt = time.perf_counter() - t0
     _CPU.clear()
-    return {"value": count / dt, "unit": "evals/s", "cores": cores, "kind": "port",
+    # the oracle fitness of every benchmark individual the sample covered (evaluation i is
+    # individual i % pop): the timed GPU fitnesses are checked against these after the timed passes
+    oracle_fit = {i: float(res[i]) for i in range(min(count, len(genomes)))}
+    return {"value": count / dt, "unit": "evals/s", "cores": cores, "host_cpus_affinity": host_cpus,
+            "os_cpu_count": os.cpu_count(), "kind": "port", "_oracle_fit": oracle_fit,
             "sample": f"{count} evaluations of the config workload (k={genomes.shape[1]}"
                       + (f", {pheno.shape[1]} traits: one blup per trait" if pheno.ndim == 2 else "")
                       + ") by the numpy oracle "
-                      f"port of BlupParallelEvaluator.blup, {cores} single-threaded worker processes, {dt:.1f} s"}
+                      f"port of BlupParallelEvaluator.blup, {cores} single-threaded worker processes (of {host_cpus} "
+                      f"CPUs in this process's affinity mask), {dt:.1f} s"}
 
 
 # ----------------------------------------------------------------------------- main
@@ -292,6 +303,19 @@ def main():
         fit = np.concatenate([fit_all[r, :b - a] for r, (a, b) in enumerate(spans)])
     else:
         fit = d_fit.cpu().numpy()[:pop]
+    # the timed fitnesses against the oracle's for every individual the CPU baseline evaluated
+    # (evaluator.py:298-314 restated in oracle/blup_oracle.py): the line proves its own results
+    parity = None
+    if cpu is not None:
+        ofit = cpu.pop("_oracle_fit")
+        idx_cov = np.array(sorted(ofit), dtype=np.int64)
+        ref = np.array([ofit[i] for i in idx_cov])
+        got = fit[idx_cov]
+        both_nan = np.isnan(ref) & np.isnan(got)
+        diff = np.where(both_nan, 0.0, np.abs(got - ref))
+        worst = float(np.nanmax(np.where(np.isnan(diff), np.inf, diff))) if len(diff) else None
+        parity = {"max_abs_fit": worst, "covered": int(len(idx_cov)), "of": int(pop), "atol": PARITY_ATOL,
+                  "oracle": "oracle/blup_oracle.py blup (float64 numpy), the CPU baseline's own evaluations"}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -324,7 +348,8 @@ def main():
     if os.path.isfile(args.pmc_json):
         try:
             pmc = json.load(open(args.pmc_json))
-            if pmc.get("config") == config and dom in pmc.get("per_launch_bytes", {}):
+            if (pmc.get("config") == config and pmc.get("pop_per_gpu", 256) == shard_max and world == 1
+                    and dom in pmc.get("per_launch_bytes", {})):
                 traffic = pmc["per_launch_bytes"][dom]
         except (ValueError, OSError):
             traffic = None
@@ -333,7 +358,16 @@ def main():
     # the live HIP-event one
     rocprof = None
     kname = {"chol_offdiag": "k_chol_offdiag", "chol_diag": "k_chol_diag", "solve": "k_solve"}.get(dom)
-    if kname and config == "config2" and os.path.isfile(args.rocprof_stats) and pd["launches"]:
+    # only when the stats file was taken on this workload: its sidecar (<stats>.meta.json, written
+    # by tools/collect_evidence.sh) names the config and the per-GPU population it ran
+    stats_meta = None
+    try:
+        stats_meta = json.load(open(os.path.splitext(args.rocprof_stats)[0] + ".meta.json"))
+    except (OSError, ValueError):
+        stats_meta = None
+    stats_match = (stats_meta is not None and stats_meta.get("config") == config
+                   and stats_meta.get("pop_per_gpu") == shard_max and world == 1)
+    if kname and stats_match and os.path.isfile(args.rocprof_stats) and pd["launches"]:
         import csv
         tot_ns, calls = 0.0, 0   # every instantiation of the kernel (k_chol_offdiag<true> / <false>, ...)
         with open(args.rocprof_stats) as f:
@@ -352,7 +386,8 @@ def main():
     if os.path.isfile(args.pmc_mfma_json):
         try:
             pm = json.load(open(args.pmc_mfma_json))
-            if pm.get("config") == config and dom in pm.get("per_class", {}):
+            if (pm.get("config") == config and pm.get("pop_per_gpu", 256) == shard_max and world == 1
+                    and dom in pm.get("per_class", {})):
                 mfma_busy = pm["per_class"][dom]["mfma_busy"]
         except (ValueError, OSError, KeyError):
             mfma_busy = None
@@ -417,8 +452,14 @@ def main():
             "gpu_de_step_ms": None if de_ms is None else round(de_ms, 4),
             "host_reference_ms": host_ref,
             "fitness_checksum": float(np.nansum(fit)),
+            "parity_max_abs_fit": None if parity is None else parity["max_abs_fit"],
+            "parity": parity,
         }
         print(json.dumps(line), flush=True)
+        if parity is not None and not (parity["max_abs_fit"] is not None and parity["max_abs_fit"] <= PARITY_ATOL):
+            print(f"bench: GPU fitness differs from the oracle by {parity['max_abs_fit']} > {PARITY_ATOL}",
+                  file=sys.stderr)
+            sys.exit(3)
     eng.close()
     if owns_group:
         tdist.destroy()

@@ -285,6 +285,9 @@ uint32_t last_term_mask(const tblup_ctx* c, const SysDims& sd, int64_t B) {
   return B <= LT_PART_MAX_B ? (1u << 1) | (1u << 3) : 0u;
 }
 bool use_last_term(const tblup_ctx* c, const SysDims& sd, int64_t B) { return last_term_mask(c, sd, B) != 0; }
+// bit J of a last-term mask; a kernel-form system can have NT > 32 tile columns (n_T > 4096), and
+// there the all-launches mask (~1u, J >= 1) keeps its meaning while a sparse mask names none
+inline bool lt_bit(uint32_t m, int J) { return J < 32 ? ((m >> J) & 1u) != 0 : m == ~1u; }
 
 size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int64_t B, int64_t sum_k,
                    bool with_ebv) {
@@ -393,13 +396,16 @@ FoldTab single_fold(const Split& sp, int64_t B) {
 // systems' splits when they are not all sp (fold-fused evaluation; sp is then fold 0).
 // stop_stage: 0 the whole pipeline; 1 / 2 debug readbacks (K, L); 3 the solve only, through the
 // one-workgroup k_solve, on the factor an earlier run_chunk of the same chunk left in the same
-// carve (host entries, after that run's chained solve gave up a wait: bit-identical results).
+// carve (host entries, after that run's chained solve gave up a wait: bit-identical results);
+// 4 the whole pipeline with the one-workgroup k_solve instead of the chained solve (a per-call
+// choice: the context's policy is not touched).
 int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& sd, hipStream_t s,
               const int64_t* d_idx, const int64_t* d_off, const int64_t* h_off, int64_t B, double h2,
               int branch, Carve& cv, double* d_fit, double* d_ebv, int stop_stage, double** K_out,
               double** z_out, const FoldTab* ftp = nullptr) {
   const FoldTab ft = ftp ? *ftp : single_fold(sp, B);
   const bool redo = stop_stage == 3;
+  const bool chain = stop_stage != 4 && use_chain(c, sd, B, d.nt);
   c->last_chain_seq = 0;
   double grm_flops = 0.0, gather_bytes = 0.0, stats_bytes = 0.0;
   const double tri = (double)d.nT * (d.nT + 1) / 2.0 + (double)d.nV * d.nT;
@@ -479,7 +485,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     int64_t nwg = 0;
     for (int J = 0; J < sd.NT; ++J) nwg += B * (1 + plan[J].ndd) + plan[J].ne + DTR_RECS + offdiag_grid(plan[J], B);
     if (use_st) nwg += B * sd.NT * (sd.NT + 1) / 2;
-    if (use_chain(c, sd, B, d.nt)) nwg += B * sd.NT;   // chained solve units
+    if (chain) nwg += B * sd.NT;   // chained solve units
     if (int rc = dev_alloc(c, c->wgt, (size_t)nwg * WGT_REC * 8)) return rc;
     HIPCHK(hipMemsetAsync(c->wgt.p, 0, (size_t)nwg * WGT_REC * 8, s));
     wgt = (uint64_t*)c->wgt.p;
@@ -523,7 +529,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     const OffPlan& p = plan[J];
     // algorithmic fp64 work: the L = J-1 SYRK term of the diagonal tile, potrf + trtri,
     // forward-substitution GEMV (the exact system tiles are counted under KC_GRM)
-    const bool qd = Qb && ((ltm >> J) & 1u), qo = Qb && ((ltm >> (J + 1)) & 1u);
+    const bool qd = Qb && lt_bit(ltm, J), qo = Qb && lt_bit(ltm, J + 1);
     const double lt_d = qd ? 0.0 : std::min(jt, 1.0);   // the last SYRK term's share of this launch
     // (+ the D-units when they run in this launch: 128^3 per L < J, as in the off-diagonal launch)
     // (+ the E-units: one 2*128^3 GEMM1 term each, moved out of launch J's T-units)
@@ -563,7 +569,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
                                  kbar * (double)(d.nT + d.nV));
   SolveChain ch{};
   const SolveChain* chp = nullptr;
-  if (!redo && use_chain(c, sd, B, d.nt)) {
+  if (!redo && chain) {
     const size_t fbytes = ((size_t)B * chain_flags(sd.NT) + CHAIN_ERR_RING + 1) * 4;
     if (c->chain.bytes < fbytes || c->chain_seq >= INT32_MAX - 1) {
       HIPCHK(hipStreamSynchronize(s));   // the flags may still be read by an earlier chained solve
@@ -1169,20 +1175,15 @@ int tblup_eval_folds(tblup_ctx* c, const int* split_ids, int n_splits, const int
           return rc;
         seqs.push_back(c->last_chain_seq);
       } else {
-        const int keep = c->solve_chain;
-        if (pass) c->solve_chain = 0;
         for (int f = 0; f < n_splits; ++f) {
           Carve cv = head;   // every fold reuses the same workspace after the inputs, in stream order
           const SysDims sd = choose_sys(c, ds[f], hoff.data(), B, branch, c->form_pref);
-          const int rc = run_chunk(c, *sps[f], ds[f], sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv,
-                                   d_fit + (int64_t)f * B, nullptr, 0, nullptr, nullptr);
-          seqs.push_back(c->last_chain_seq);
-          if (rc) {
-            c->solve_chain = keep;
+          // the recovery pass runs every fold with k_solve (stop_stage 4: a per-call choice)
+          if (int rc = run_chunk(c, *sps[f], ds[f], sd, c->stream, d_idx, d_off, hoff.data(), B, h2, branch, cv,
+                                 d_fit + (int64_t)f * B, nullptr, pass ? 4 : 0, nullptr, nullptr))
             return rc;
-          }
+          seqs.push_back(c->last_chain_seq);
         }
-        c->solve_chain = keep;
       }
       for (int f = 0; f < n_splits; ++f)
         HIPCHK(hipMemcpyAsync(fitness + (int64_t)f * batch + b0, d_fit + (int64_t)f * B, (size_t)B * 8,

@@ -234,8 +234,12 @@ int tblup_de_step_device_async_mix(tblup_ctx* c, const int32_t* strategies, cons
     clear_error();
     return fail(TBLUP_ERR_ARG, "null strategies/F/cr");
   }
-  return de_step_async(c, strategies[0], strategies, F, cr, d_parents, pop, L, ld, donors, fixed, F[0], cr[0], clip,
-                       clip_hi, mt_key, mt_pos, d_children, ldc, stream);
+  // element 0 is read only for a non-empty population (validate_de rejects pop < 1); the scalar
+  // slots are placeholders when per-individual arrays are given
+  const bool any = pop >= 1;
+  return de_step_async(c, any ? strategies[0] : TBLUP_DE_RAND_1, strategies, F, cr, d_parents, pop, L, ld, donors,
+                       fixed, any ? F[0] : 0.0, any ? cr[0] : 0.0, clip, clip_hi, mt_key, mt_pos, d_children, ldc,
+                       stream);
 }
 
 int tblup_de_state_wait(tblup_ctx* c, uint32_t* mt_key, int32_t* mt_pos) {

@@ -30,18 +30,16 @@ def validate_genotypes(data):
     Raises ValueError for anything else (e.g. imputed dosages), instead of
     silently changing the arithmetic.
     """
-    g = np.asarray(data)
+    from .panel import convert_rows
+    g = data if isinstance(data, np.ndarray) else np.asarray(data)
     if g.ndim != 2:
         raise ValueError("genotype matrix must be 2-D (animals x SNPs)")
     if g.dtype == np.int8:
-        ok = g.size == 0 or (int(g.min()) >= 0 and int(g.max()) <= 2)
-        out = g
-    else:
-        ok = bool(np.all((g == 0) | (g == 1) | (g == 2)))
-        out = g.astype(np.int8) if ok else None
-    if not ok:
-        raise ValueError("genotypes must take values in {0, 1, 2} for the MI355X evaluator")
-    return np.ascontiguousarray(out)
+        if g.size and (int(g.min()) < 0 or int(g.max()) > 2):
+            raise ValueError("genotypes must take values in {0, 1, 2} for the MI355X evaluator")
+        return np.ascontiguousarray(g)
+    # converted by blocks of rows (tblup_amd.panel): no full-size boolean or float temporaries
+    return convert_rows(g)
 
 
 def concat_genomes(genomes):

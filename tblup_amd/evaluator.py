@@ -103,9 +103,17 @@ class ParallelEvaluator(Evaluator):
 
     def _open_engine(self):
         from .engine import GpuBlupEngine  # loads libtblup_gpu.so or raises ImportError
-        data = np.load(self.data_path)
+        from .panel import load_panel
+        # the float64 .npy streamed into int8 once per node (a /dev/shm segment every rank maps),
+        # not a float64 copy per rank as evaluator.py:188 / 215-216 load it
+        data = load_panel(self.data_path, self._device() if self._nccl() else None)
         labels = np.load(self.labels_path)
         return GpuBlupEngine(data, labels, device=self._device())
+
+    @staticmethod
+    def _nccl():
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
 
     def __enter__(self):
         if init_from_env(self._device()):
@@ -113,7 +121,8 @@ class ParallelEvaluator(Evaluator):
         if self.engine is None:
             self.engine = self._open_engine()
         from .keystore import freeze_heap
-        freeze_heap()   # the imported modules out of python's full collections (a 93 ms pause)
+        # the imported modules out of python's full collections (a 93 ms pause); undone in __exit__
+        self._froze_heap = freeze_heap()
         return self
 
     def __exit__(self, exc_type, exc_val, exc_tb):
@@ -123,6 +132,10 @@ class ParallelEvaluator(Evaluator):
         if self._owns_group:
             self._owns_group = False
             destroy()
+        if getattr(self, "_froze_heap", False):
+            from .keystore import thaw_heap
+            self._froze_heap = False
+            thaw_heap()
 
     def genomes_to_evaluate(self, population):
         raise NotImplementedError()
@@ -440,13 +453,15 @@ class MonteCarloCVBlupParallelEvaluator(BlupParallelEvaluator):
 
 def _gather_or_raise(evaluate, shape, n_total, device):
     """This rank's shard evaluated, then the all-gather (torch.distributed).  A failure of the
-    shard's evaluation (an index outside [-P, P) in one rank's genomes) would otherwise raise on
-    that rank only and leave its peers waiting in the collective: the error code travels in the
-    same all-gather, and every rank raises together."""
+    shard's evaluation -- an index outside [-P, P) in one rank's genomes, or any other exception
+    (a torch / ctypes error, a ValueError from a genome's shape, device memory) -- would otherwise
+    raise on that rank only and leave its peers waiting in the collective: the error code travels
+    in the same all-gather, every rank leaves it together, the failing rank re-raises its own
+    exception and the others raise TblupError (TblupIndexError for an index error)."""
     err = None
     try:
         local = evaluate()
-    except _native.TblupError as e:
+    except Exception as e:   # noqa: BLE001 -- re-raised below, after the collective
         err = e
         local = np.full(shape, np.nan)
     code = 0 if err is None else (1 if isinstance(err, IndexError) else 2)

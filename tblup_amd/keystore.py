@@ -26,6 +26,7 @@ buffer protocol) meets a read-only array and raises.  A stale or replaced genome
 read from the host.  Device memory is plumbing here: torch tensors on the context's
 device.
 """
+import os
 import weakref
 
 import numpy as np
@@ -167,13 +168,29 @@ def freeze_heap():
     heap took 93 ms, every ~15 DE generations at pop 1024 (profiles/r05_generation_gc.jsonl); after
     the freeze it walks only the objects created since (the population, its genomes).  Called
     where the drop-ins start up (ParallelEvaluator.__enter__, the first GPU DE step); objects alive
-    at that moment are never collected as cyclic garbage (reference counting still frees them)."""
+    at that moment are never collected as cyclic garbage (reference counting still frees them).
+
+    A process-wide side effect, so it can be switched off (TBLUP_GC_FREEZE=0) and is undone by
+    thaw_heap() -- ParallelEvaluator.__exit__ calls it -- which moves the frozen objects back into
+    the collected generations.  Returns True when this call froze the heap."""
     global _FROZEN
-    if not _FROZEN:
+    if _FROZEN or os.environ.get("TBLUP_GC_FREEZE", "1") == "0":
+        return False
+    import gc
+    _FROZEN = True
+    gc.collect()
+    gc.freeze()
+    return True
+
+
+def thaw_heap():
+    """Undo freeze_heap (gc.unfreeze): the permanent generation back into the oldest collected
+    one, so the host application's objects frozen with the imports are collectable again."""
+    global _FROZEN
+    if _FROZEN:
         import gc
-        _FROZEN = True
-        gc.collect()
-        gc.freeze()
+        gc.unfreeze()
+        _FROZEN = False
 
 
 _STREAMS = {}

@@ -116,8 +116,48 @@ def run_rank_error(rank, world, port, out_dir):
         out["raised"] = None
     except _native.TblupIndexError as e:
         out["raised"] = type(e).__name__
+    # any other exception on one rank (a torch / ValueError / ctypes failure): the
+    # failing rank re-raises its own error, the other raises TblupError, nobody hangs
+    def shard_other():
+        if rank == 0:
+            raise ValueError("genome of the wrong shape")
+        return np.ones(4)
+    try:
+        _gather_or_raise(shard_other, (4,), 8, None)
+        out["raised_other"] = None
+    except Exception as e:   # noqa: BLE001
+        out["raised_other"] = type(e).__name__
     full = _gather_or_raise(lambda: np.full(4, rank + 0.5), (4,), 8, None)   # and a clean call after it
     out["clean"] = [float(x) for x in full]
     json.dump(out, open(os.path.join(out_dir, f"err_rank{rank}.json"), "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_panel_load(rank, world, port, path, out_dir):
+    """Node-shared panel start-up (tblup_amd.panel.load_panel): both ranks get
+    the int8 panel while their peak RSS grows by far less than the float64 file."""
+    import resource
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import numpy as np
+    import torch.distributed as dist
+
+    from tblup_amd.panel import load_panel
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    before = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
+    arr = load_panel(path)
+    # every row read (as the GPU context's copy reads them), summed in blocks of rows
+    checksum = sum(int(arr[i:i + 50].sum(dtype=np.int64)) for i in range(0, arr.shape[0], 50))
+    rows = arr.shape[0]
+    peak = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
+    shared = not isinstance(arr, np.ndarray) or isinstance(arr, np.memmap)
+    json.dump({"grow": peak - before, "dtype": str(arr.dtype), "shape": list(arr.shape), "rows": rows,
+               "shared": bool(shared), "checksum": checksum,
+               "leftover": sorted(f for f in os.listdir("/dev/shm") if f.startswith("tblup_panel_"))},
+              open(os.path.join(out_dir, f"panel_rank{rank}.json"), "w"))
     dist.barrier()
     dist.destroy_process_group()

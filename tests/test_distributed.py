@@ -97,4 +97,36 @@ def test_rank_failure_raises_on_every_rank(tmp_path):
         assert res[r]["status_max"] == [1, 5]
         assert res[r]["full"] == [0.0] * 4 + [1.0] * 3
         assert res[r]["raised"] == "TblupIndexError"
+        assert res[r]["raised_other"] == ("ValueError" if r == 0 else "TblupError")
         assert res[r]["clean"] == [0.5] * 4 + [1.5] * 4
+
+
+def test_two_rank_panel_start_up_is_node_shared(tmp_path):
+    """the float64 .npy panel is streamed into int8 once per node (a /dev/shm
+    segment both ranks map) instead of loaded whole as float64 by every rank: each rank's peak RSS
+    grows by well under the float64 panel's size, both see the same int8 panel, and the segment's
+    name is gone once both hold it."""
+    from tests import dist_worker
+    rng = np.random.default_rng(9)
+    n, p = 1000, 40_000
+    g = rng.integers(0, 3, size=(n, p)).astype(np.int8)
+    path = str(tmp_path / "geno.npy")
+    np.save(path, g.astype(np.float64))          # 320 MB of float64, as the reference stores it
+    f64 = n * p * 8
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=dist_worker.run_panel_load, args=(r, 2, port, path, str(tmp_path))) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+        assert pr.exitcode == 0
+    res = [json.load(open(tmp_path / f"panel_rank{r}.json")) for r in range(2)]
+    want = int(g.astype(np.int64).sum())
+    print("peak RSS growth per rank (bytes):", [res[r]["grow"] for r in range(2)], "float64 panel:", f64)
+    for r in range(2):
+        assert res[r]["dtype"] == "int8" and res[r]["shape"] == [n, p] and res[r]["rows"] == n
+        assert res[r]["checksum"] == want
+        assert res[r]["shared"]
+        assert res[r]["grow"] < f64 // 2, (r, res[r]["grow"], f64)
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("tblup_panel_")]

@@ -122,3 +122,25 @@ def test_leading_padding_matches_trailing(panel, gpu):
     for i in range(len(genomes)):
         f, _ = O.blup_grm_form(genomes[i], panel["T"], panel["V"], panel["geno"], panel["pheno"], 0.4)
         assert abs(lead[0][i] - f) <= 1e-9, i
+
+
+def test_last_term_mask_past_32_columns(gpu):
+    """a kernel-form system with more than 32 tile columns (n_T = 4224: NT = 33) at
+    B <= 64, where the automatic last-term mask is every diagonal launch J >= 1 -- including
+    J = 32, whose bit a 32-bit shift used to wrap to bit 0.  Every setting gives the same bits
+    (the last term moves between launches on the same MFMA chains), equal to the oracle."""
+    rng = np.random.default_rng(33)
+    n, p = 4400, 6000
+    geno = O.synth_geno(rng, n, p)
+    pheno = rng.standard_normal(n)
+    perm = rng.permutation(n)
+    T, V = perm[:4224], perm[4224:4324]
+    genomes = [rng.choice(p, 4300, replace=False), rng.choice(p, 4250, replace=False)]   # k > n_T: kernel form
+    ref = _evaluate(geno, pheno, genomes, T, V, {"TBLUP_LAST_TERM": "0"})
+    for env in ({"TBLUP_LAST_TERM": "-1"}, {"TBLUP_LAST_TERM": "1"}):
+        got = _evaluate(geno, pheno, genomes, T, V, env)
+        np.testing.assert_array_equal(got[0], ref[0])
+        np.testing.assert_array_equal(got[1], ref[1])
+    f, e = O.blup(genomes[0], T, V, geno.astype(np.float64), pheno, 0.4, return_ebv=True)
+    assert abs(ref[0][0] - f) <= 1e-9
+    assert np.max(np.abs(ref[1][0] - e)) <= 1e-9 * np.max(np.abs(e))

@@ -7,6 +7,10 @@ for c in config3 config4 config5 pop32 pop64 pop128; do
   [ -f $O/bench_${c}_$T.log ] && tail -1 $O/bench_${c}_$T.log > $P/${T}_bench_$c.jsonl
 done
 cp $O/prof_$T/trace_kernel_stats.csv $P/${T}_kernel_stats.csv
+# the bench's rocprof-timed roofline reads profiles/kernel_stats.csv only for the workload its
+# sidecar names (tools/gpu_evidence.sh profiles the default bench: config 2, pop 256 on one GPU)
+cp $O/prof_$T/trace_kernel_stats.csv $P/kernel_stats.csv
+echo '{"config": "config2", "pop_per_gpu": 256, "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline", "source": "'$T'"}' > $P/kernel_stats.meta.json
 cp $O/prof_$T/trace_domain_stats.csv $P/${T}_domain_stats.csv
 cp $O/prof_$T/trace_kernel_trace.csv $P/${T}_kernel_trace.csv
 cp $(find $O/pmcf_$T -name "*counter_collection.csv" | head -1) $P/${T}_pmc_fetch.csv

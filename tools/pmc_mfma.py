@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--config", default="config2")
+    ap.add_argument("--pop", type=int, default=256, help="per-GPU population the profiled bench ran")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
     per = defaultdict(lambda: defaultdict(dict))   # class -> dispatch -> counter -> value
@@ -63,7 +64,7 @@ def main():
                         "grbm_quotient_ghz": round(clk / 1e9, 3),
                         "normalised_by": "wall time x the long dispatches' clock %.3f GHz" % (ref / 1e9),
                         "dispatches": nd}
-    json.dump({"config": args.config, "source": args.csv,
+    json.dump({"config": args.config, "pop_per_gpu": args.pop, "source": args.csv,
                "note": "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x the dispatch's cycles): cycles = "
                        "GRBM_GUI_ACTIVE / 8 XCDs for dispatches >= 0.2 ms whose quotient is <= 2.4 GHz, else wall time x the clock those held",
                "per_class": out}, open(args.out, "w"), indent=1)

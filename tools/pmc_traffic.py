@@ -41,11 +41,12 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("--config", default="config2")
+    ap.add_argument("--pop", type=int, default=256, help="per-GPU population the profiled bench ran")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch = per_class(a.fetch_csv, "FETCH_SIZE")
     write = per_class(a.write_csv, "WRITE_SIZE")
-    out = {"config": a.config, "source": [a.fetch_csv, a.write_csv],
+    out = {"config": a.config, "pop_per_gpu": a.pop, "source": [a.fetch_csv, a.write_csv],
            "note": "bytes per launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024, averaged over launches",
            "per_launch_bytes": {}, "per_launch_fetch_bytes": {}, "per_launch_write_bytes": {}, "launches": {}}
     for cls in CLASSES.values():
