@@ -38,7 +38,7 @@ import numpy as np
 
 from . import _native
 from .distributed import shard_range, world
-from .keystore import DeviceKeyStore, freeze_heap, track, work_stream
+from .keystore import DeviceKeyStore, TrackedGenome, freeze_heap, track, track_rows, work_stream
 from .shmrows import RING as _SHM
 
 
@@ -317,11 +317,16 @@ class _RowBlocks:
     def rows(self, block):
         import weakref
         self._reg[id(block)] = weakref.ref(block)
-        rows = [track(block[i], lock=False) for i in range(block.shape[0])]
+        rows = track_rows(block)
         block.flags.writeable = False   # the rows' private aliases are the only writable ones
         return rows
 
     def _block_of(self, g):
+        b = g._blk if type(g) is TrackedGenome else None   # set by track_rows: no base walk
+        if b is not None:
+            r = self._reg.get(id(b))
+            if r is not None and r() is b:
+                return b
         b = g
         while isinstance(b, np.ndarray):
             r = self._reg.get(id(b))
@@ -412,6 +417,17 @@ _BLOCK_MAX = int(os.environ.get("TBLUP_BLOCK_ROWS_MB", "1024")) << 20
 _PINNED_ROWS_MAX = int(os.environ.get("TBLUP_PINNED_ROWS_MB", "2048")) << 20
 
 
+_DC_INDEX = {}
+
+
+def _deepcopy_is_index(dc):
+    """Whether `dc` is IndexIndividual.__deepcopy__ (the reference's, individual.py:110-118)."""
+    hit = _DC_INDEX.get(dc)
+    if hit is None:
+        hit = _DC_INDEX[dc] = getattr(dc, "__qualname__", "") == "IndexIndividual.__deepcopy__"
+    return hit
+
+
 def _copy_individual(indv):
     """deepcopy(indv) as the reference's evolvers take it (evolver.py:130, 208), without
     copying the internal genome the caller replaces right after (set_internal_genome):
@@ -423,7 +439,10 @@ def _copy_individual(indv):
     # the class's own __deepcopy__ (individual.py:43-59, 110-118) called directly: copy.deepcopy's
     # dispatch and throwaway memo bookkeeping cost a third of the time for the same object
     dc = getattr(type(indv), "__deepcopy__", None)
-    indv._genome = _NO_GENOME
+    # IndexIndividual.__deepcopy__ (individual.py:110-118) only deep-copies the placeholder: None is
+    # an atomic for copy.deepcopy (returned as is), where an empty array's deepcopy took ~half the
+    # copy's time; other classes' __deepcopy__ may read the genome, so they get an empty array
+    indv._genome = None if _deepcopy_is_index(dc) else _NO_GENOME
     try:
         return dc(indv, {}) if dc is not None else deepcopy(indv)
     finally:

@@ -41,6 +41,7 @@ class TrackedGenome(np.ndarray):
     _owner = None    # the recorded array this view belongs to (None: it is the owner)
     _stale = False
     _w = None        # owner only: a writable plain alias of its memory, held by nobody else
+    _blk = None      # track_rows: the 2-D block this row belongs to (the evolver's page-locked blocks)
 
     def __array_finalize__(self, obj):
         if isinstance(obj, TrackedGenome) and obj._tracked() and not self.flags.owndata:
@@ -158,6 +159,21 @@ def track(a, lock=True):
     return t
 
 
+def track_rows(block):
+    """track() for every row of a 2-D float64 block in one pass: each row its own owner (marking
+    one row stale leaves the others alone) with a writable alias taken from one writable view of
+    the block (list(view) slices the rows without per-row indexing: 2.8 -> 1.0 ms for 1024 rows).
+    The caller locks the block itself afterwards, as with track(lock=False)."""
+    wl = list(block.view(np.ndarray))
+    tb = block.view(TrackedGenome)
+    tb.flags.writeable = False      # the rows inherit it
+    rows = list(tb)
+    for t, w in zip(rows, wl):
+        t._w = w
+        t._blk = block
+    return rows
+
+
 _FROZEN = False
 
 
@@ -241,9 +257,15 @@ class DeviceKeyStore:
         parents recorded from other arrays are not tracked and are read from the host).
         Individuals that derive their internal genome (Coevolution appends its length) are not
         recorded and are read from the host."""
-        for i, indv in enumerate(individuals):
-            g = self._key_array(indv)
-            if g is None or g is not arrays[i]:
+        ent = self._entries
+        for i, (indv, a) in enumerate(zip(individuals, arrays)):
+            g = getattr(indv, "_genome", None)
+            if g is not a or g is None:
+                continue
+            if type(g) is TrackedGenome and not g._stale:   # the common case, inlined
+                ent[indv.uid] = (tensor, i, weakref.ref(g), getattr(indv, "length", None))
+                continue
+            if not isinstance(g, np.ndarray):
                 continue
             if not isinstance(g, TrackedGenome):
                 # a genome the evolver did not create (the initial population): adopt it as a
