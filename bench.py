@@ -160,6 +160,18 @@ def cpu_baseline(geno, pheno, T, V, genomes, h2, target_s):
                       f"CPUs in this process's affinity mask), {dt:.1f} s"}
 
 
+def fitness_parity(fit, oracle_fit, pop):
+    """Max |GPU - oracle| fitness over the individuals the CPU baseline evaluated (both NaN counts
+    as equal -- scipy's pearsonr of a constant prediction; one NaN is a mismatch: inf)."""
+    idx_cov = np.array(sorted(oracle_fit), dtype=np.int64)
+    ref = np.array([oracle_fit[i] for i in idx_cov], dtype=np.float64)
+    got = np.asarray(fit, dtype=np.float64)[idx_cov]
+    diff = np.where(np.isnan(ref) & np.isnan(got), 0.0, np.abs(got - ref))
+    worst = float(np.max(np.where(np.isnan(diff), np.inf, diff))) if len(diff) else None
+    return {"max_abs_fit": worst, "covered": int(len(idx_cov)), "of": int(pop), "atol": PARITY_ATOL,
+            "oracle": "oracle/blup_oracle.py blup (float64 numpy), the CPU baseline's own evaluations"}
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -307,15 +319,7 @@ def main():
     # (evaluator.py:298-314 restated in oracle/blup_oracle.py): the line proves its own results
     parity = None
     if cpu is not None:
-        ofit = cpu.pop("_oracle_fit")
-        idx_cov = np.array(sorted(ofit), dtype=np.int64)
-        ref = np.array([ofit[i] for i in idx_cov])
-        got = fit[idx_cov]
-        both_nan = np.isnan(ref) & np.isnan(got)
-        diff = np.where(both_nan, 0.0, np.abs(got - ref))
-        worst = float(np.nanmax(np.where(np.isnan(diff), np.inf, diff))) if len(diff) else None
-        parity = {"max_abs_fit": worst, "covered": int(len(idx_cov)), "of": int(pop), "atol": PARITY_ATOL,
-                  "oracle": "oracle/blup_oracle.py blup (float64 numpy), the CPU baseline's own evaluations"}
+        parity = fitness_parity(fit, cpu.pop("_oracle_fit"), pop)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
