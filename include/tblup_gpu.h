@@ -137,8 +137,11 @@ int tblup_eval_batch_device(tblup_ctx* ctx, int split_id, const int64_t* d_idx,
  * k folds, tblup/evaluator.py:509-537, whose fitness is the mean over folds; or any split set):
  * fitness is n_splits x batch row-major (row f = split_ids[f]).  The splits' evaluations are
  * enqueued back to back on one stream with one upload of the index lists and one
- * synchronisation, instead of one tblup_eval_batch round trip per fold.  Same numbers as
- * tblup_eval_batch per split, bit for bit.  Host pointers, synchronous.
+ * synchronisation, instead of one tblup_eval_batch round trip per fold.  When the splits partition
+ * one animal set (IntraGCV's folds), the exact genotype products are shared: in the SNP-space form
+ * C_{T_f} = C_{T_all} - C_{V_f}, in the kernel (GRM) form one A_R A_R^T per individual that every
+ * fold's system reads its counts from.  Same numbers as tblup_eval_batch per split, bit for bit.
+ * Host pointers, synchronous.
  */
 int tblup_eval_folds(tblup_ctx* ctx, const int* split_ids, int n_splits, const int64_t* idx, const int64_t* offsets,
                      int64_t batch, double h2, int branch, double* fitness);

@@ -11,6 +11,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "capi_ctx.h"
@@ -512,6 +513,13 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     cl.stats = nullptr;
     if (rc) return rc;
   } else {
+    if (ft.gsh) {
+      // kernel-form folds: every individual's A_R A_R^T once (int ops 2 x nRp^2 x k / 2 + the diagonal tiles)
+      const double NR = (double)(d.nRp / TILE);
+      const double fgs = (double)ft.bpf * NR * (NR + 1) / 2.0 * 2.0 * 128.0 * 128.0 * kbar;
+      rc = timed(c, s, KC_GRM, fgs, (double)ft.bpf * d.nRp * d.nRp * 4.0, [&] { return launch_gshare(cl, s); });
+      if (rc) return rc;
+    }
     // int ops of the diagonal GRM tiles J < 2 (J >= 2 run inside the column-0 off-diagonal launch)
     const double nJ = (double)std::min(sd.NT, 2);
     const double fg = (double)B * nJ * 128.0 * 129.0 * cbar;
@@ -692,6 +700,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_FOLD_FUSE")) c->fold_fuse = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_SYS_ST")) c->sys_st = std::max(-1, std::min(1, atoi(e)));
+  if (const char* e = getenv("TBLUP_FOLD_GSHARE")) c->fold_gshare = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_DIAG_E")) c->diag_e = std::max(-1, std::min(2, atoi(e)));
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
@@ -785,6 +794,8 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   sp->nRp = sp->nTp + sp->nVp;
   sp->rows.assign(train, train + nT);
   sp->rows.insert(sp->rows.end(), valid, valid + nV);
+  sp->train.assign(train, train + nT);
+  sp->valid.assign(valid, valid + nV);
   std::sort(sp->rows.begin(), sp->rows.end());
   std::vector<int32_t> rowmap(sp->nRp, -1);
   for (int64_t i = 0; i < nT; ++i) rowmap[i] = (int32_t)train[i];
@@ -1014,6 +1025,22 @@ static bool fold_fusable(const tblup_ctx* c, const std::vector<Split*>& sps, con
   return true;   // either form: every system reads its own split through the FoldTab
 }
 
+// Kernel form, folds partitioning one animal set (IntraGCV): the systems' int8 counts come from one
+// A_R A_R^T per individual over fold 0's split rows (k_gshare; FoldTab::gsh) -- the fold systems'
+// training rows are all rows of fold 0's split -- instead of one int8 GEMM per system.  The counts
+// are the same exact integers, so the results are bit-identical (TBLUP_FOLD_GSHARE=0 for A/B).
+static bool fold_gshare(const tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd) {
+  if (sd.form != FORM_DUAL || !c->fold_share || !c->fold_gshare || sps.size() < 2) return false;
+  for (const Split* sp : sps)
+    if (sp->rows != sps[0]->rows || (int64_t)sp->train.size() != sp->nT || (int64_t)sp->valid.size() != sp->nV)
+      return false;
+  return true;
+}
+static size_t gshare_bytes(const std::vector<Split*>& sps, int64_t B) {
+  const int64_t nRp = sps[0]->nRp, nTp = sps[0]->nTp, F = (int64_t)sps.size();
+  return (size_t)round_up(B * nRp * nRp * 4, 256) + (size_t)round_up(F * nTp * 4, 256) + 512;
+}
+
 // The fused chunk: the index lists replicated per fold (F x sum_k, device to device), the fused
 // offsets built on the device, then run_chunk over F x B systems.
 static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd, hipStream_t s,
@@ -1036,6 +1063,35 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
   ft.nf = (int)F;
   ft.share = c->fold_share;
   for (int64_t f = 1; f < F; ++f) ft.share = ft.share && sps[f]->rows == sps[0]->rows;
+  if (fold_gshare(c, sps, sd) && stop_stage != 3) {
+    // the fold row maps: system row r of fold f -> fold 0's split row of the same animal
+    const int64_t nRp = sps[0]->nRp, nTp = sps[0]->nTp, nT = sps[0]->nT;
+    std::unordered_map<int64_t, int32_t> pos0;
+    pos0.reserve((size_t)(sps[0]->nT + sps[0]->nV) * 2);
+    for (int64_t i = 0; i < sps[0]->nT; ++i) pos0[sps[0]->train[i]] = (int32_t)i;
+    for (int64_t j = 0; j < sps[0]->nV; ++j) pos0[sps[0]->valid[j]] = (int32_t)(nTp + j);
+    std::vector<int32_t>& hm = c->gmap_host;
+    HIPCHK(hipStreamSynchronize(s));   // the previous chunk's map copy may still read hm
+    hm.assign((size_t)(F * nTp), -1);
+    for (int64_t f = 0; f < F; ++f)
+      for (int64_t r = 0; r < nT; ++r) {
+        const auto it = pos0.find(sps[f]->train[r]);
+        if (it == pos0.end()) return fail(TBLUP_ERR_STATE, "internal error: fold rows are not one animal set");
+        hm[(size_t)(f * nTp + r)] = it->second;
+      }
+    ft.gsh = cv.take<int32_t>((size_t)(B * nRp * nRp));
+    int32_t* dmap = cv.take<int32_t>((size_t)(F * nTp));
+    if (int rc = ws_check(c, cv)) return rc;
+    HIPCHK(hipMemcpyAsync(dmap, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, s));
+    ft.gmap = dmap;
+    ft.gsh_ld = nRp;
+    ft.gmap_ld = nTp;
+  } else if (fold_gshare(c, sps, sd)) {
+    // the solve-only re-run: the counts are not read again, but the carve must match the first pass
+    const int64_t nRp = sps[0]->nRp, nTp = sps[0]->nTp;
+    cv.take<int32_t>((size_t)(B * nRp * nRp));
+    cv.take<int32_t>((size_t)(F * nTp));
+  }
   for (int64_t f = 0; f < F; ++f) {
     ft.gpk[f] = (const uint8_t*)sps[f]->gpk.p;
     ft.gs[f] = (const int8_t*)sps[f]->geno.p;
@@ -1054,7 +1110,8 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
 static size_t fused_bytes(const tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd, int64_t B,
                           int64_t sum_k) {
   const int64_t F = (int64_t)sps.size();
-  return chunk_bytes(c, dims_of(c, *sps[0]), sd, F * B, F * sum_k, false) + (size_t)(sum_k + B + 1) * 8 + 1024;
+  return chunk_bytes(c, dims_of(c, *sps[0]), sd, F * B, F * sum_k, false) + (size_t)(sum_k + B + 1) * 8 + 1024 +
+         (fold_gshare(c, sps, sd) ? gshare_bytes(sps, B) : 0);
 }
 
 static int validate_splits(tblup_ctx* c, const int* split_ids, int n_splits, std::vector<Split*>& sps) {

@@ -434,6 +434,16 @@ __device__ __forceinline__ const uint8_t* row_packed(const CholArgs& a, int64_t 
   return a.ft.gpk[fold_of(a.ft, b)] + p * a.gs_row;
 }
 
+// Kernel form, folds sharing one animal set (FoldTab::gsh): the exact count A_r . A_c of system
+// rows r, c (< n_Tp) of system s, from its individual's A_R A_R^T (k_gshare); padding rows count 0,
+// as their zero panel rows do
+__device__ __forceinline__ int32_t gsh_count(const CholArgs& a, int64_t s, int64_t r, int64_t c) {
+  const FoldTab& ft = a.ft;
+  const int32_t* mp = ft.gmap + (int64_t)fold_of(ft, s) * ft.gmap_ld;
+  const int32_t mr = mp[r], mc = mp[c];
+  return (mr >= 0 && mc >= 0) ? ft.gsh[((s % ft.bpf) * ft.gsh_ld + mr) * ft.gsh_ld + mc] : 0;
+}
+
 // ---------------------------------------------------------------------------
 // Diagonal tile T_J = K_JJ - sum_{L<J} L_JL L_JL^T is assembled from pieces that are
 // computed OFF the column-to-column critical path:
@@ -1266,6 +1276,12 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
       const int row = 16 * w + (l >> 2), pos = l & 3;
       i8_tt2d_pk64<4>(row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
                       row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, lds8, cnt);
+    } else if (!(a.skip & 32) && a.ft.gsh) {
+      // kernel-form folds: the counts of the individual's shared A_R A_R^T (same integers)
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cnt[cb][r] = gsh_count(a, b, j0 + 16 * cb + (l >> 4) + 4 * r, i0 + il);
     } else if (!(a.skip & 32)) {
       const int row = 16 * w + (l >> 2), pos = l & 3;
       i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
@@ -1527,6 +1543,13 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
   for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
   if (a.skip & 1) {
     __syncthreads();
+  } else if (a.ft.gsh) {
+    // kernel-form folds: the lower blocks' counts from the individual's shared A_R A_R^T
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+      if (cb >= wc)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cnt[cb][r] = gsh_count(a, b, j0 + 16 * cb + (l >> 4) + 4 * r, j0 + 16 * wc + (l & 15));
   } else if (a.form == FORM_PRIMAL) {
     const uint8_t* rp = row_packed(a, b, j0 + row);
     const uint8_t* sa = rp + 16 * (pos ^ ((row >> 2) & 3));
@@ -2321,6 +2344,48 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
   a.wgt = nullptr;
   const int nJ = std::min(c.sd.NT, 2);
   hipLaunchKernelGGL(k_diag_grm8, dim3((unsigned)(c.B * nJ)), dim3(OTH), 0, s, a, nJ);
+  return hipGetLastError();
+}
+
+// Kernel-form folds sharing one animal set: A_R A_R^T of individual b over fold 0's split rows (its
+// panel, system b), every 128 x 128 tile pair I >= J of the n_Rp rows on int8 MFMA (the off-diagonal
+// units' i8_tt8), stored both ways into a full n_Rp x n_Rp int32 matrix (FoldTab::gsh)
+__global__ __launch_bounds__(OTH, 2) void k_gshare(CholArgs a, int NR) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[4 * 2 * TILE * KBLK];
+  const int64_t ntp = (int64_t)NR * (NR + 1) / 2;
+  const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
+  const int64_t b = lg / ntp;
+  const int tp = (int)(lg % ntp);
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= tp) ++I;
+  const int J = tp - I * (I + 1) / 2;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
+  const int row = 16 * w + (l >> 2), pos = l & 3;
+  const int64_t nblk = (int64_t)a.scal[b * SCAL + SC_CBLK];
+  v4i cnt[8];
+  i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
+            row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, a.prow * KBLK, lds, cnt);
+  const int64_t ld = a.ft.gsh_ld;
+  int32_t* G = a.ft.gsh + b * ld * ld;
+  const int64_t ic = i0 + 16 * w + (l & 15);
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t jr = j0 + 16 * cb + (l >> 4) + 4 * r;
+      G[jr * ld + ic] = cnt[cb][r];
+      G[ic * ld + jr] = cnt[cb][r];
+    }
+}
+
+hipError_t launch_gshare(const CholLaunch& c, hipStream_t s) {
+  const FoldTab& ft = c.ft;
+  if (!ft.gsh || c.sd.form != FORM_DUAL || c.d.nRp % TILE) return hipErrorInvalidValue;
+  CholArgs a = make_args(c, 0);
+  a.wgt = nullptr;
+  const int NR = (int)(c.d.nRp / TILE);
+  hipLaunchKernelGGL(k_gshare, dim3((unsigned)(ft.bpf * NR * (NR + 1) / 2)), dim3(OTH), 0, s, a, NR);
   return hipGetLastError();
 }
 

@@ -147,6 +147,12 @@ struct FoldTab {
   const double* yV[MAXF];      // [nt][nV]
   const double* yT[MAXF];      // [nt][nTp] (kernel form: the right-hand sides y_T - mu on the fly)
   const double* ymu[MAXF];     // [nt]
+  // kernel form with shared counts (IntraGCV, share): every system's int8 count A_r . A_c is read
+  // from its individual's A_R A_R^T over fold 0's split rows (k_gshare), system row r of fold f at
+  // row gmap[f][r] (-1: padding) -- one int8 GEMM per individual instead of one per fold
+  int32_t* gsh;                // [bpf][gsh_ld][gsh_ld] (null: counts per system, int8 MFMA in the units)
+  const int32_t* gmap;         // [nf][gmap_ld]
+  int64_t gsh_ld, gmap_ld;     // nRp, nTp
 };
 __host__ __device__ __forceinline__ int fold_of(const FoldTab& ft, int64_t s) { return (int)(s / ft.bpf); }
 
@@ -285,6 +291,8 @@ hipError_t launch_chol_diag(const CholLaunch& c, int J, const OffPlan& p, hipStr
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s);
 // all diagonal GRM tiles K_JJ of the batch (one launch, before the column loop)
 hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s);
+// kernel form, shared fold counts: A_R A_R^T of every individual (FoldTab::gsh) from fold 0's panels
+hipError_t launch_gshare(const CholLaunch& c, hipStream_t s);
 // SNP form: every (I >= J) system tile of the batch on FP4 MFMA in one launch -- off-diagonal
 // counts into c.kc, diagonal tiles' counts into c.kd (replaces launch_diag_grm and the int8 phase
 // of the off-diagonal tiles)

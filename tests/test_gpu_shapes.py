@@ -245,7 +245,13 @@ def test_kernel_form_folds_fused(panel):
     with _env({"TBLUP_FOLD_FUSE": "0"}):
         with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
             unfused = eng.evaluate_folds(genomes, folds, 0.4)
+    # round 6: the folds' int8 counts from one shared A_R A_R^T per individual (default) or each
+    # system's own int8 tiles -- the same integers
+    with _env({"TBLUP_FOLD_GSHARE": "0"}):
+        with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
+            own = eng.evaluate_folds(genomes, folds, 0.4)
     np.testing.assert_array_equal(fused, unfused)
+    np.testing.assert_array_equal(fused, own)
     for f in range(5):
         np.testing.assert_array_equal(fused[f], singles[f])
     for i in (0, 1):

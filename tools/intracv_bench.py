@@ -4,7 +4,8 @@ k = 1000, pop 256) and a config-4-shaped kernel-form case (5000 x 50k, k = 5000,
   * device-resident genomes (no host decode in the ratio): one fold's evaluate_device and the
     k folds' evaluate_folds_device (tblup_eval_folds_device: fold-fused, the k x pop systems as
     one batch through one launch sequence, system tiles from shared counts; beside it the same
-    call with TBLUP_FOLD_SHARE=0 -- every fold's tiles from its own rows -- and with
+    call with TBLUP_FOLD_SHARE=0 -- every fold's tiles from its own rows --, TBLUP_FOLD_GSHARE=0 (kernel form:
+    each system's own int8 tiles instead of one A_R A_R^T per individual) and with
     TBLUP_FOLD_FUSE=0, the folds back to back on one stream), medians over repeats, and ratios;
   * end to end through the drop-in classes: the median time of a fresh population's evaluate()
     for the plain evaluator (one split) and for IntraGCV (one evaluate_folds call).
@@ -89,7 +90,7 @@ def main():
             assert np.array_equal(got[f], eng.evaluate(genomes, *splits[f], 0.4))
         eng.close()
         alt = {}
-        for var in ("TBLUP_FOLD_SHARE", "TBLUP_FOLD_FUSE"):
+        for var in ("TBLUP_FOLD_SHARE", "TBLUP_FOLD_FUSE", "TBLUP_FOLD_GSHARE"):
             os.environ[var] = "0"   # read at context creation
             eng = GpuBlupEngine(geno, np.load(pp), device=0)
             del os.environ[var]
@@ -103,6 +104,9 @@ def main():
                 "device_one_fold_ms": round(one_dev, 3), "device_k_folds_ms": round(folds_dev, 3),
                 "device_ratio": round(folds_dev / one_dev, 2),
                 "device_k_folds_unshared_ms": round(alt["TBLUP_FOLD_SHARE"], 3),
+                # kernel form: the folds' int8 counts from each system's own tiles instead of one
+                # shared A_R A_R^T per individual (round 6); the SNP form ignores the knob
+                "device_k_folds_own_counts_ms": round(alt["TBLUP_FOLD_GSHARE"], 3),
                 "device_k_folds_unfused_ms": round(seq_dev, 3),
                 "device_ratio_unfused": round(seq_dev / one_dev, 2)}
         if name == "config4shape":
