@@ -437,7 +437,10 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   const bool fold_share = use_st && ft.nf > 1 && ft.share;   // k_sys_tiles_folds
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
-  for (int J = 0; J < sd.NT; ++J) plan[J] = plan_of(c, B, sd.NT, J, use_st);
+  for (int J = 0; J < sd.NT; ++J) {
+    plan[J] = plan_of(c, B, sd.NT, J, use_st);
+    if (ft.gsh) plan[J].ne = 0;   // the diagonal kernel's E-units do not read shared fold counts
+  }
   const int32_t* csA = (const int32_t*)c->colsum_all.p;
   // the scalars formed after k_sys_tiles_st / k_sys_tiles_folds, in their K_JJ epilogue launch (one
   // launch less; neither reads a scalar), else by k_indiv_stats first

@@ -1240,7 +1240,10 @@ __device__ __forceinline__ void k_stage(const CholArgs& a, int64_t b, int64_t i0
   }
 }
 
-template <int NCB>
+// GSH: the kernel-form path may read shared fold counts (FoldTab::gsh); the diagonal kernel's E-units
+// are built without it (E-units are not planned for such chunks: run_chunk), which keeps that
+// latency-bound kernel's code as it was
+template <int NCB, bool GSH = true>
 __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int Jt, int cb0, const int2 (&kcv)[NCB],
                                       uint8_t* lds8, const double* pq_sh, const double* ui_sh, v4d (&acc)[NCB]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1276,7 +1279,7 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
       const int row = 16 * w + (l >> 2), pos = l & 3;
       i8_tt2d_pk64<4>(row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
                       row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, lds8, cnt);
-    } else if (!(a.skip & 32) && a.ft.gsh) {
+    } else if (GSH && !(a.skip & 32) && a.ft.gsh) {
       // kernel-form folds: the counts of the individual's shared A_R A_R^T (same integers)
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb)
@@ -1470,7 +1473,7 @@ __device__ __forceinline__ void e_unit(const CholArgs& a, int64_t b, int I, int 
     if (a.kc) kc_issue<8>(a, b, I, J, 0, kcv);
     k_stage(a, b, i0, j0, uj_sh, ui_sh);
     __syncthreads();
-    k_acc<8>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
+    k_acc<8, false>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
   }
   const double* Lb = a.L + b * (int64_t)NT * NT * TT;
   if (!(a.skip & 64))
@@ -2392,8 +2395,9 @@ hipError_t launch_gshare(const CholLaunch& c, hipStream_t s) {
 hipError_t launch_chol_diag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s) {
   CholArgs a = make_args(c, J);
   const int64_t nwg = c.B * (1 + p.ndd) + p.ne;
-  // E-units need the partial-sum slots and a tile below the diagonal
-  if (p.ne > 0 && (c.part == nullptr || J < 1 || p.ne > c.B * p.nI)) return hipErrorInvalidValue;
+  // E-units need the partial-sum slots and a tile below the diagonal, and are built without the
+  // shared fold counts (k_acc<8, false>)
+  if (p.ne > 0 && (c.part == nullptr || J < 1 || p.ne > c.B * p.nI || c.ft.gsh)) return hipErrorInvalidValue;
   // profiling: the phase stamps of this launch follow its workgroup records
   if (c.wgt) a.dtr = c.wgt + nwg * WGT_REC;
   hipLaunchKernelGGL(k_chol_diag, dim3((unsigned)nwg), dim3(DTHR), 0, s, a, p.ne, p.ahead_cur ? J - 1 : 0);
