@@ -130,3 +130,24 @@ def test_two_rank_panel_start_up_is_node_shared(tmp_path):
         assert res[r]["shared"]
         assert res[r]["grow"] < f64 // 2, (r, res[r]["grow"], f64)
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("tblup_panel_")]
+
+
+def test_panel_reader_streams_and_validates(tmp_path):
+    """tblup_amd.panel.read_panel_int8 (single process): C- and Fortran-ordered .npy panels of any
+    integral dtype, chunk boundaries that split the rows unevenly, and the {0,1,2} contract."""
+    from tblup_amd.panel import convert_rows, read_panel_int8
+    rng = np.random.default_rng(3)
+    g = rng.integers(0, 3, size=(257, 1031)).astype(np.float64)
+    for arr in (g, np.asfortranarray(g), g.astype(np.float32), g.astype(np.int8), g.astype(np.int64)):
+        p = str(tmp_path / "g.npy")
+        np.save(p, arr)
+        for cb in (1 << 20, 12_345, 1):
+            out = read_panel_int8(p, chunk_bytes=cb)
+            assert out.dtype == np.int8 and np.array_equal(out, g)
+    assert np.array_equal(convert_rows(g, chunk_bytes=4096), g.astype(np.int8))
+    for bad in (0.5, 3.0, -1.0):
+        h = g.copy()
+        h[200, 1000] = bad
+        np.save(str(tmp_path / "h.npy"), h)
+        with pytest.raises(ValueError):
+            read_panel_int8(str(tmp_path / "h.npy"))

@@ -149,3 +149,27 @@ def test_gpu_write_after_evolve_is_seen(gpu, tmp_path):
             want = O.blup(O.decode_randkeys(kids[j].get_internal_genome(), k), T, V, geno.astype(np.float64),
                           pheno, 0.4)
             assert abs(kids[j].fitness - want) < 1e-9
+
+
+def test_track_rows_matches_track():
+    """track_rows (round 6: a block's rows tracked in one pass) gives every row the semantics of
+    track(row): its own owner, staleness per row, writes land in the block, the block is found
+    from the row (the evolver's compaction), views stay tracked and copies are plain."""
+    from tblup_amd.keystore import track_rows
+    block = np.arange(24, dtype=np.float64).reshape(4, 6)
+    rows = track_rows(block)
+    block.flags.writeable = False
+    assert len(rows) == 4 and all(type(r) is TrackedGenome for r in rows)
+    assert all(r._blk is block and not r.flags.writeable for r in rows)
+    rows[2][1] = -1.0                          # the private writable alias
+    assert rows[2]._stale and not rows[1]._stale and not rows[3]._stale
+    assert block[2, 1] == -1.0
+    with pytest.raises(ValueError):
+        np.asarray(rows[0])[0] = 5.0           # no other writable alias
+    v = rows[3][1:4]
+    assert v._tracked() and v._root() is rows[3]
+    np.copyto(v, 7.0)
+    assert rows[3]._stale and np.all(block[3, 1:4] == 7.0)
+    c = rows[1].copy()
+    assert not c._tracked() and np.array_equal(c, block[1])
+    assert np.array_equal(copy.deepcopy(rows[0]), block[0])
