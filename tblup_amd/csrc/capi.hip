@@ -129,11 +129,14 @@ inline int dbg_skip(const tblup_ctx* c) {
 #endif
 }
 
-// SNP (primal) form: the batched system-tile launch (k_sys_tiles) builds every exact tile up
-// front; int16 counts stay exact while n_T <= KC_MAX_NT (beyond it, and for one-tile systems, the
-// in-tile int8 products of the off-diagonal kernel).
-bool sys_tiles(const EvalDims& d, const SysDims& sd) {
-  return sd.form == FORM_PRIMAL && d.nT <= KC_MAX_NT && sd.NT >= 2;
+// The batched system-tile launch (k_sys_tiles) builds every exact tile up front; int16 counts stay
+// exact while the contraction -- n_T animals (SNP form), k SNPs (kernel form: every k <= 64 cblk) --
+// is <= KC_MAX_NT (beyond it, and for one-tile systems, the in-tile int8 products of the
+// off-diagonal kernel).  Kernel form: TBLUP_DUAL_ST=0 keeps the in-tile products (A/B timing).
+bool sys_tiles(const tblup_ctx* c, const EvalDims& d, const SysDims& sd) {
+  if (sd.NT < 2) return false;
+  if (sd.form == FORM_PRIMAL) return d.nT <= KC_MAX_NT;
+  return c->dual_st && sd.cblk * KBLK <= KC_MAX_NT;
 }
 
 }  // namespace
@@ -294,7 +297,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
                    bool with_ebv) {
   size_t s = 0;
   auto add = [&](size_t x) { s = (size_t)round_up((int64_t)(s + x), 256); };
-  add(sd.form == FORM_DUAL ? (size_t)B * sd.cblk * sd.prow * KBLK : 0);   // panel (dual only)
+  add(sd.form == FORM_DUAL ? (size_t)B * sd.prow * dual_pk_row(sd) : 0);   // packed panel (dual only)
   add((size_t)B * sd.prow * 8);                                 // u
   add((size_t)B * SCAL * 8);                                    // scal
   add((size_t)B * sd.ns * sd.ns * 8);                           // L (Lt tiles)
@@ -304,9 +307,9 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add((size_t)B * d.nt * sd.ns * 8);                            // rhs
   add((size_t)B * TBLUP_NSLOT * 36 * 256 * 8);                  // next diagonal tile (minus its last SYRK term)
   add((size_t)B * sd.NT * NPACK * BLKD * 8);                    // diagonal GRM tiles
-  add(sys_tiles(d, sd) ? (size_t)B * sd.NT * KD_TILE * 2 : 0);  // their int16 counts (k_sys_tiles)
-  add(sys_tiles(d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
-  add(uses_part(c, B, sd.NT, sys_tiles(d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
+  add(sys_tiles(c, d, sd) ? (size_t)B * sd.NT * KD_TILE * 2 : 0);  // their int16 counts (k_sys_tiles)
+  add(sys_tiles(c, d, sd) ? (size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE * 2 : 0);   // off-diagonal counts
+  add(uses_part(c, B, sd.NT, sys_tiles(c, d, sd)) ? (size_t)2 * B * sd.NT * TILE * TILE * 8 : 0);   // partial sums
   if (use_chain(c, sd, B, d.nt)) {                                    // chained solve: beta, c_{J->I}, EBV shares
     add((size_t)B * d.nt * sd.ns * 8);
     add((size_t)B * sd.NT * sd.NT * d.nt * TILE * 8);
@@ -384,7 +387,6 @@ FoldTab single_fold(const Split& sp, int64_t B) {
   ft.bpf = std::max<int64_t>(B, 1);
   ft.nf = 1;
   ft.gpk[0] = (const uint8_t*)sp.gpk.p;
-  ft.gs[0] = (const int8_t*)sp.geno.p;
   ft.csT[0] = (const int32_t*)sp.colsumT.p;
   ft.xty[0] = (const double*)sp.xty.p;
   ft.yV[0] = (const double*)sp.yV.p;
@@ -413,11 +415,12 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   for (int64_t b = 0; b < B; ++b) {
     const int64_t k = h_off[b + 1] - h_off[b];
     grm_flops += 2.0 * (double)k * tri;
-    gather_bytes += 2.0 * (double)k * (double)(d.nT + d.nV);
+    gather_bytes += 0.5 * (double)k * (double)(d.nT + d.nV);   // 2-bit split rows in, 2-bit rows out
     stats_bytes += 16.0 * (double)k;
   }
-  const int64_t pstride = (sd.form == FORM_DUAL) ? sd.cblk * sd.prow * KBLK : 0;
-  int8_t* panel = cv.take<int8_t>((size_t)B * pstride);
+  const int64_t pk_row = (sd.form == FORM_DUAL) ? dual_pk_row(sd) : 0;
+  const int64_t pstride = sd.prow * pk_row;
+  uint8_t* panel = cv.take<uint8_t>((size_t)B * pstride);
   double* u = cv.take<double>((size_t)B * sd.prow);
   double* scal = cv.take<double>((size_t)B * SCAL);
   double* L = cv.take<double>((size_t)B * sd.ns * sd.ns);
@@ -426,15 +429,16 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   double* wv = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* rhs = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* Sp = cv.take<double>((size_t)B * TBLUP_NSLOT * 36 * 256);
-  const bool use_st = sys_tiles(d, sd) && stop_stage != 1;
+  // (kernel-form fold chunks read their counts from the shared A_R A_R^T instead)
+  const bool use_st = sys_tiles(c, d, sd) && stop_stage != 1 && !ft.gsh;
   // diagonal system tiles: fp64 K_JJ + lambda I (with k_sys_tiles: J < 2 only, the diagonal
   // kernel's direct reads) and, with k_sys_tiles, the exact int16 counts of J >= 2 (the D-units')
   double* Kdg = cv.take<double>((size_t)B * sd.NT * NPACK * BLKD);
   int16_t* kdb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * KD_TILE) : nullptr;
   int16_t* kcb = use_st ? cv.take<int16_t>((size_t)B * sd.NT * (sd.NT - 1) / 2 * KC_TILE) : nullptr;
-  double* Pp = uses_part(c, B, sd.NT, sys_tiles(d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
+  double* Pp = uses_part(c, B, sd.NT, sys_tiles(c, d, sd)) ? cv.take<double>((size_t)2 * B * sd.NT * TILE * TILE) : nullptr;
   double* Qb = use_last_term(c, sd, B) ? cv.take<double>((size_t)B * NPACK * BLKD) : nullptr;
-  const bool fold_share = use_st && ft.nf > 1 && ft.share;   // k_sys_tiles_folds
+  const bool fold_share = use_st && sd.form == FORM_PRIMAL && ft.nf > 1 && ft.share;   // k_sys_tiles_folds
   if (int rc = ws_check(c, cv)) return rc;
   std::vector<OffPlan> plan(sd.NT);
   for (int J = 0; J < sd.NT; ++J) {
@@ -460,7 +464,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   if (sd.form == FORM_DUAL && !redo) {
     // primal rows are read in place from the split matrix: no gather
     rc = timed(c, s, KC_GATHER, 0.0, gather_bytes, [&] {
-      return launch_gather(ft, d_idx, d_off, pstride, B, csA, scal, d, panel, u, s);
+      return launch_gather(ft, d_idx, d_off, pstride, B, csA, scal, d, pk_row, panel, u, s);
     });
     if (rc) return rc;
   }
@@ -473,7 +477,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
     if (K_out) *K_out = K;
     const double kbytes = (double)B * ((double)d.nT * d.nT / 2.0 + (double)d.nV * d.nT) * 8.0;
     return timed(c, s, KC_GRM, grm_flops, kbytes + gather_bytes / 2.0,
-                 [&] { return launch_grm(panel, pstride, d_off, u, scal, d, B, K, s); });
+                 [&] { return launch_grm(panel, pstride, pk_row, d_off, u, scal, d, B, K, s); });
   }
   if (K_out) *K_out = L;
   CholLaunch cl{d, sd, B, L, Dinv, z, wv, rhs, Sp, Kdg, (const double*)sp.yT.p, panel, pstride, d_off, d_idx,
@@ -704,6 +708,7 @@ int tblup_ctx_create(const int8_t* geno, int64_t n, int64_t P, int layout, const
   if (const char* e = getenv("TBLUP_FOLD_SHARE")) c->fold_share = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_SYS_ST")) c->sys_st = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_FOLD_GSHARE")) c->fold_gshare = atoi(e) != 0;
+  if (const char* e = getenv("TBLUP_DUAL_ST")) c->dual_st = atoi(e) != 0;
   if (const char* e = getenv("TBLUP_DIAG_D")) c->diag_d = std::max(-1, std::min(1, atoi(e)));
   if (const char* e = getenv("TBLUP_DIAG_E")) c->diag_e = std::max(-1, std::min(2, atoi(e)));
   if (const char* e = getenv("TBLUP_PAD_FIRST")) c->pad_first = atoi(e) != 0;
@@ -749,7 +754,6 @@ int tblup_ctx_destroy(tblup_ctx* c) {
   }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   for (auto& kv : c->splits) {
-    kv.second->geno.release();
     kv.second->gpk.release();
     kv.second->colsumT.release();
     kv.second->xty.release();
@@ -817,7 +821,6 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
     sp->meanyT[t] = (double)(acc / (long double)nT);
     for (int64_t i = 0; i < nV; ++i) yV[t * nV + i] = c->pheno[valid[i] * nt + t];
   }
-  if (int rc = dev_alloc(c, sp->geno, (size_t)(c->P + 1) * sp->nRp)) return rc;
   if (int rc = dev_alloc(c, sp->gpk, (size_t)(c->P + 1) * (sp->nRp / 4) + 64)) return rc;
   if (int rc = dev_alloc(c, sp->colsumT, (size_t)c->P * 4)) return rc;
   if (int rc = dev_alloc(c, sp->xty, (size_t)nt * c->P * 8)) return rc;
@@ -831,13 +834,11 @@ int tblup_set_split(tblup_ctx* c, int split_id, const int64_t* train, int64_t nT
   HIPCHK(hipMemcpyAsync(sp->yV.p, yV.data(), yV.size() * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(sp->ymu.p, sp->meanyT.data(), (size_t)nt * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(launch_build_split((const int8_t*)c->geno_sm.p, c->n, c->P, (const int32_t*)rm.p, sp->nRp, nT,
-                            (const double*)sp->yT.p, (const double*)sp->ymu.p, nt, (int8_t*)sp->geno.p,
-                            (uint8_t*)sp->gpk.p, (int32_t*)sp->colsumT.p, (double*)sp->xty.p, c->stream));
+                            (const double*)sp->yT.p, (const double*)sp->ymu.p, nt, (uint8_t*)sp->gpk.p, (int32_t*)sp->colsumT.p, (double*)sp->xty.p, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   dev_free(c, rm);
   auto it = c->splits.find(split_id);
   if (it != c->splits.end()) {
-    dev_free(c, it->second->geno);
   dev_free(c, it->second->gpk);
     dev_free(c, it->second->colsumT);
     dev_free(c, it->second->xty);
@@ -857,7 +858,6 @@ int tblup_set_traits(tblup_ctx* c, const double* pheno, int64_t n_traits) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   for (auto& kv : c->splits) {   // splits hold per-trait phenotype vectors
-    dev_free(c, kv.second->geno);
     dev_free(c, kv.second->gpk);
     dev_free(c, kv.second->colsumT);
     dev_free(c, kv.second->xty);
@@ -883,7 +883,6 @@ int tblup_drop_split(tblup_ctx* c, int split_id) {
   if (it == c->splits.end()) return fail(TBLUP_ERR_ARG, "unknown split id");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  dev_free(c, it->second->geno);
   dev_free(c, it->second->gpk);
   dev_free(c, it->second->colsumT);
   dev_free(c, it->second->xty);
@@ -1032,8 +1031,11 @@ static bool fold_fusable(const tblup_ctx* c, const std::vector<Split*>& sps, con
 // A_R A_R^T per individual over fold 0's split rows (k_gshare; FoldTab::gsh) -- the fold systems'
 // training rows are all rows of fold 0's split -- instead of one int8 GEMM per system.  The counts
 // are the same exact integers, so the results are bit-identical (TBLUP_FOLD_GSHARE=0 for A/B).
+// (only where the systems would form their counts in-tile: FP4 system tiles per fold system beat the
+// shared int32 counts' row-mapped reads -- config-4-shaped 5 folds 21.9 vs 22.5 ms)
 static bool fold_gshare(const tblup_ctx* c, const std::vector<Split*>& sps, const SysDims& sd) {
   if (sd.form != FORM_DUAL || !c->fold_share || !c->fold_gshare || sps.size() < 2) return false;
+  if (sys_tiles(c, dims_of(c, *sps[0]), sd)) return false;
   for (const Split* sp : sps)
     if (sp->rows != sps[0]->rows || (int64_t)sp->train.size() != sp->nT || (int64_t)sp->valid.size() != sp->nV)
       return false;
@@ -1097,7 +1099,6 @@ static int run_folds_fused(tblup_ctx* c, const std::vector<Split*>& sps, const S
   }
   for (int64_t f = 0; f < F; ++f) {
     ft.gpk[f] = (const uint8_t*)sps[f]->gpk.p;
-    ft.gs[f] = (const int8_t*)sps[f]->geno.p;
     ft.csT[f] = (const int32_t*)sps[f]->colsumT.p;
     ft.xty[f] = (const double*)sps[f]->xty.p;
     ft.yV[f] = (const double*)sps[f]->yV.p;

@@ -36,7 +36,7 @@ struct Split {
   std::vector<int64_t> rows;   // train + valid animals, sorted (fold sets: shared counts)
   std::vector<int64_t> train, valid;   // the split's animal lists in system-row order
   std::vector<double> meanyT;   // [nt]
-  DevBuf geno, gpk, colsumT, xty, yT, yV, ymu;
+  DevBuf gpk, colsumT, xty, yT, yV, ymu;
 };
 
 enum { KC_STATS = 0, KC_GATHER, KC_GRM, KC_DIAG, KC_OFFDIAG, KC_SOLVE };
@@ -106,6 +106,7 @@ struct tblup_ctx {
   int fold_fuse = 1;     // TBLUP_FOLD_FUSE: 0 evaluates a fold set split by split (A/B timing)
   int fold_share = 1;    // TBLUP_FOLD_SHARE: 0 builds every fold's system tiles from its own rows
   int fold_gshare = 1;   // TBLUP_FOLD_GSHARE: kernel-form folds read their counts from one A_R A_R^T
+  int dual_st = 1;       // TBLUP_DUAL_ST: kernel-form system tiles from k_sys_tiles (0: in-tile products)
   std::vector<int32_t> gmap_host;   // the fold row maps of the last fused kernel-form chunk (H2D source)
   int sys_st = -1;       // TBLUP_SYS_ST: system tiles by the persistent super-tile kernel (k_sys_tiles_st):
                          // -1 auto (sys_tiles_grid), 0 never, 1 whenever it applies -- the same exact counts

@@ -1,22 +1,36 @@
 // int8 MFMA tile GEMM shared by the GRM kernels:
 //   C(128x128, int32) = sum_s A[i][s] * B[j][s]
-// where A and B are 128-row tiles of the animal-major panel ([kb][row][64 SNPs]).
+// where A and B are 128-row tiles of the kernel form's packed panel (rows of pk_row bytes, 64-SNP
+// block kb at + 16 kb), unpacked to int8 on the way into LDS.
 // 256 threads = 4 waves in a 2x2 grid, each wave a 64x64 block of 2x2
-// v_mfma_i32_32x32x32_i8 tiles (lane l holds 16 consecutive k of row l&31).
+// v_mfma_i32_32x32x32_i8 tiles (lane l holds 16 k of row l&31).
 // Genotypes are {0,1,2}: every partial sum is an exact integer.
 #pragma once
 #include "tblup_internal.h"
 
 namespace tblup {
 
+// ---- 2-bit packed genotypes ----
+// A packed row holds 4 genotypes per byte, animal 4j+i at bits 2i of byte j.  One 32-bit
+// word (16 animals) unpacks to the 16 int8 MFMA operand bytes with two ops per dword:
+// dword q = (x >> 2q) & 0x03030303, i.e. byte m of dword q is animal 4m+q.  This fixed
+// permutation of the 16 animals is the same for every row, so A.B^T contractions are
+// unchanged.
+__device__ __forceinline__ v4i unpack16(uint32_t x) {
+  return v4i{(int)(x & 0x03030303u), (int)((x >> 2) & 0x03030303u), (int)((x >> 4) & 0x03030303u),
+             (int)((x >> 6) & 0x03030303u)};
+}
+
+
 // [128 rows][64 B]; 16-B chunk c of row r stored at c ^ ((r >> 2) & 3):
 // conflict-free ds_read_b128 for the 32x32x32 i8 fragment pattern.
 __device__ __forceinline__ int lds_off_i8(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 2) & 3)); }
 
-// lds: >= 32 KiB (two buffers x A/B x 8 KiB).  a_base/b_base point at kb = 0 of the
-// two 128-row tiles; consecutive kb blocks are kb_stride bytes apart.
-__device__ __forceinline__ void i8_tile_gemm(const int8_t* __restrict__ a_base, const int8_t* __restrict__ b_base,
-                                             bool same, int64_t nblk, int64_t kb_stride, int8_t* lds,
+// lds: >= 32 KiB (two buffers x A/B x 8 KiB).  a_base/b_base point at the first packed row of the
+// two 128-row tiles; rows are pk_row bytes apart.  Dword c of a row's block kb (16 SNPs) becomes the
+// row's 16-B int8 chunk c (unpack16: the same SNP order in every row).
+__device__ __forceinline__ void i8_tile_gemm(const uint8_t* __restrict__ a_base, const uint8_t* __restrict__ b_base,
+                                             bool same, int64_t nblk, int64_t pk_row, int8_t* lds,
                                              v16i (&acc)[2][2]) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
 #pragma unroll
@@ -29,13 +43,12 @@ __device__ __forceinline__ void i8_tile_gemm(const int8_t* __restrict__ a_base, 
   constexpr int TB = TILE * KBLK;  // 8 KiB
   v4i ra[2], rb[2];
   auto gload = [&](int64_t kb) {
-    const int8_t* A = a_base + kb * kb_stride;
-    const int8_t* Bp = b_base + kb * kb_stride;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int q = t + 256 * e;
-      ra[e] = *reinterpret_cast<const v4i*>(A + 16 * q);
-      if (!same) rb[e] = *reinterpret_cast<const v4i*>(Bp + 16 * q);
+      const int q = t + 256 * e, row = q >> 2, c = q & 3;
+      const int64_t o = (int64_t)row * pk_row + 16 * kb + 4 * c;
+      ra[e] = unpack16(*reinterpret_cast<const uint32_t*>(a_base + o));
+      if (!same) rb[e] = unpack16(*reinterpret_cast<const uint32_t*>(b_base + o));
     }
   };
   auto swrite = [&](int buf) {
@@ -70,17 +83,6 @@ __device__ __forceinline__ void i8_tile_gemm(const int8_t* __restrict__ a_base, 
     if (kb + 1 < nblk) swrite(cur ^ 1);
     __syncthreads();
   }
-}
-
-// ---- 2-bit packed genotypes ----
-// A packed row holds 4 genotypes per byte, animal 4j+i at bits 2i of byte j.  One 32-bit
-// word (16 animals) unpacks to the 16 int8 MFMA operand bytes with two ops per dword:
-// dword q = (x >> 2q) & 0x03030303, i.e. byte m of dword q is animal 4m+q.  This fixed
-// permutation of the 16 animals is the same for every row, so A.B^T contractions are
-// unchanged.
-__device__ __forceinline__ v4i unpack16(uint32_t x) {
-  return v4i{(int)(x & 0x03030303u), (int)((x >> 2) & 0x03030303u), (int)((x >> 4) & 0x03030303u),
-             (int)((x >> 6) & 0x03030303u)};
 }
 
 // Row / column (within the 128x128 tile) of accumulator element r of block (m, n) for lane l.

@@ -1,5 +1,5 @@
 // Batched left-looking tile Cholesky of (K_TT + lambda I), fp64, 128x128 tiles,
-// with the GRM tiles rebuilt on the fly from the int8 panel (K is never stored).
+// with the GRM tiles from exact integer counts (K is never stored in fp64).
 //
 // Replaces the reference's per-individual dense solves
 //   gblup:    G_inv = np.linalg.inv(G_TT + lambda I)          (tblup/evaluator.py:280-284)
@@ -292,7 +292,7 @@ struct CholArgs {
   double* Kd;               // [B][NT][36*256] GRM diagonal tiles (k_diag_grm)
   const double* yT;         // [nt][ytp] dual right-hand sides (y_T - mu, on the fly)
   const double* rhs;        // [B][nt][ns] primal right-hand sides
-  const int8_t* panel;      // [B] x pstride
+  const uint8_t* panel;     // [B] x pstride: kernel form, prow packed animal rows of pstride / prow bytes
   int64_t pstride;
   const double* u;          // [B][prow]
   const double* scal;       // [B][SCAL]
@@ -309,14 +309,14 @@ struct CholArgs {
   int skip;                 // diagnostic ablation mask (TBLUP_DBG_SKIP); 0 in production
   uint64_t* wgt;            // workgroup trace records (TBLUP_WG_TRACE), null in production
   uint64_t* dtr;            // diagonal launch: phase timestamps of workgroup 0 (TBLUP_WG_TRACE), else null
-  const int16_t* kc;        // SNP form: off-diagonal system-tile counts (k_sys_tiles), else null
+  const int16_t* kc;        // off-diagonal system-tile counts (k_sys_tiles, either form), else null
   double* part;             // [2][B][NT][128*128] off-diagonal partial sums K - sum_{L<J-1} (acc layout), slot J&1
   double* q;                // last-term mode: [B][NPACK*BLKD] L_{J,J-1} L_{J,J-1}^T, from launch J-1's tile (J, J-1)
   int64_t B;                // individuals in the chunk
   FoldTab ft;               // each system's split (ymu, packed rows)
   int padskip;              // contractions over block column 0 skip the leading padding rows (SNP form)
   int padfirst;             // SNP form: padding rows lead (SC_PAD = ns - k)
-  int16_t* kd;              // SNP form with k_sys_tiles: the diagonal tiles' exact counts for J >= 2 (KD_TILE
+  int16_t* kd;              // with k_sys_tiles: the diagonal tiles' exact counts for J >= 2 (KD_TILE
                             // each; the D-units form K_JJ + lambda I where they read it, kd_block); Kd then
                             // holds J < 2 only (the diagonal kernel's direct reads)
 };
@@ -417,10 +417,10 @@ struct WgTrace {
   }
 };
 
-// Address of system row r's contraction block 0 for individual b: the gathered panel
-// (dual; stage kb at + kb * prow * 64).
-__device__ __forceinline__ const int8_t* row_base(const CholArgs& a, int64_t b, int64_t r) {
-  return a.panel + b * a.pstride + r * KBLK;
+// Packed panel row of system row r of individual b (kernel form: the gathered animal rows,
+// dual_pk_row = pstride / prow bytes each; stage kb at + 16 kb, as row_packed's)
+__device__ __forceinline__ const uint8_t* row_dpk(const CholArgs& a, int64_t b, int64_t r) {
+  return a.panel + b * a.pstride + r * (a.pstride / a.prow);
 }
 // Packed split row of system row r (primal: row r holds selected SNP r - pad; padding rows -> the
 // zero row P; stage kb at + 16 kb).
@@ -465,52 +465,9 @@ static_assert(DTHR == 4 * TILE, "diag z: four lanes per row");
 constexpr int OW = 8;            // waves per off-diagonal workgroup
 constexpr int OTH = 64 * OW;     // threads
 
-// int8 tile, kernel form (gathered int8 panel): A = panel rows of tile J, B = tile I.
-// Stage kb = 8 KiB per operand; wave w loads 1 KiB chunk w of each (rows 16w..16w+15).
-// WCL >= 0: this wave computes column block WCL and only the row blocks cb >= WCL (the
-// lower blocks of a symmetric diagonal tile); WCL < 0: column block w, all row blocks.
-template <int D, int WCL = -1>
-__device__ __forceinline__ void i8_tt8(const int8_t* sa, const int8_t* sb, int64_t nblk, int64_t kstep, int8_t* lds,
-                                       v4i (&cnt)[8]) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wc = (WCL < 0) ? w : WCL;
-#pragma unroll
-  for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
-  if (nblk <= 0) return;
-  constexpr int TB = TILE * KBLK;
-  auto issue = [&](int64_t kb) {
-    int8_t* slot = lds + (int)(kb % D) * 2 * TB;
-    ring_glds<TBLUP_AB_ASM_I8>(sa + kb * kstep, slot + w * 1024);
-    ring_glds<TBLUP_AB_ASM_I8>(sb + kb * kstep, slot + TB + w * 1024);
-  };
-  for (int64_t kb = 0; kb < D - 1 && kb < nblk; ++kb) issue(kb);
-  const int rho = l & 15, prow = (rho >> 2) + 4 * (rho & 3), ch = l >> 4;
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    if (kb + D - 2 < nblk) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 2) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kb + D - 1 < nblk) issue(kb + D - 1);
-    const int8_t* As = lds + (int)(kb % D) * 2 * TB;
-    const int8_t* Bs = As + TB;
-    const v4i bv = *reinterpret_cast<const v4i*>(Bs + i8off_b(16 * wc + rho, ch));
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
-      if (cb >= WCL) {
-        const v4i av = *reinterpret_cast<const v4i*>(As + i8off_a(16 * cb + prow, ch));
-        cnt[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cnt[cb], 0, 0, 0);
-      }
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-// SNP form, 64-B stages: stage st = 256 animals = 64 B of each packed row, loaded and laid
-// out exactly like the int8 panel stages of i8_tt8 (rows of 4 swizzled 16-B chunks; every
-// 128-B line of a row is consumed by two consecutive stages instead of eight 16-B pieces).
+// Packed rows (the SNP form's split rows, the kernel form's gathered panel), 64-B stages: stage st
+// = 256 contraction elements = 64 B of each packed row (rows of 4 swizzled 16-B chunks; every
+// 128-B line of a row is consumed by two consecutive stages).
 // Lane (rho, ch) reads one 16-B chunk = 4 packed dwords and feeds dword s to k-step s, so
 // the four lane groups x four k-steps cover the 16 dwords once (animal order inside a
 // stage is immaterial to the counts; A and B use the same order).  A stage past the
@@ -1197,7 +1154,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
 // ---------------------------------------------------------------------------
 // Off-diagonal launch of column J: one 8-wave workgroup per unit, two per CU (LDS <= 72 KiB).
 //   T-unit, tile (I, J), I > J:
-//     0. acc = K_JI in the f64 accumulator layout: from k_sys_tiles' counts (SNP form) or int8
+//     0. acc = K_JI in the f64 accumulator layout: from k_sys_tiles' counts (either form) or int8
 //        MFMA here (rows permuted so the counts land in the f64 layout) -- or, when launch J-1 ran
 //        ahead, its partial sum K_JI - sum_{L<J-1} L_JL L_IL^T
 //     1. acc -= sum_{L} L_JL L_IL^T over the L < J not summed yet   (acc = T^T, wave w: its 16 i)
@@ -1275,21 +1232,19 @@ __device__ __forceinline__ void k_acc(const CholArgs& a, int64_t b, int I, int J
   if constexpr (NCB == 8) {
     v4i cnt[8];
     const int64_t nblk = (int64_t)sc[SC_CBLK];
-    if (!(a.skip & 32) && a.form == FORM_PRIMAL) {
-      const int row = 16 * w + (l >> 2), pos = l & 3;
-      i8_tt2d_pk64<4>(row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
-                      row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, lds8, cnt);
-    } else if (GSH && !(a.skip & 32) && a.ft.gsh) {
+    if (GSH && !(a.skip & 32) && a.form != FORM_PRIMAL && a.ft.gsh) {
       // kernel-form folds: the counts of the individual's shared A_R A_R^T (same integers)
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) cnt[cb][r] = gsh_count(a, b, j0 + 16 * cb + (l >> 4) + 4 * r, i0 + il);
     } else if (!(a.skip & 32)) {
+      // 2-bit packed rows of either form: the SNP form's split rows, the kernel form's gathered panel
       const int row = 16 * w + (l >> 2), pos = l & 3;
-      i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
-                row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, a.prow * KBLK,
-                reinterpret_cast<int8_t*>(lds8), cnt);
+      const bool pf = a.form == FORM_PRIMAL;
+      const uint8_t* sa = (pf ? row_packed(a, b, j0 + row) : row_dpk(a, b, j0 + row)) + 16 * (pos ^ ((row >> 2) & 3));
+      const uint8_t* sb = (pf ? row_packed(a, b, i0 + row) : row_dpk(a, b, i0 + row)) + 16 * (pos ^ ((row >> 2) & 2));
+      i8_tt2d_pk64<4>(sa, sb, nblk, lds8, cnt);
     } else {
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) cnt[cb] = v4i{0, 0, 0, 0};
@@ -1553,8 +1508,9 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
       if (cb >= wc)
 #pragma unroll
         for (int r = 0; r < 4; ++r) cnt[cb][r] = gsh_count(a, b, j0 + 16 * cb + (l >> 4) + 4 * r, j0 + 16 * wc + (l & 15));
-  } else if (a.form == FORM_PRIMAL) {
-    const uint8_t* rp = row_packed(a, b, j0 + row);
+  } else {
+    // 2-bit packed rows: the SNP form's split rows, the kernel form's gathered panel
+    const uint8_t* rp = a.form == FORM_PRIMAL ? row_packed(a, b, j0 + row) : row_dpk(a, b, j0 + row);
     const uint8_t* sa = rp + 16 * (pos ^ ((row >> 2) & 3));
     const uint8_t* sb = rp + 16 * (pos ^ ((row >> 2) & 2));
     switch (wc) {   // wave-uniform: one instantiation per column block
@@ -1566,22 +1522,6 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
       case 5: i8_tt8_pk64<4, 5>(sa, sb, nblk, lds, cnt); break;
       case 6: i8_tt8_pk64<4, 6>(sa, sb, nblk, lds, cnt); break;
       default: i8_tt8_pk64<4, 7>(sa, sb, nblk, lds, cnt); break;
-    }
-  } else {
-    const int8_t* rb = row_base(a, b, j0 + row);
-    const int8_t* sa = rb + 16 * (pos ^ ((row >> 2) & 3));
-    const int8_t* sb = rb + 16 * (pos ^ ((row >> 2) & 2));
-    int8_t* ld8 = reinterpret_cast<int8_t*>(lds);
-    const int64_t ks = a.prow * KBLK;
-    switch (wc) {
-      case 0: i8_tt8<4, 0>(sa, sb, nblk, ks, ld8, cnt); break;
-      case 1: i8_tt8<4, 1>(sa, sb, nblk, ks, ld8, cnt); break;
-      case 2: i8_tt8<4, 2>(sa, sb, nblk, ks, ld8, cnt); break;
-      case 3: i8_tt8<4, 3>(sa, sb, nblk, ks, ld8, cnt); break;
-      case 4: i8_tt8<4, 4>(sa, sb, nblk, ks, ld8, cnt); break;
-      case 5: i8_tt8<4, 5>(sa, sb, nblk, ks, ld8, cnt); break;
-      case 6: i8_tt8<4, 6>(sa, sb, nblk, ks, ld8, cnt); break;
-      default: i8_tt8<4, 7>(sa, sb, nblk, ks, ld8, cnt); break;
     }
   }
   __syncthreads();
@@ -1781,6 +1721,7 @@ __device__ __forceinline__ v4i fp4_operand(uint32_t x0, uint32_t x1) {
 __device__ v4f mfma_fp4_16x16x128(v4i a, v4i b, v4f c, int cbsz, int blgp, int opsel_a, int scale_a, int opsel_b,
                                   int scale_b) __asm("llvm.amdgcn.mfma.scale.f32.16x16x128.f8f6f4.v4i32.v4i32");
 
+template <bool DUAL>   // kernel form: the gathered panel's packed animal rows
 __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* kc, int ntri) {
   constexpr int D = 3;                 // 64-B stages (256 animals) in the LDS ring (48 KiB: 3 workgroups per CU)
   constexpr int TB = TILE * 64;        // one operand image of a stage: 8 KiB
@@ -1805,8 +1746,8 @@ __global__ __launch_bounds__(64 * STW, 2) void k_sys_tiles(CholArgs a, int16_t* 
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = 16 * (2 * w + h) + (l >> 2), pos = l & 3;
-    sa[h] = row_packed(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3));
-    sb[h] = row_packed(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2));
+    sa[h] = (DUAL ? row_dpk(a, b, j0 + row) : row_packed(a, b, j0 + row)) + 16 * (pos ^ ((row >> 2) & 3));
+    sb[h] = (DUAL ? row_dpk(a, b, i0 + row) : row_packed(a, b, i0 + row)) + 16 * (pos ^ ((row >> 2) & 2));
   }
   auto issue = [&](int64_t st) {
     uint8_t* slot = lds + (int)(st % D) * 2 * TB;
@@ -1890,6 +1831,7 @@ constexpr int SP_MAXIND = 64;          // individuals in one workgroup's run (sy
 static_assert(TBLUP_AB_SP_D >= 3 && TBLUP_AB_SP_D <= 4, "ring waits are written for 1-2 stages ahead");
 constexpr int64_t SYS_ST_MIN = TBLUP_AB_SYS_ST_MIN;   // auto: at least this many units per CU
 
+template <bool DUAL>   // kernel form: the gathered panel's packed animal rows
 __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_t* kc, int nsu, int nunits) {
   constexpr int D = TBLUP_AB_SP_D;     // stages in the ring
   constexpr int TB2 = 2 * TILE * 64;   // one 256-row operand image of a stage: 16 KiB
@@ -1923,8 +1865,12 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
     const int64_t o0 = a.off[b], k = a.off[b + 1] - o0;
     const int64_t pad = a.padfirst ? a.ns - k : 0;
     const int nrt = 2 * TILE * ((NT + 1) / 2);   // rows a super-tile reads (ns rounded up to 256)
-    for (int r = t; r < nrt; r += 64 * SPW)
-      rowtab[r] = (int32_t)(r < a.ns && sys_real(r, pad, k) ? snp_col(a.idx[o0 + r - pad], a.P) : a.P);
+    if constexpr (!DUAL) {
+      for (int r = t; r < nrt; r += 64 * SPW)
+        rowtab[r] = (int32_t)(r < a.ns && sys_real(r, pad, k) ? snp_col(a.idx[o0 + r - pad], a.P) : a.P);
+    } else {   // kernel form: the panel's own rows (past ns: any row -- those tiles are not stored)
+      for (int r = t; r < nrt; r += 64 * SPW) rowtab[r] = r < a.ns ? r : 0;
+    }
     __syncthreads();
     tab_b = b;
   };
@@ -1933,7 +1879,7 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
   int ist = 0, inst = 0;
   int ra[2], rb[2];                    // packed rows of this lane's A / B loads (h = 0, 1)
   const uint8_t* gbase = nullptr;
-  const int64_t gsr = a.gs_row;
+  const int64_t gsr = DUAL ? a.pstride / a.prow : a.gs_row;   // packed row bytes
   const int offa[2] = {16 * (pos ^ (((l >> 2) >> 2) & 3)), 16 * (pos ^ (((16 + (l >> 2)) >> 2) & 3))};
   const int offb[2] = {16 * (pos ^ (((l >> 2) >> 2) & 2)), 16 * (pos ^ (((16 + (l >> 2)) >> 2) & 2))};
   auto setup_issue = [&]() __attribute__((always_inline)) {
@@ -1941,7 +1887,7 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
     unit_tiles(iu, ib, I0, J0);
     if (ib != tab_b) load_rowtab(ib);
     inst = (cblk_tab[ib - b_first] + 3) >> 2;
-    gbase = a.ft.gpk[fold_of(a.ft, ib)];
+    gbase = DUAL ? a.panel + ib * a.pstride : a.ft.gpk[fold_of(a.ft, ib)];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = 16 * (2 * w + h) + (l >> 2);
@@ -1963,7 +1909,10 @@ __global__ __launch_bounds__(64 * SPW, 1) void k_sys_tiles_st(CholArgs a, int16_
   };
   if (u0 >= u1) return;
   const int nind = (u1 - 1) / nsu - b_first + 1;
-  if (t < nind) cblk_tab[t] = (int32_t)(a.ytp / KBLK);
+  if (t < nind) {   // kernel form: the individual's k SNPs
+    const int64_t bt = b_first + t;
+    cblk_tab[t] = (int32_t)(DUAL ? (a.off[bt + 1] - a.off[bt] + KBLK - 1) / KBLK : a.ytp / KBLK);
+  }
   __syncthreads();
   setup_issue();
   // total stages of the run (the units of one individual share its stage count)
@@ -2307,8 +2256,12 @@ hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
   const int64_t grid = sys_tiles_grid(c);
   if (grid > 0) {
     const int NS = (c.sd.NT + 1) / 2;
-    hipLaunchKernelGGL(k_sys_tiles_st, dim3((unsigned)grid), dim3(64 * SPW), 0, s, a, c.kc, NS * (NS + 1) / 2,
-                       (int)(c.B * (NS * (NS + 1) / 2)));
+    if (c.sd.form == FORM_PRIMAL)
+      hipLaunchKernelGGL(k_sys_tiles_st<false>, dim3((unsigned)grid), dim3(64 * SPW), 0, s, a, c.kc, NS * (NS + 1) / 2,
+                         (int)(c.B * (NS * (NS + 1) / 2)));
+    else
+      hipLaunchKernelGGL(k_sys_tiles_st<true>, dim3((unsigned)grid), dim3(64 * SPW), 0, s, a, c.kc, NS * (NS + 1) / 2,
+                         (int)(c.B * (NS * (NS + 1) / 2)));
     if (hipError_t e = hipGetLastError()) return e;
     a.wgt = nullptr;
     if (c.stats)
@@ -2317,7 +2270,10 @@ hipError_t launch_sys_tiles(const CholLaunch& c, hipStream_t s) {
       hipLaunchKernelGGL(k_sys_diag_counts, dim3((unsigned)(c.B * 2)), dim3(64 * STW), 0, s, a);
   } else {
     if (c.stats) return hipErrorInvalidValue;   // the per-tile kernel reads the scalars
-    hipLaunchKernelGGL(k_sys_tiles, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
+    if (c.sd.form == FORM_PRIMAL)
+      hipLaunchKernelGGL(k_sys_tiles<false>, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
+    else
+      hipLaunchKernelGGL(k_sys_tiles<true>, dim3((unsigned)(c.B * ntri)), dim3(64 * STW), 0, s, a, c.kc, ntri);
   }
   return hipGetLastError();
 }
@@ -2351,10 +2307,10 @@ hipError_t launch_diag_grm(const CholLaunch& c, hipStream_t s) {
 }
 
 // Kernel-form folds sharing one animal set: A_R A_R^T of individual b over fold 0's split rows (its
-// panel, system b), every 128 x 128 tile pair I >= J of the n_Rp rows on int8 MFMA (the off-diagonal
-// units' i8_tt8), stored both ways into a full n_Rp x n_Rp int32 matrix (FoldTab::gsh)
+// panel, system b), every 128 x 128 tile pair I >= J of the n_Rp rows on int8 MFMA from the packed
+// rows (i8_tt8_pk64), stored both ways into a full n_Rp x n_Rp int32 matrix (FoldTab::gsh)
 __global__ __launch_bounds__(OTH, 2) void k_gshare(CholArgs a, int NR) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[4 * 2 * TILE * KBLK];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * TILE * 64];
   const int64_t ntp = (int64_t)NR * (NR + 1) / 2;
   const int64_t lg = xcd_remap(blockIdx.x, gridDim.x);   // an individual's tiles on one XCD
   const int64_t b = lg / ntp;
@@ -2367,8 +2323,8 @@ __global__ __launch_bounds__(OTH, 2) void k_gshare(CholArgs a, int NR) {
   const int row = 16 * w + (l >> 2), pos = l & 3;
   const int64_t nblk = (int64_t)a.scal[b * SCAL + SC_CBLK];
   v4i cnt[8];
-  i8_tt8<4>(row_base(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
-            row_base(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, a.prow * KBLK, lds, cnt);
+  i8_tt8_pk64<4>(row_dpk(a, b, j0 + row) + 16 * (pos ^ ((row >> 2) & 3)),
+                 row_dpk(a, b, i0 + row) + 16 * (pos ^ ((row >> 2) & 2)), nblk, lds, cnt);
   const int64_t ld = a.ft.gsh_ld;
   int32_t* G = a.ft.gsh + b * ld * ld;
   const int64_t ic = i0 + 16 * w + (l & 15);

@@ -9,7 +9,7 @@
 //
 // Tiling: one 256-thread workgroup per 128x128 output tile (4 waves, 64x64 each
 // = 2x2 MFMA 32x32 blocks); K steps of 64 SNPs read from the animal-major
-// panel (one 128x64 operand tile = 8 KB contiguous).  Only the tiles the
+// panel (one 128x64 operand tile = 128 packed 16-B row blocks, unpacked into LDS).  Only the tiles the
 // Cholesky and the prediction read are computed: the TT lower triangle
 // (diagonal tiles in full) and the VT block.  Workgroups of one individual are
 // kept on one XCD (xcd_remap) so the individual's panel is re-read from L2.
@@ -17,7 +17,7 @@
 
 namespace tblup {
 
-__global__ __launch_bounds__(256) void k_grm(const int8_t* __restrict__ panel, int64_t panel_stride,
+__global__ __launch_bounds__(256) void k_grm(const uint8_t* __restrict__ panel, int64_t panel_stride, int64_t pk_row,
                                              const int64_t* __restrict__ off, const double* __restrict__ u,
                                              const double* __restrict__ scal, int64_t nT, int64_t nTp, int64_t nV,
                                              int64_t nRp, int NT, int64_t tiles_per, double* __restrict__ K) {
@@ -40,10 +40,10 @@ __global__ __launch_bounds__(256) void k_grm(const int8_t* __restrict__ panel, i
     tj = (int)(tt % NT);
   }
   const int64_t k = off[b + 1] - off[b];
-  const int8_t* pb = panel + b * panel_stride;
+  const uint8_t* pb = panel + b * panel_stride;
   v16i acc[2][2];
-  i8_tile_gemm(pb + (int64_t)ti * TILE * KBLK, pb + (int64_t)tj * TILE * KBLK, ti == tj, (k + KBLK - 1) / KBLK,
-               nRp * KBLK, lds, acc);
+  i8_tile_gemm(pb + (int64_t)ti * TILE * pk_row, pb + (int64_t)tj * TILE * pk_row, ti == tj, (k + KBLK - 1) / KBLK,
+               pk_row, lds, acc);
 
   // epilogue: exact-integer centring in fp64, padding rows/cols -> identity
   const double* sc = scal + b * SCAL;
@@ -73,11 +73,11 @@ __global__ __launch_bounds__(256) void k_grm(const int8_t* __restrict__ panel, i
   }
 }
 
-hipError_t launch_grm(const int8_t* panel, int64_t panel_stride, const int64_t* off, const double* u,
+hipError_t launch_grm(const uint8_t* panel, int64_t panel_stride, int64_t pk_row, const int64_t* off, const double* u,
                       const double* scal, const EvalDims& d, int64_t B, double* K, hipStream_t s) {
   const int64_t tiles_per = (int64_t)d.NT * (d.NT + 1) / 2 + (int64_t)(d.NR - d.NT) * d.NT;
   const int64_t nwg = tiles_per * B;
-  hipLaunchKernelGGL(k_grm, dim3((unsigned)nwg), dim3(256), 0, s, panel, panel_stride, off, u, scal, d.nT, d.nTp, d.nV,
+  hipLaunchKernelGGL(k_grm, dim3((unsigned)nwg), dim3(256), 0, s, panel, panel_stride, pk_row, off, u, scal, d.nT, d.nTp, d.nV,
                      d.nRp, d.NT, tiles_per, K);
   return hipGetLastError();
 }

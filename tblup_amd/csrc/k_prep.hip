@@ -78,20 +78,18 @@ hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, 
 }
 
 // ---------------------------------------------------------------------------
-// split build: permuted SNP-major rows [T | pad | V | pad] and train counts
+// split build: permuted 2-bit packed SNP-major rows [T | pad | V | pad] and train counts
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ g, int64_t n, int64_t P,
                                                      const int32_t* __restrict__ rowmap, int64_t nRp, int64_t nT,
                                                      const double* __restrict__ yT, const double* __restrict__ ymu,
-                                                     int nt, int8_t* __restrict__ out, uint8_t* __restrict__ opk,
+                                                     int nt, uint8_t* __restrict__ opk,
                                                      int32_t* __restrict__ csT, double* __restrict__ xty) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * 4 + w;
   if (p > P) return;
-  int8_t* orow = out + p * nRp;
   uint8_t* prow = opk + p * (nRp / 4);
   if (p == P) {   // the zero row
-    for (int64_t r = l; r < nRp; r += 64) orow[r] = 0;
     for (int64_t q = l; q < nRp / 4; q += 64) prow[q] = 0;
     return;
   }
@@ -108,11 +106,10 @@ __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ 
   const int64_t nTp = (nT + TILE - 1) / TILE * TILE;
   int s = 0;
   double dot[MAXT] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t r = l; r < nRp; r += 64) {
+  for (int64_t r = l; r < nT; r += 64) {
     const int32_t src = rowmap[r];
     const int8_t v = src >= 0 ? row[src] : (int8_t)0;
-    orow[r] = v;
-    if (r < nT) {
+    {
       s += v;
 #pragma unroll
       for (int t = 0; t < MAXT; ++t)
@@ -134,10 +131,10 @@ __global__ __launch_bounds__(256) void k_build_split(const int8_t* __restrict__ 
 }
 
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap, int64_t nRp,
-                              int64_t nT, const double* yT, const double* ymu, int nt, int8_t* geno_split,
+                              int64_t nT, const double* yT, const double* ymu, int nt,
                               uint8_t* geno_packed, int32_t* colsum_T, double* xty, hipStream_t s) {
   hipLaunchKernelGGL(k_build_split, dim3((unsigned)((P + 1 + 3) / 4)), dim3(256), 0, s, geno_sm, n, P, rowmap, nRp,
-                     nT, yT, ymu, nt, geno_split, geno_packed, colsum_T, xty);
+                     nT, yT, ymu, nt, geno_packed, colsum_T, xty);
   return hipGetLastError();
 }
 
@@ -178,17 +175,19 @@ hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B,
 }
 
 // ---------------------------------------------------------------------------
-// gather: panel[b][kb][r][64] (animal-major 64-SNP blocks) + u_r = sum m_s a_rs
+// gather: panel[b][r][pk_row] (animal rows, 2-bit packed over the selected SNPs: 16 B per 64-SNP
+// block, byte j holding SNPs 4j..4j+3 at bits 2i; SNPs past k are zero) + u_r = sum m_s a_rs
 //   grid (nRp/128, B), 128 threads; thread t owns animal row r0 + t.
-//   Each 64-SNP block: 64 gathered SNP rows x 128 animals staged in LDS
-//   (coalesced 16-B row-segment loads), then transposed by byte reads.
+//   Each 64-SNP block: 64 gathered packed SNP rows x 128 animals (32 B each) staged in LDS
+//   (16-B row-segment loads), then transposed by 2-bit reads.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __restrict__ idx,
                                                 const int64_t* __restrict__ off,
                                                 int64_t panel_stride, const int32_t* __restrict__ csA,
                                                 const double* __restrict__ scal, int64_t P, int64_t nRp,
-                                                int8_t* __restrict__ panel, double* __restrict__ u) {
-  __shared__ __attribute__((aligned(16))) int8_t tile[KBLK][GATHER_ROWS];
+                                                int64_t pk_row, uint8_t* __restrict__ panel,
+                                                double* __restrict__ u) {
+  __shared__ __attribute__((aligned(16))) uint32_t tile[KBLK][GATHER_ROWS / 16];   // 2-bit packed
   __shared__ int64_t srow[KBLK];
   __shared__ int32_t sm[KBLK];
   const int t = threadIdx.x;
@@ -196,10 +195,11 @@ __global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __res
   const int64_t r0 = (int64_t)blockIdx.x * GATHER_ROWS;
   const int64_t o0 = off[b], k = off[b + 1] - o0;
   const int mode = (int)scal[b * SCAL + SC_MODE];
-  const int8_t* __restrict__ gs = ft.gs[fold_of(ft, b)];   // the system's split (fold-fused batches)
+  // the system's split (fold-fused batches), 2-bit packed SNP rows of nRp / 4 bytes
+  const uint8_t* __restrict__ gp = ft.gpk[fold_of(ft, b)];
   const int32_t* cs = (mode == 1) ? csA : ft.csT[fold_of(ft, b)];
   const int64_t nblk = (k + KBLK - 1) / KBLK;
-  int8_t* pb = panel + b * panel_stride;
+  uint8_t* pb = panel + b * panel_stride + (r0 + t) * pk_row;
   int64_t uacc = 0;
   for (int64_t kb = 0; kb < nblk; ++kb) {
     if (t < KBLK) {
@@ -214,46 +214,42 @@ __global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __res
       }
     }
     __syncthreads();
-    // 64 rows x 128 B = 512 x 16 B chunks, 4 per thread
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = t + 128 * e, j = q >> 3, c = q & 7;
+    // 64 SNP rows x 128 animals at 2 bits = 64 x 32 B: one 16-B chunk per thread
+    {
+      const int j = t >> 1, c = t & 1;
       const int64_t p = srow[j];
       v4i v = {0, 0, 0, 0};
-      if (p >= 0) v = *reinterpret_cast<const v4i*>(gs + p * nRp + r0 + 16 * c);
-      *reinterpret_cast<v4i*>(&tile[j][16 * c]) = v;
+      if (p >= 0) v = *reinterpret_cast<const v4i*>(gp + p * (nRp / 4) + r0 / 4 + 16 * c);
+      *reinterpret_cast<v4i*>(&tile[j][4 * c]) = v;
     }
     __syncthreads();
-    v4i out[4];
+    v4i out;
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
+    for (int d = 0; d < 4; ++d) {
+      uint32_t word = 0;
 #pragma unroll
-      for (int d4 = 0; d4 < 4; ++d4) {
-        uint32_t word = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int j = q4 * 16 + d4 * 4 + e;
-          const uint32_t byte = (uint8_t)tile[j][t];
-          uacc += (int64_t)sm[j] * (int64_t)byte;
-          word |= byte << (8 * e);
-        }
-        out[q4][d4] = (int)word;
+      for (int e = 0; e < 16; ++e) {
+        const int j = d * 16 + e;
+        const uint32_t g = (tile[j][t >> 4] >> (2 * (t & 15))) & 3u;   // animal r0 + t
+        uacc += (int64_t)sm[j] * (int64_t)g;
+        word |= g << (2 * e);
       }
+      out[d] = (int)word;
     }
-    v4i* dstp = reinterpret_cast<v4i*>(pb + (kb * nRp + r0 + t) * KBLK);
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) dstp[q4] = out[q4];
+    *reinterpret_cast<v4i*>(pb + kb * 16) = out;
     __syncthreads();
   }
+  // the rest of the row's last stage: zero (the tiles' unpacked operands read whole 64-B stages)
+  for (int64_t kb = nblk; kb < (nblk + 3) / 4 * 4; ++kb) *reinterpret_cast<v4i*>(pb + kb * 16) = v4i{0, 0, 0, 0};
   u[b * nRp + r0 + t] = (double)uacc;
 }
 
 hipError_t launch_gather(const FoldTab& ft, const int64_t* idx, const int64_t* off, int64_t panel_stride, int64_t B,
-                         const int32_t* colsum_all, const double* scal, const EvalDims& d, int8_t* panel, double* u,
-                         hipStream_t s) {
+                         const int32_t* colsum_all, const double* scal, const EvalDims& d, int64_t pk_row,
+                         uint8_t* panel, double* u, hipStream_t s) {
   dim3 grid((unsigned)(d.nRp / GATHER_ROWS), (unsigned)B);
   hipLaunchKernelGGL(k_gather, grid, dim3(GATHER_ROWS), 0, s, ft, idx, off, panel_stride, colsum_all,
-                     scal, d.P, d.nRp, panel, u);
+                     scal, d.P, d.nRp, pk_row, panel, u);
   return hipGetLastError();
 }
 

@@ -1,7 +1,7 @@
 // Back substitution, prediction and fitness, one 1024-thread workgroup per individual.
 //
 //   alpha = L^{-T} z                       (z = L^{-1} rhs from k_chol_diag)
-//   dual:   EBV_V = K_VT alpha + mu, K_VT applied in factored form from the int8 panel
+//   dual:   EBV_V = K_VT alpha + mu, K_VT applied in factored form from the packed panel
 //                                          gblup: evaluator.py:284 (G[:,T] Ginv y_T, mu = 0)
 //                                          snp:   evaluator.py:314 (clf.predict, intercept mean(y_T))
 //   primal: EBV_V = (X_V - 2p) beta + mean(y_T), beta = alpha (sklearn primal Ridge coef_)
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   extern __shared__ double dyn[];  // alpha[nt][ns], e[nt][nV], then (primal) int32 rowp[ns]
   __shared__ double part[NTH / 64][2 * TILE];   // reused as [64][64]
   __shared__ double vsh[MAXT][TPAD];
-  __shared__ double wblk[KBLK];
+  __shared__ double wblk[4 * KBLK];   // kernel form: w_s of one 256-SNP stage
   __shared__ double red[4 * 16];
   const int64_t nTp = c.d.nTp, nT = c.d.nT, nV = c.d.nV, ns = c.sd.ns, prow = c.sd.prow;
   const int NT = c.sd.NT;
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
 
   if (c.skip & 4096) return;
   const double* ub = c.u + b * prow;
-  const uint32_t* pb = reinterpret_cast<const uint32_t*>(c.panel + b * c.pstride);
+  const uint8_t* pb = c.panel + b * c.pstride;   // kernel form: packed animal rows (dual_pk_row bytes)
   if (c.sd.form == FORM_PRIMAL) {
     // system row r holds selected SNP r - pad (leading padding rows: the zero split row P)
     const int64_t kk = (int64_t)sc[SC_K], o0 = c.off[b], pad = (int64_t)sc[SC_PAD];
@@ -307,8 +307,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
     }
     __syncthreads();
   }
-  const int dq = t & 15, rg = t >> 4;   // dword (4 bytes) within a 64-wide block row, row group (64)
-  double* pw = &part[0][0];             // [64 row groups][64]
+  double* pw = &part[0][0];             // kernel form: [16 waves][256]
   double fsum = 0.0;
   if (c.sd.form == FORM_PRIMAL) {
     // EBV_v = sum_J e_J[v] - (sum_J mb_J) / n_T + mu with block J's shares e_J[v] = sum_{a in J}
@@ -366,38 +365,48 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
       const double S = block_sum(s_a, red);
       const double UA = block_sum(s_ua, red);
       for (int64_t v = t; v < nV; v += NTH) e[v] = 0.0;
-      const int64_t nblk = (int64_t)sc[SC_CBLK];
-      for (int64_t kb = 0; kb < nblk; ++kb) {
-        const uint32_t* blk = pb + kb * prow * (KBLK / 4);
-        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-        for (int64_t r = rg; r < nT; r += NTH / 16) {
-          const uint32_t x = blk[r * (KBLK / 4) + dq];
+      // 256-SNP stages (64 B of each packed row): thread (rh, hq) = (t >> 5, t & 31) sums half-dword
+      // hq of its rows (SNPs 8 hq .. 8 hq + 7 of the stage, 2 bits each); a wave's two row groups by
+      // a shuffle, then the 16 waves' partials in LDS
+      const int64_t nst = ((int64_t)sc[SC_CBLK] + 3) / 4;
+      const int64_t pkr = c.pstride / prow;   // packed row bytes (dual_pk_row)
+      const int hq = t & 31, rh = t >> 5;
+      for (int64_t st = 0; st < nst; ++st) {
+        const uint8_t* sp = pb + st * 64;
+        double p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = 0.0;
+        for (int64_t r = rh; r < nT; r += NTH / 32) {
+          const uint32_t x = *reinterpret_cast<const uint16_t*>(sp + r * pkr + 2 * hq);
           const double ar = al[r];
-          p0 += (double)(x & 0xff) * ar;
-          p1 += (double)((x >> 8) & 0xff) * ar;
-          p2 += (double)((x >> 16) & 0xff) * ar;
-          p3 += (double)(x >> 24) * ar;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p[j] += (double)((x >> (2 * j)) & 3) * ar;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] += __shfl_xor(p[j], 32);
+        __syncthreads();
+        if ((t & 63) < 32) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pw[(t >> 6) * 4 * KBLK + 8 * hq + j] = p[j];
         }
         __syncthreads();
-        pw[rg * KBLK + 4 * dq + 0] = p0;
-        pw[rg * KBLK + 4 * dq + 1] = p1;
-        pw[rg * KBLK + 4 * dq + 2] = p2;
-        pw[rg * KBLK + 4 * dq + 3] = p3;
-        __syncthreads();
-        if (t < KBLK) {
+        if (t < 4 * KBLK) {
           double acc = 0.0;
-          for (int q = 0; q < NTH / 16; ++q) acc += pw[q * KBLK + t];
+          for (int q = 0; q < NTH / 64; ++q) acc += pw[q * 4 * KBLK + t];
           wblk[t] = acc;
         }
         __syncthreads();
         for (int64_t v = t; v < nV; v += NTH) {
-          const uint32_t* row = blk + (nTp + v) * (KBLK / 4);
+          const uint4* row = reinterpret_cast<const uint4*>(sp + (nTp + v) * pkr);
           double acc = 0.0;
-#pragma unroll 4
-          for (int d4 = 0; d4 < KBLK / 4; ++d4) {
-            const uint32_t x = row[d4];
-            acc += (double)(x & 0xff) * wblk[4 * d4] + (double)((x >> 8) & 0xff) * wblk[4 * d4 + 1] +
-                   (double)((x >> 16) & 0xff) * wblk[4 * d4 + 2] + (double)(x >> 24) * wblk[4 * d4 + 3];
+#pragma unroll 1
+          for (int h = 0; h < 4; ++h) {   // (not unrolled: wblk's 256 loads are not hoisted out of the v loop)
+            const uint4 q = row[h];
+            const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+#pragma unroll
+              for (int j = 0; j < 16; ++j) acc += (double)((qw[d] >> (2 * j)) & 3) * wblk[16 * (4 * h + d) + j];
           }
           e[v] += acc;
         }

@@ -4,9 +4,9 @@
 //   geno_sm   int8  [P][n]        SNP-major genotypes, built once (transpose of the .npy)
 //   colsum_all int32 [P]          per-SNP allele count over all n animals (gblup p)
 //   per split s (train T, valid V; nTp/nVp = sizes rounded up to 128):
-//     geno      int8 [P+1][nRp]   SNP-major rows permuted to [T | 0-pad | V | 0-pad], nRp = nTp+nVp;
-//                                 row P is all zero (padding rows of the primal form)
-//     gpk       uint8 [P+1][nRp/4] the same, 2-bit packed (animal 4j+i at bits 2i of byte j)
+//     gpk       uint8 [P+1][nRp/4] SNP-major rows permuted to [T | 0-pad | V | 0-pad], nRp = nTp+nVp,
+//                                 2-bit packed (animal 4j+i at bits 2i of byte j); row P is all zero
+//                                 (padding rows of the primal form)
 //     colsum_T  int32 [P]         allele counts over T (snp p)
 //     xty       f64  [nt][P]      sum_t x_tp (y_t - mean y_T): the primal right-hand side, per SNP and trait
 //     yT        f64 [nTp]         phenotypes of T (0 in padding), yV f64 [nV]
@@ -15,9 +15,8 @@
 //     kernel (dual) form   rows = train animals (ns = nTp), contraction over the k SNPs
 //     SNP (primal) form    rows = the k selected SNPs (ns = round_up(k)), contraction over
 //                          the train animals -- sklearn Ridge's own choice when k <= n_T
-//     panel  int8 [b][cblk][prow][64]  gathered genotypes: 64-wide contraction blocks of
-//                                      prow rows (dual: animals x 64 SNPs, prow = nRp;
-//                                      primal: SNPs x 64 animals, prow = ns, T then V blocks)
+//     panel  uint8 [b][nRp][dual_pk_row]  kernel form only: each system's animal rows 2-bit packed
+//                                      over its k SNPs (the primal form reads gpk rows in place)
 //     u      f64  [B][prow]            centring sums (dual: u_i = sum_s m_s a_is; primal: s_a)
 //     scal   f64  [B][16]              see SC_* below
 //     L      f64  [B][NT][NT][128^2]   Lt tiles (tile (I,J) holds L_IJ^T)
@@ -82,6 +81,10 @@ struct SysDims {
   int64_t cblk;      // contraction blocks per individual in the panel (max over the chunk)
   int pad_first = 0; // SNP form: padding rows lead (SC_PAD = ns - k; TBLUP_PAD_FIRST, default on)
 };
+// Kernel form: the gathered panel holds each system's prow (= n_Rp) animal rows 2-bit packed over its
+// selected SNPs -- byte j of a row holds SNPs 4j..4j+3 at bits 2i, the SNP-form split rows' code --
+// in whole 64-B (256-SNP) stages: bytes per row
+inline int64_t dual_pk_row(const SysDims& sd) { return (sd.cblk + 3) / 4 * 64; }
 
 typedef double v2d __attribute__((ext_vector_type(2)));
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -141,7 +144,6 @@ struct FoldTab {
   int nf;
   int share;                   // every fold's train + valid rows are one multiset (k_sys_tiles_folds)
   const uint8_t* gpk[MAXF];    // 2-bit packed split rows [P+1][nRp/4]
-  const int8_t* gs[MAXF];      // int8 split rows [P+1][nRp]
   const int32_t* csT[MAXF];    // train allele counts [P]
   const double* xty[MAXF];     // [nt][P]
   const double* yV[MAXF];      // [nt][nV]
@@ -161,7 +163,7 @@ hipError_t launch_transpose_geno(const int8_t* src, int8_t* dst, int64_t n, int6
 hipError_t launch_colsum_all(const int8_t* geno_sm, int32_t* colsum, int64_t n, int64_t P, hipStream_t s);
 hipError_t launch_build_split(const int8_t* geno_sm, int64_t n, int64_t P, const int32_t* rowmap,
                               int64_t nRp, int64_t nT, const double* yT, const double* ymu, int nt,
-                              int8_t* geno_split, uint8_t* geno_packed, int32_t* colsum_T, double* xty,
+                              uint8_t* geno_packed, int32_t* colsum_T, double* xty,
                               hipStream_t s);
 // fused offsets of F copies of a B-individual index list (sum_k indices each): out[F * B + 1]
 hipError_t launch_fold_offsets(const int64_t* off, int64_t B, int64_t F, int64_t sum_k, int64_t* out, hipStream_t s);
@@ -171,13 +173,14 @@ hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B,
                               const int32_t* colsum_all, const EvalDims& d, const SysDims& sd,
                               int branch, double h2, double* scal, double* u, double* rhs, int32_t* err,
                               hipStream_t s);
-// kernel form: each system's animal-major panel from its split's rows (ft: fold of system b)
+// kernel form: each system's 2-bit packed animal rows (dual_pk_row bytes each) from its split's rows
+// (ft: fold of system b)
 hipError_t launch_gather(const FoldTab& ft, const int64_t* idx, const int64_t* off, int64_t panel_stride, int64_t B,
-                         const int32_t* colsum_all, const double* scal, const EvalDims& d, int8_t* panel, double* u,
-                         hipStream_t s);
+                         const int32_t* colsum_all, const double* scal, const EvalDims& d, int64_t pk_row,
+                         uint8_t* panel, double* u, hipStream_t s);
 
 // ---- launchers (k_grm.hip) ----
-hipError_t launch_grm(const int8_t* panel, int64_t panel_stride, const int64_t* off, const double* u,
+hipError_t launch_grm(const uint8_t* panel, int64_t panel_stride, int64_t pk_row, const int64_t* off, const double* u,
                       const double* scal, const EvalDims& d, int64_t B, double* K, hipStream_t s);
 
 // ---- launchers (k_chol.hip, k_solve.hip) ----
@@ -206,7 +209,7 @@ struct CholLaunch {
   double* S;             // [B][2][36*256] diagonal-tile preparation, slot J&1
   double* Kd;            // [B][NT][36*256] GRM diagonal tiles K_JJ + lambda I (kernel form / no system tiles)
   const double* yT;      // split phenotypes [nt][nTp] (kernel form: one split)
-  const int8_t* panel;   // gathered genotypes
+  const uint8_t* panel;  // kernel form: the gathered 2-bit packed animal rows (dual_pk_row bytes each)
   int64_t pstride;       // panel bytes per individual
   const int64_t* off;    // [B+1] device offsets
   const int64_t* idx;    // device SNP indices of the chunk
@@ -217,11 +220,11 @@ struct CholLaunch {
   const double* scal;    // [B][SCAL]
   int skip;              // diagnostic ablation mask (env TBLUP_DBG_SKIP), 0 in production
   uint64_t* wgt;         // per-workgroup timestamp records of this launch (env TBLUP_WG_TRACE), else null
-  int16_t* kc;           // SNP form: exact off-diagonal system-tile counts from k_sys_tiles, else null
+  int16_t* kc;           // exact off-diagonal system-tile counts from k_sys_tiles (either form), else null
   double* part;          // [2][B][NT][128*128] partial sums of the next column's tiles (ahead schedule)
   double* q;             // last-term mode: [B][36*256] diagonal tile J's last SYRK term, from launch J-1
   int padskip;           // contractions over block column 0 skip the leading padding rows (SC_PAD)
-  int16_t* kd;           // SNP form with k_sys_tiles: the diagonal tiles' exact counts instead of Kd,
+  int16_t* kd;           // with k_sys_tiles: the diagonal tiles' exact counts instead of Kd,
                          // [B][NT][36 packed lower blocks][64 lanes][4] (KD_TILE int16 per tile); the
                          // consumers form K_JJ + lambda I from them (kd_block, k_chol.hip)
   int sys_st = -1;       // k_sys_tiles_st: -1 auto, 0 never, 1 whenever it applies (TBLUP_SYS_ST)
@@ -265,7 +268,7 @@ struct OffPlan {
 //   ahead: -1 auto (launch j ahead when B * (NT - 2 - j) < AHEAD_SLOTS; measured at config 2 against
 //   the classic schedule: +14% at B = 32, +2.3% at B = 128, even at 256; a whole-chunk B < 64 rule
 //   and thresholds 512 / 1024 were slower at 128), 0 never, 1 always; nrs: 0 auto (fill >= 2 units per CU
-//   slot pair), else fixed 1 / 2 / 4; dual: no k_sys_tiles counts (int8 K in-tile: nrs = 1)
+//   slot pair), else fixed 1 / 2 / 4; without k_sys_tiles counts (int8 K in-tile) nrs = 1
 constexpr int64_t AHEAD_SLOTS = 256;
 // diag_d: D-units in the diagonal launch, -1 auto (DD_MIN_B < B <= DD_MAX_B and J <= DD_MAX_J), 0 never,
 // 1 always.  Measured (config 2, A/B): pop 128 +2.4% (off-diagonal -49 us, diagonal +11 us per step);

@@ -245,18 +245,41 @@ def test_kernel_form_folds_fused(panel):
     with _env({"TBLUP_FOLD_FUSE": "0"}):
         with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
             unfused = eng.evaluate_folds(genomes, folds, 0.4)
-    # round 6: the folds' int8 counts from one shared A_R A_R^T per individual (default) or each
-    # system's own int8 tiles -- the same integers
-    with _env({"TBLUP_FOLD_GSHARE": "0"}):
-        with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
-            own = eng.evaluate_folds(genomes, folds, 0.4)
+    # round 6: the folds' counts from FP4 system tiles per fold system (default), or -- where the
+    # counts are formed in-tile (TBLUP_DUAL_ST=0) -- from one shared A_R A_R^T per individual, or
+    # each system's own int8 tiles: the same integers
+    runs = []
+    for env in ({"TBLUP_DUAL_ST": "0"}, {"TBLUP_DUAL_ST": "0", "TBLUP_FOLD_GSHARE": "0"}):
+        with _env(env):
+            with GpuBlupEngine(p["geno"], p["pheno"], device=0) as eng:
+                runs.append(eng.evaluate_folds(genomes, folds, 0.4))
     np.testing.assert_array_equal(fused, unfused)
-    np.testing.assert_array_equal(fused, own)
+    for r in runs:
+        np.testing.assert_array_equal(fused, r)
     for f in range(5):
         np.testing.assert_array_equal(fused[f], singles[f])
     for i in (0, 1):
         fo, _ = O.blup_grm_form(genomes[i], folds[2][0], folds[2][1], p["geno"], p["pheno"], 0.4)
         assert abs(fused[2][i] - fo) <= FIT_ATOL
+
+
+@pytest.mark.parametrize("ks,B", [((2500,), 64), ((300, 1700), 5), ((1150, 2100, 1000), 37), ((1000, 640), 300)])
+def test_kernel_form_sys_tiles_bit_identical(panel, ks, B):
+    """Kernel form (TBLUP_FORM=1): the system tiles' exact counts from k_sys_tiles on the gathered
+    2-bit rows -- the persistent super-tile kernel and the per-tile one -- against the in-tile int8
+    products (TBLUP_DUAL_ST=0): the same integers, so bit-identical fitness and EBVs; k from 300 to
+    2500 (not multiples of 64 / 256), runs crossing individuals; and the oracle."""
+    p = panel
+    rng = np.random.default_rng(81 + B)
+    genomes = [rng.choice(50_000, ks[i % len(ks)], replace=False) for i in range(B)]
+    ref = _run(p, genomes, {"TBLUP_FORM": "1", "TBLUP_DUAL_ST": "0"})
+    for env in ({"TBLUP_FORM": "1"}, {"TBLUP_FORM": "1", "TBLUP_SYS_ST": "1"}, {"TBLUP_FORM": "1", "TBLUP_SYS_ST": "0"}):
+        got = _run(p, genomes, env)
+        np.testing.assert_array_equal(got[0], ref[0])
+        np.testing.assert_array_equal(got[1], ref[1])
+    for i in (0, B - 1):
+        fo, _ = O.blup_grm_form(genomes[i], p["T"], p["V"], p["geno"], p["pheno"], 0.4)
+        assert abs(ref[0][i] - fo) <= FIT_ATOL
 
 
 @pytest.mark.parametrize("ks,B", [((1000,), 256), ((100, 300), 3), ((1150, 700, 1000), 37), ((1000, 640), 300)])

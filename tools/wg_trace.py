@@ -1,10 +1,10 @@
-"""Per-workgroup timeline of one config-2 evaluation step (TBLUP_WG_TRACE=1).
+"""Per-workgroup timeline of one evaluation step (config 2 unless --config) (TBLUP_WG_TRACE=1).
 
 For every Cholesky launch: makespan, workgroups by kind with their mean / max duration,
 slot utilisation (sum of workgroup time / (resident slots x makespan); the off-diagonal
 kernel fits 2 workgroups per CU, the diagonal 1), the time the first / last workgroup
 starts, and the gap to the previous launch.  Writes the raw records to an .npy for later
-analysis.   usage: python tools/wg_trace.py [out.npy] [--pop N]
+analysis.   usage: python tools/wg_trace.py [out.npy] [--pop N] [--config configN]
 """
 import os
 import sys
@@ -23,9 +23,10 @@ KIND = {1: "diag", 2: "tile", 3: "prep", 4: "kjj", 5: "sys", 6: "part", 9: "dpre
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "gpurun_out/wg_trace.npy"
     pop = int(sys.argv[sys.argv.index("--pop") + 1]) if "--pop" in sys.argv else 256
+    config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "config2"
     import torch
     from tblup_amd.engine import GpuBlupEngine, concat_genomes
-    cfg = bench.CONFIGS["config2"]
+    cfg = bench.CONFIGS[config]
     geno, pheno, T, V, genomes, _ = bench.make_workload(cfg, 1234, 0, pop)
     eng = GpuBlupEngine(geno, pheno, device=0)
     sid = eng.split_id(T, V)
