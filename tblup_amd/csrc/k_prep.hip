@@ -178,18 +178,20 @@ hipError_t launch_indiv_stats(const int64_t* idx, const int64_t* off, int64_t B,
 // gather: panel[b][r][pk_row] (animal rows, 2-bit packed over the selected SNPs: 16 B per 64-SNP
 // block, byte j holding SNPs 4j..4j+3 at bits 2i; SNPs past k are zero) + u_r = sum m_s a_rs
 //   grid (nRp/128, B), 128 threads; thread t owns animal row r0 + t.
-//   Each 64-SNP block: 64 gathered packed SNP rows x 128 animals (32 B each) staged in LDS
-//   (16-B row-segment loads), then transposed by 2-bit reads.
+//   Each 256-SNP stage: 256 gathered packed SNP rows x 128 animals (32 B each) staged in LDS
+//   (16-B row-segment loads), transposed by 2-bit reads, and stored as one 64-B piece per row.
 // ---------------------------------------------------------------------------
+constexpr int GST = 4 * KBLK;   // SNPs per gather stage (one 64-B packed row piece)
 __global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __restrict__ idx,
                                                 const int64_t* __restrict__ off,
                                                 int64_t panel_stride, const int32_t* __restrict__ csA,
                                                 const double* __restrict__ scal, int64_t P, int64_t nRp,
                                                 int64_t pk_row, uint8_t* __restrict__ panel,
                                                 double* __restrict__ u) {
-  __shared__ __attribute__((aligned(16))) uint32_t tile[KBLK][GATHER_ROWS / 16];   // 2-bit packed
-  __shared__ int64_t srow[KBLK];
-  __shared__ int32_t sm[KBLK];
+  static_assert(GATHER_ROWS == 128, "two SNP rows and four 16-B row pieces per thread and stage");
+  __shared__ __attribute__((aligned(16))) uint32_t tile[GST][GATHER_ROWS / 16];   // 2-bit packed
+  __shared__ int64_t srow[GST];
+  __shared__ int32_t sm[GST];
   const int t = threadIdx.x;
   const int64_t b = blockIdx.y;
   const int64_t r0 = (int64_t)blockIdx.x * GATHER_ROWS;
@@ -198,49 +200,54 @@ __global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __res
   // the system's split (fold-fused batches), 2-bit packed SNP rows of nRp / 4 bytes
   const uint8_t* __restrict__ gp = ft.gpk[fold_of(ft, b)];
   const int32_t* cs = (mode == 1) ? csA : ft.csT[fold_of(ft, b)];
-  const int64_t nblk = (k + KBLK - 1) / KBLK;
+  const int64_t nst = (k + GST - 1) / GST;
   uint8_t* pb = panel + b * panel_stride + (r0 + t) * pk_row;
   int64_t uacc = 0;
-  for (int64_t kb = 0; kb < nblk; ++kb) {
-    if (t < KBLK) {
-      const int64_t s = kb * KBLK + t;
+  for (int64_t st = 0; st < nst; ++st) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = t + 128 * e;
+      const int64_t s = st * GST + j;
       if (s < k) {
         const int64_t p = snp_col(idx[o0 + s], P);
-        srow[t] = p;
-        sm[t] = cs[p];
+        srow[j] = p;
+        sm[j] = cs[p];
       } else {
-        srow[t] = -1;
-        sm[t] = 0;
+        srow[j] = -1;
+        sm[j] = 0;
       }
     }
     __syncthreads();
-    // 64 SNP rows x 128 animals at 2 bits = 64 x 32 B: one 16-B chunk per thread
-    {
-      const int j = t >> 1, c = t & 1;
+    // 256 SNP rows x 128 animals at 2 bits = 256 x 32 B: four 16-B chunks per thread
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = t + 128 * e, j = q >> 1, c = q & 1;
       const int64_t p = srow[j];
       v4i v = {0, 0, 0, 0};
       if (p >= 0) v = *reinterpret_cast<const v4i*>(gp + p * (nRp / 4) + r0 / 4 + 16 * c);
       *reinterpret_cast<v4i*>(&tile[j][4 * c]) = v;
     }
     __syncthreads();
-    v4i out;
+    v4i out[4];
+    int32_t us = 0;   // <= 256 x 2 x 2n: exact in 32 bits
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
+    for (int d = 0; d < 16; ++d) {
       uint32_t word = 0;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int j = d * 16 + e;
         const uint32_t g = (tile[j][t >> 4] >> (2 * (t & 15))) & 3u;   // animal r0 + t
-        uacc += (int64_t)sm[j] * (int64_t)g;
+        us += sm[j] * (int32_t)g;
         word |= g << (2 * e);
       }
-      out[d] = (int)word;
+      out[d >> 2][d & 3] = (int)word;
     }
-    *reinterpret_cast<v4i*>(pb + kb * 16) = out;
+    uacc += us;
+    v4i* dst = reinterpret_cast<v4i*>(pb + st * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = out[q];
     __syncthreads();
   }
-  // the rest of the row's last stage: zero (the tiles' unpacked operands read whole 64-B stages)
-  for (int64_t kb = nblk; kb < (nblk + 3) / 4 * 4; ++kb) *reinterpret_cast<v4i*>(pb + kb * 16) = v4i{0, 0, 0, 0};
   u[b * nRp + r0 + t] = (double)uacc;
 }
 
