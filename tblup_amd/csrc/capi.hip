@@ -300,7 +300,7 @@ size_t chunk_bytes(const tblup_ctx* c, const EvalDims& d, const SysDims& sd, int
   add(sd.form == FORM_DUAL ? (size_t)B * sd.prow * dual_pk_row(sd) : 0);   // packed panel (dual only)
   add((size_t)B * sd.prow * 8);                                 // u
   add((size_t)B * SCAL * 8);                                    // scal
-  add((size_t)B * sd.ns * sd.ns * 8);                           // L (Lt tiles)
+  add((size_t)B * l_stride(sd.NT) * 8);                         // L (Lt tiles)
   add((size_t)B * sd.NT * NPACK * BLKD * 8);                    // Dinv (packed X)
   add((size_t)B * d.nt * sd.ns * 8);                            // z
   add((size_t)B * d.nt * sd.ns * 8);                            // w
@@ -423,7 +423,7 @@ int run_chunk(tblup_ctx* c, const Split& sp, const EvalDims& d, const SysDims& s
   uint8_t* panel = cv.take<uint8_t>((size_t)B * pstride);
   double* u = cv.take<double>((size_t)B * sd.prow);
   double* scal = cv.take<double>((size_t)B * SCAL);
-  double* L = cv.take<double>((size_t)B * sd.ns * sd.ns);
+  double* L = cv.take<double>((size_t)B * l_stride(sd.NT));
   double* Dinv = cv.take<double>((size_t)B * sd.NT * NPACK * BLKD);
   double* z = cv.take<double>((size_t)B * d.nt * sd.ns);
   double* wv = cv.take<double>((size_t)B * d.nt * sd.ns);

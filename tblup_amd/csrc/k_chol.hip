@@ -853,7 +853,7 @@ __device__ __forceinline__ void syrk_partial8(const CholArgs& a, int64_t b, int 
       kv[i] = (i < syrk_nb(w) && ((slice_mask(sl) >> i) & 1)) ? kd_load(a, b, Jt, e) : int2{0, 0};
     }
   }
-  if (!(a.skip & 2)) syrk_lower8_32(a.L + ((b * a.NT + Jt) * (int64_t)a.NT) * TT, 8 * nterm, lds, acc, sl, skip_rows(a, b));
+  if (!(a.skip & 2)) syrk_lower8_32(a.L + b * l_stride(a.NT) + (int64_t)Jt * a.NT * TT, 8 * nterm, lds, acc, sl, skip_rows(a, b));
   double* dst = a.S + (b * NSLOT + (Jt & 1)) * (int64_t)NPACK * BLKD;
   if (!a.kd) {
     store_syrk_blocks(dst, a.Kd + (b * a.NT + Jt) * (int64_t)NPACK * BLKD, acc, sl);
@@ -1002,7 +1002,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
       for (int i = 0; i < 5; ++i) acc[i] = v4d{0.0, 0.0, 0.0, 0.0};
       // waits for all its stages (and the older S loads) and ends in a barrier
       // (no padding skip here: at J = 1 only, and it keeps the peeled stage out of this kernel)
-      syrk_lower8_32(a.L + ((b * NT + J) * (int64_t)NT + L0) * TT, 8 * (J - L0), Xp, acc);
+      syrk_lower8_32(a.L + b * l_stride(NT) + ((int64_t)J * NT + L0) * TT, 8 * (J - L0), Xp, acc);
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
         const int e = syrk_e(w, i);
@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void diag_tile(const CholArgs& a, int64_t b, int J, i
     }
   }
   if (a.skip & FLAG_WRITE_LJJ) {
-    double* Ld = a.L + ((b * NT + J) * (int64_t)NT + J) * TT;
+    double* Ld = a.L + b * l_stride(NT) + ((int64_t)J * NT + J) * TT;
     for (int e = t; e < TT; e += DTHR) {
       const int rr = e >> 7, cc = e & 127;
       Ld[e] = (cc >= rr) ? Tp[pk(cc >> 4, rr >> 4) + bo(cc & 15, rr & 15)] : 0.0;
@@ -1280,7 +1280,7 @@ __device__ __forceinline__ void part_unit(const CholArgs& a, int64_t b, int I, i
   __syncthreads();
   v4d acc[NCB];
   k_acc<NCB>(a, b, I, Jt, cb0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
-  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+  const double* Lb = a.L + b * l_stride(NT);
   if (!(a.skip & 64))
     gemm1_a32<NCB>(Lb + (int64_t)Jt * NT * TT, Lb + (int64_t)I * NT * TT, J, cb0, lds, acc, skip_rows(a, b));
   double* pd = part_ptr(a, b, I, Jt);
@@ -1305,7 +1305,7 @@ __device__ __forceinline__ void tile_unit(const CholArgs& a, int64_t b, int I, i
   const int J = a.J, NT = a.NT;
   const int64_t ns = a.ns;
   const int64_t i0 = (int64_t)I * TILE, j0 = (int64_t)J * TILE;
-  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+  const double* Lb = a.L + b * l_stride(NT);
   v4d acc[8];
   int2 kcv[8];
   const bool from_part = ahead_cur || edone;
@@ -1430,7 +1430,7 @@ __device__ __forceinline__ void e_unit(const CholArgs& a, int64_t b, int I, int 
     __syncthreads();
     k_acc<8, false>(a, b, I, J, 0, kcv, reinterpret_cast<uint8_t*>(lds), uj_sh, ui_sh, acc);
   }
-  const double* Lb = a.L + b * (int64_t)NT * NT * TT;
+  const double* Lb = a.L + b * l_stride(NT);
   if (!(a.skip & 64))
     gemm1_a32<8>(Lb + (int64_t)J * NT * TT + (int64_t)ls0 * TT, Lb + (int64_t)I * NT * TT + (int64_t)ls0 * TT, 1, 0, lds,
                  acc, ls0 == 0 ? skip_rows(a, b) : 0);

@@ -242,7 +242,7 @@ __global__ __launch_bounds__(NTH) void k_solve(CholLaunch c, double* __restrict_
   int32_t* rowp = reinterpret_cast<int32_t*>(eall + nt * nV);   // [ns] primal: split row per SNP
   const int t = threadIdx.x;
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);   // the XCD that factorised it
-  const double* Lb = c.L + b * (int64_t)NT * NT * TILE * TILE;
+  const double* Lb = c.L + b * l_stride(NT);
   const double* Db = c.Dinv + b * (int64_t)NT * NPACK * BLKD;
   const double* sc = c.scal + b * SCAL;
   const double invN = sc[SC_SA], cN = sc[SC_CN], invd = sc[SC_INVD], muf = sc[SC_MUF];
@@ -567,7 +567,7 @@ __device__ __forceinline__ void chain_publish(int32_t* f, int32_t seq, int mode)
 __device__ __forceinline__ void chain_tile_load(const CholLaunch& c, int64_t b, int J, int I, int rc, int seg,
                                                 v2d (&x)[2][8]) {
   const int NT = c.sd.NT;
-  const double* tile = c.L + ((b * NT + J) * (int64_t)NT + I) * TILE * TILE + 2 * seg;
+  const double* tile = c.L + b * l_stride(NT) + ((int64_t)J * NT + I) * TILE * TILE + 2 * seg;
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -645,7 +645,7 @@ __device__ void chain_unit(const CholLaunch& c, const SolveChain& ch, int64_t b,
       }
       if (t < NTR * TILE) bsh[t / TILE][t % TILE] = cload(ch.beta + (b * NTR + t / TILE) * ns + (int64_t)K * TILE + t % TILE);
       __syncthreads();
-      const double* nxt = c.L + ((b * NT + K - 1) * (int64_t)NT + J) * TILE * TILE + 2 * seg;
+      const double* nxt = c.L + b * l_stride(NT) + ((int64_t)(K - 1) * NT + J) * TILE * TILE + 2 * seg;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         double p[NTR];

@@ -197,6 +197,15 @@ struct StatsFuse {
   double* u;             // [B][ns]
   double* rhs;           // [B][nt][ns]
 };
+// 4 KiB between individuals' Lt tiles, so the same tile of different individuals does not start on the
+// same HBM channel offset: off-diagonal -5 us at pop 128, solve -1% (A/B, profiles/r06_lpad_ab.txt;
+// 64 KiB was slower, 260 KiB even)
+#ifndef TBLUP_AB_LPAD   // A/B builds (tools/ab_build_defs.sh): doubles of padding between individuals' L
+#define TBLUP_AB_LPAD 512
+#endif
+constexpr int64_t L_PAD = TBLUP_AB_LPAD;
+// doubles from one individual's Lt tiles to the next's
+__host__ __device__ inline int64_t l_stride(int NT) { return (int64_t)NT * NT * TILE * TILE + L_PAD; }
 struct CholLaunch {
   EvalDims d;
   SysDims sd;
