@@ -208,7 +208,8 @@ int tblup_debug_grm(tblup_ctx* ctx, int split_id, const int64_t* idx, int64_t k,
 /*
  * VanRaden GRM of the selected columns over ALL animals, make_grm(data[:, idx])
  * (tblup/utils.py:7-18): G = W W^T / (2 sum p(1-p)), W = Z - 2p, p = column mean / 2.
- * Exact-integer A A^T on int8 MFMA plus the fp64 rank-1 centring (k_grm).  `G` is
+ * Exact-integer A A^T on int8 MFMA (2-bit packed rows unpacked into LDS) plus the fp64 rank-1
+ * centring (k_grm).  `G` is
  * n_animals x n_animals row-major (host).  Used by the PCA splitter
  * (pca_splitter, evaluator.py:641-663, with idx = every SNP).  Synchronous.
  */
