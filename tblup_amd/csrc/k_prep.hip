@@ -229,7 +229,7 @@ __global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __res
     }
     __syncthreads();
     v4i out[4];
-    int32_t us = 0;   // <= 256 x 2 x 2n: exact in 32 bits
+    int64_t us = 0;
 #pragma unroll
     for (int d = 0; d < 16; ++d) {
       uint32_t word = 0;
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(128) void k_gather(FoldTab ft, const int64_t* __res
       for (int e = 0; e < 16; ++e) {
         const int j = d * 16 + e;
         const uint32_t g = (tile[j][t >> 4] >> (2 * (t & 15))) & 3u;   // animal r0 + t
-        us += sm[j] * (int32_t)g;
+        us += (int64_t)(sm[j] * (int32_t)g);   // <= 4n per term
         word |= g << (2 * e);
       }
       out[d >> 2][d & 3] = (int)word;
