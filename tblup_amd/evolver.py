@@ -504,7 +504,6 @@ class _GpuDEEvolver(Evolver):
         import torch
         inds, genomes, L = members if members is not None else _members(population)
         n = len(inds)
-        dtypes = _child_dtypes(genomes, donors, strategy, mi, clip)
         t = _mark(t, "ev_donors")
         step = GpuDEStep.get(self.device)
         store = DeviceKeyStore.get(step.device)
@@ -516,6 +515,8 @@ class _GpuDEEvolver(Evolver):
                                                   self.dimensionality - 1, defer=True)
             t = _mark(t, "ev_prepare_step")
             try:
+                # the children's numpy dtypes (None: all float64), while the step runs
+                dtypes = _child_dtypes(genomes, donors, strategy, mi, clip)
                 # the population's evaluator (tblup_amd) may start evaluating the children on the GPU
                 # now, while their genomes cross to the host (BlupParallelEvaluator._speculate)
                 evaluator = getattr(population, "evaluator", None)

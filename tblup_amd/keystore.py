@@ -236,7 +236,19 @@ class DeviceKeyStore:
 
     def __init__(self, device):
         self.device = int(device)
-        self._entries = {}   # uid -> (tensor, row, weakref(genome array), length)
+        # uid -> (tensor, row, weakref(genome array), length, row address, row length): the row's
+        # device address (0 unless the tensor is a plain row-major float64 matrix) taken when the
+        # row is recorded, so the DE step's gather reads addresses instead of tensor geometry
+        self._entries = {}
+
+    @staticmethod
+    def _geo(tensor):
+        """(base address, row pitch in bytes, row length) of a plain row-major float64 (., L) device
+        matrix, else (0, 0, -1)."""
+        import torch
+        if tensor.dim() == 2 and tensor.stride(1) == 1 and tensor.dtype == torch.float64:
+            return tensor.data_ptr(), 8 * tensor.stride(0), tensor.shape[1]
+        return 0, 0, -1
 
     @staticmethod
     def _key_array(indv):
@@ -246,7 +258,9 @@ class DeviceKeyStore:
     def record_rows(self, tensor, individuals, arrays):
         """record() for a generation's children that the evolver has just bound to fresh TrackedGenome
         rows (every individual's genome IS arrays[i]): one dict update."""
-        self._entries.update({indv.uid: (tensor, i, weakref.ref(g), getattr(indv, "length", None))
+        p0, pitch, nc = self._geo(tensor)
+        self._entries.update({indv.uid: (tensor, i, weakref.ref(g), getattr(indv, "length", None),
+                                         p0 + pitch * i if p0 else 0, nc)
                               for i, (indv, g) in enumerate(zip(individuals, arrays))
                               if getattr(indv, "_genome", None) is g})
 
@@ -258,12 +272,13 @@ class DeviceKeyStore:
         Individuals that derive their internal genome (Coevolution appends its length) are not
         recorded and are read from the host."""
         ent = self._entries
+        p0, pitch, nc = self._geo(tensor)
         for i, (indv, a) in enumerate(zip(individuals, arrays)):
             g = getattr(indv, "_genome", None)
             if g is not a or g is None:
                 continue
             if type(g) is TrackedGenome and not g._stale:   # the common case, inlined
-                ent[indv.uid] = (tensor, i, weakref.ref(g), getattr(indv, "length", None))
+                ent[indv.uid] = (tensor, i, weakref.ref(g), getattr(indv, "length", None), p0 + pitch * i if p0 else 0, nc)
                 continue
             if not isinstance(g, np.ndarray):
                 continue
@@ -276,25 +291,24 @@ class DeviceKeyStore:
                 indv._genome = g
             if g._stale:
                 continue
-            self._entries[indv.uid] = (tensor, i, weakref.ref(g), getattr(indv, "length", None))
+            ent[indv.uid] = (tensor, i, weakref.ref(g), getattr(indv, "length", None), p0 + pitch * i if p0 else 0, nc)
 
     def lookup(self, indv):
         e = self._entries.get(indv.uid)
         if e is None:
             return None
-        tensor, row, ref, length = e
-        g = ref()
-        if g is None or g is not self._key_array(indv) or g._stale or getattr(indv, "length", None) != length:
+        g = e[2]()
+        if g is None or g is not self._key_array(indv) or g._stale or getattr(indv, "length", None) != e[3]:
             del self._entries[indv.uid]
             return None
-        return tensor, row
+        return e[0], e[1]
 
     def rebind(self, indv, old, new):
         """indv's genome array `old` was replaced by the equal-valued TrackedGenome `new`
         (the evolver compacting page-locked blocks): keep its device row."""
         e = self._entries.get(indv.uid)
         if e is not None and e[2]() is old and not old._stale:
-            self._entries[indv.uid] = (e[0], e[1], weakref.ref(new), e[3])
+            self._entries[indv.uid] = (e[0], e[1], weakref.ref(new)) + e[3:]
 
     def rows(self, individuals):
         """(tensor, row) per individual (None where absent): lookup() inlined over the batch."""
@@ -303,12 +317,11 @@ class DeviceKeyStore:
         for indv in individuals:
             e = ent.get(indv.uid)
             if e is not None:
-                tensor, row, ref, length = e
-                g = ref()
+                g = e[2]()
                 k = getattr(indv, "_genome", None)
                 if (g is not None and g is k and isinstance(k, np.ndarray) and not g._stale
-                        and getattr(indv, "length", None) == length):
-                    out.append((tensor, row))
+                        and getattr(indv, "length", None) == e[3]):
+                    out.append((e[0], e[1]))
                     continue
                 del ent[indv.uid]
             out.append(None)
@@ -320,8 +333,12 @@ class DeviceKeyStore:
         No copy when the individuals are exactly one recorded block in order.  copy_rows(out,
         pointers): one native gather of the recorded rows (pointer 0 = row to skip)."""
         import torch
-        hits = self.rows(individuals)
         n = len(individuals)
+        if copy_rows is not None and n:
+            out = self._gather_ptrs(individuals, L, host_rows, copy_rows)
+            if out is not False:
+                return out
+        hits = self.rows(individuals)
         if n and all(h is not None for h in hits):
             t0 = hits[0][0]
             if t0.shape == (n, L) and all(h[0] is t0 and h[1] == i for i, h in enumerate(hits)):
@@ -375,6 +392,48 @@ class DeviceKeyStore:
             di = torch.tensor(dst, device=out.device)
             si = torch.tensor(src, device=out.device)
             out.index_copy_(0, di, t.index_select(0, si))
+        if missing:
+            self._fill_missing(out, missing, host_rows)
+        return out
+
+    def _gather_ptrs(self, individuals, L, host_rows, copy_rows):
+        """gather() from the recorded row addresses in one pass (rows() inlined); False when some
+        recorded tensor is not a plain (., L) matrix (the caller's general path)."""
+        import torch
+        ent = self._entries
+        n = len(individuals)
+        ptrs = [0] * n
+        missing = []
+        t0 = None
+        block = True   # exactly rows 0 .. n-1 of one recorded (n, L) tensor, in order
+        for i, indv in enumerate(individuals):
+            e = ent.get(indv.uid)
+            if e is not None:
+                g = e[2]()
+                if (g is not None and g is getattr(indv, "_genome", None) and not g._stale
+                        and getattr(indv, "length", None) == e[3]):
+                    if not e[4] or e[5] != L:
+                        return False
+                    ptrs[i] = e[4]
+                    if block:
+                        if t0 is None:
+                            t0 = e[0]
+                        block = e[0] is t0 and e[1] == i
+                    continue
+                del ent[indv.uid]
+            missing.append(i)
+            block = False
+        if block and t0 is not None and t0.shape[0] == n:
+            return t0
+        if missing and host_rows is None:
+            return None
+        out = torch.empty((n, L), dtype=torch.float64, device="cuda:%d" % self.device)
+        if len(missing) < n:
+            if missing:   # missing slots: any recorded row, overwritten below
+                any_row = next(q for q in ptrs if q)
+                for i in missing:
+                    ptrs[i] = any_row
+            copy_rows(out, ptrs)
         if missing:
             self._fill_missing(out, missing, host_rows)
         return out
