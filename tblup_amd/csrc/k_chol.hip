@@ -1550,6 +1550,9 @@ __device__ __forceinline__ void diag_grm_tile(const CholArgs& a, int64_t b, int 
 // their own individual, as one list per individual, the launches ran 9% longer) -- each class
 // XCD-remapped so that one XCD's L2 serves an individual's Lt block rows; and, column 0 of the
 // kernel form only, the K_JJ workgroups for J >= 2 at the end.
+// NTRK: the traits the T-units' w update runs over (1, or MAXT for several traits) -- one kernel per
+// case, so the single-trait kernel's registers are allocated for its own path
+template <int NTRK>
 __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) {
   __shared__ __attribute__((aligned(16))) double lds[NPACK * BLKD];   // 72 KiB: rings, then packed X
   __shared__ __attribute__((aligned(16))) double uj_sh[2 * TILE];   // k_stage's column pairs (P_j, Q_j)
@@ -1608,8 +1611,7 @@ __global__ __launch_bounds__(OTH, 4) void k_chol_offdiag(CholArgs a, OffPlan p) 
     }
     // an E-unit of the diagonal launch summed the term L = Ls0 of the first ne tiles (I-major)
     const int ed = (int64_t)(I - a.J - 1) * a.B + b < p.ne ? 1 : 0;
-    if (a.nt == 1) tile_unit<1>(a, b, I, p.ahead_cur, ed, lds, uj_sh, ui_sh, zj_sh, tr);
-    else tile_unit<MAXT>(a, b, I, p.ahead_cur, ed, lds, uj_sh, ui_sh, zj_sh, tr);
+    tile_unit<NTRK>(a, b, I, p.ahead_cur, ed, lds, uj_sh, ui_sh, zj_sh, tr);
     tr.done(WGT_TILE, a.J, I, b);
     return;
   }
@@ -2363,7 +2365,10 @@ hipError_t launch_chol_diag(const CholLaunch& c, int J, const OffPlan& p, hipStr
 hipError_t launch_chol_offdiag(const CholLaunch& c, int J, const OffPlan& p, hipStream_t s) {
   if (p.nI <= 0) return hipSuccess;
   CholArgs a = make_args(c, J);
-  hipLaunchKernelGGL(k_chol_offdiag, dim3((unsigned)offdiag_grid(p, c.B)), dim3(OTH), 0, s, a, p);
+  if (c.d.nt == 1)
+    hipLaunchKernelGGL(k_chol_offdiag<1>, dim3((unsigned)offdiag_grid(p, c.B)), dim3(OTH), 0, s, a, p);
+  else
+    hipLaunchKernelGGL(k_chol_offdiag<MAXT>, dim3((unsigned)offdiag_grid(p, c.B)), dim3(OTH), 0, s, a, p);
   return hipGetLastError();
 }
 
